@@ -1,0 +1,215 @@
+"""Headline benchmark: GAT neighbour AGGREGATE on Reddit-shaped CSR (BASELINE.json metric).
+
+One "step" = one pass of the hot path over the whole graph: the fused
+COMP_MUL_COMP_ADD block [3, 11, 12] of GAT layer 1 (scatter C -> applyedge MUL
+-> gather ADD, reference code/interpreter.py:575-636, 764-802), i.e.
+    Y[i, :] = sum_{e -> i} alpha[e, head(c)] * X1[src(e), :]
+with N = 232,965, E = 114,615,892, F = 128 fp32 = 8 heads x 16, alpha [E, 8]
+fp32.  Inputs are synthetic (seeded lognormal-degree CSR, uniform sources,
+X ~ N(0,1), alpha = softmax over in-edges of N(0,1) logits) and resident in
+HBM before the timed region.
+
+--gpus N (launched by torch.distributed.run): edges are partitioned by source
+column ranges; each rank aggregates its shard per destination-row chunk and
+RCCL all-reduces the partial Y chunk by chunk (total work fixed: "strong").
+
+Printed JSON (rank 0): value = edges/s of the whole job; roofline = the
+aggregate kernel's algorithmic HBM bytes (548 B/edge + 520 B/node, SURVEY.md
+§8d) per launch / its HIP-event-timed duration vs 8 TB/s; cpu_baseline = the
+oracle's C restatement (OpenMP) on a bounded row sample on the host cores.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G, ops, partition  # noqa: E402
+
+N_REDDIT, E_REDDIT = 232965, 114615892
+F, HEADS = 128, 8
+PEAK_HBM_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def alg_bytes(n_rows, nnz, f=F, heads=HEADS):
+    """per edge 4 (col idx) + 4*H (alpha) + 4*F (gathered X row); per node 8 (indptr) + 4*F (Y)."""
+    return nnz * (4 + 4 * heads + 4 * f) + n_rows * (8 + 4 * f)
+
+
+def make_inputs(n, e, device, seed=0):
+    g = G.synthetic(n, e, seed=seed, device=device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(seed + 100)
+    x = torch.randn(n, F, generator=gen, device=device)
+    logits = torch.randn(g.nnz, HEADS, generator=gen, device=device)
+    # alpha = softmax over each destination's in-edges, per head (GAT ops 6-10), computed with libgta
+    ex = torch.exp(logits)
+    s = ops.gather_add(g, ex)
+    alpha = ops.apply_edge(g, "DIV", None, ex, "edge", s, "dst")
+    del logits, ex, s
+    return g, x, alpha
+
+
+def cpu_baseline(g, x, alpha, target_s=12.0):
+    """Oracle C aggregate (OpenMP) on the first rows of the same workload, ~target_s of CPU work."""
+    from oracle import cbase
+    cbase.load()
+    try:
+        cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
+    except AttributeError:
+        cores = os.cpu_count()
+    ip = g.indptr.cpu().numpy()
+    ix = g.indices.cpu().numpy()
+    xh = x.cpu().numpy()
+
+    def run(rows):
+        e1 = int(ip[rows])
+        a = alpha[:e1].cpu().numpy()
+        t0 = time.perf_counter()
+        cbase.aggregate(ip[: rows + 1], ix[:e1], xh, a, 0, rows, threads=cores)
+        return time.perf_counter() - t0, e1
+
+    rows = min(g.n_rows, 2000)
+    dt, ecount = run(rows)  # calibration
+    rate = ecount / max(dt, 1e-6)
+    want_edges = min(int(rate * target_s / 3), g.nnz)
+    rows = int(min(g.n_rows, max(1, np.searchsorted(ip, want_edges))))
+    times = []
+    for _ in range(3):
+        dt, ecount = run(rows)
+        times.append(dt)
+    best = float(np.median(times))
+    return {"value": ecount / best, "unit": "edges/s", "cores": cores, "kind": "port",
+            "sample": f"rows [0,{rows}) = {ecount} edges of the same graph/X/alpha, median of 3, "
+                      f"oracle/spmm_ref.c fp32 OpenMP"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--chunk", type=int, default=512, help="aggregate plan row-chunk (edges)")
+    ap.add_argument("--row-chunks", type=int, default=0, help="row chunks for comm overlap (0 = auto)")
+    ap.add_argument("--lpe", type=int, default=0, help="force lanes-per-edge variant (32 or 64)")
+    ap.add_argument("--n", type=int, default=N_REDDIT)
+    ap.add_argument("--e", type=int, default=E_REDDIT)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+    if args.lpe:
+        ops.set_debug("agg_lpe", args.lpe)
+
+    g, x, alpha = make_inputs(args.n, args.e, dev)
+    nnz_total = g.nnz
+    if world > 1:
+        shard = partition.make_shard(g, rank, world)
+        gl = shard.graph
+        xl = x[shard.c0:shard.c1].contiguous()
+        wl = alpha[shard.edge_ids].contiguous()
+        n_chunks = args.row_chunks or 8
+    else:
+        shard, gl, xl, wl = None, g, x, alpha
+        n_chunks = args.row_chunks or 1
+    chunked = partition.ChunkedRows(gl, n_chunks=n_chunks, chunk=args.chunk)
+    y = torch.empty(g.n_rows, F, device=dev)
+    stream = torch.cuda.current_stream(dev)
+
+    def step():
+        partition.distributed_aggregate(chunked, xl, wl, y)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # kernel-only timing (HIP events on the launch stream) for the roofline
+    n_evt = min(args.steps, 10)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_evt)]
+    for a, b in evs:
+        a.record(stream)
+        for r0, r1, gg, plan in chunked.parts:
+            ops.aggregate(gg, xl, "src", wl, out=y[r0:r1], plan=plan)
+        b.record(stream)
+    torch.cuda.synchronize()
+    kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+    # timed region: K steps, barrier + sync on both sides, max over ranks
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    ms_per_step = dt * 1e3 / args.steps
+    value = nnz_total / (ms_per_step / 1e3)
+
+    # roofline of the dominant kernel (this rank's shard)
+    ab = alg_bytes(gl.n_rows, gl.nnz)
+    achieved = ab / (kern_ms / 1e3) / 1e9
+    traffic = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(pmc_path) and world == 1:
+        try:
+            pm = json.load(open(pmc_path))
+            if pm.get("n") == args.n and pm.get("e") == args.e:
+                traffic = pm.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+
+    result = {
+        "metric": "edges/sec + achieved HBM GB/s, GAT aggregate on Reddit, 1/2/4/8 MI355X",
+        "value": value,
+        "unit": "edges/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic: seeded lognormal-degree CSR (mean deg 492), uniform sources, X~N(0,1), "
+                "alpha=per-head softmax over in-edges",
+        "config": {"workload": "GAT layer-1 aggregate block [3,11,12] (scatter C -> applyedge MUL -> gather ADD)",
+                   "graph": "reddit-shaped", "N": args.n, "E": nnz_total, "F": F, "heads": HEADS,
+                   "parallelism": f"edge-partition by source column x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
+                   "plan_chunk": args.chunk, "row_chunks": n_chunks},
+        "achieved_GBps": nnz_total and alg_bytes(g.n_rows, nnz_total) / (ms_per_step / 1e3) / 1e9,
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
+                     "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
+                     "kernel_ms": kern_ms, "alg_bytes_per_launch": ab},
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(g, x, alpha)
+    elif rank == 0:
+        result["cpu_baseline"] = None
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,80 @@
+"""ctypes binding of libgta.so (include/gta.h).
+
+The product path has no fallback: if the HIP library is missing or stale the
+import of any op raises.  Build it with `python -c "import __graft_entry__ as g; g.build()"`
+or `python -m gta_graph_tensor_acclelrator_for_general_gnn_amd._build`.
+"""
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgta.so")
+ABI_VERSION = 1
+
+# enum mirrors of include/gta.h
+GTA_F32, GTA_BF16 = 0, 1
+DIR_R, DIR_C = 0, 1
+IDX_EDGE, IDX_SRC, IDX_DST = 0, 1, 2
+BIN_NONE, BIN_ADD, BIN_MUL, BIN_DIV, BIN_SUB = 0, 1, 2, 3, 4
+SF = {"NONE": 0, "RELU": 1, "EXP_LEAKY_RELU": 2, "ELU": 3, "EXP": 4, "LEAKY_RELU": 5, "SIGMOID": 6,
+      "TANH": 7, "RECIP": 8}
+
+_i64, _i32, _vp, _cp = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p
+
+# name -> (restype, argtypes); every symbol here is declared in include/gta.h
+# except gta_debug_set (a tuning hook for bench.py)
+SIGNATURES = {
+    "gta_abi_version": (_i32, []),
+    "gta_last_error": (_cp, []),
+    "gta_scatter": (_i32, [_i32, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _i64, _vp]),
+    "gta_aggregate": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _i32,
+                             _vp, _i64, _vp, _vp]),
+    "gta_aggregate_plan_bytes": (_i64, [_i64, _i64, _i64]),
+    "gta_aggregate_plan_build": (_i32, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
+    "gta_aggregate_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
+    "gta_gather_add": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i32, _vp]),
+    "gta_apply_edge": (_i32, [_i32, _i32, _vp, _vp, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp,
+                              _i64, _vp]),
+    "gta_apply_node": (_i32, [_i32, _i32, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp]),
+    "gta_update_mm": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
+    "gta_tile_nnz": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
+    "gta_debug_set": (_i32, [_cp, _i64]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class GTAError(RuntimeError):
+    pass
+
+
+def load(path=LIB_PATH):
+    """Load libgta.so and bind every symbol; raises GTAError if anything is missing."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(path):
+            raise GTAError(f"libgta.so not found at {path}: the HIP backend is not built "
+                           "(run __graft_entry__.build()); there is no CPU fallback")
+        lib = ctypes.CDLL(path)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name, None)
+            if fn is None:
+                raise GTAError(f"libgta.so lacks symbol {name}")
+            fn.restype = res
+            fn.argtypes = args
+        v = lib.gta_abi_version()
+        if v != ABI_VERSION:
+            raise GTAError(f"libgta ABI {v} != expected {ABI_VERSION}; rebuild")
+        _lib = lib
+        return lib
+
+
+def check(rc, what):
+    if rc < 0:
+        msg = load().gta_last_error()
+        raise GTAError(f"{what} failed ({rc}): {msg.decode() if msg else ''}")
+    return rc

@@ -1,0 +1,867 @@
+// gta_kernels.hip -- hand-written CDNA4 (gfx950) kernels + the extern "C" ABI of
+// libgta (declared in include/gta.h).  Each kernel executes one ISA op / fused
+// pattern of the GTA instruction stream; see gta.h for the reference citation of
+// each entry point and DESIGN.md for the HBM layout and rooflines.
+//
+// Wave = 64 lanes.  Workgroups are 256 threads (4 waves) everywhere.
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <string>
+
+#include "../../include/gta.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define GTA_HIP(x)                                                                   \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) return fail(GTA_ERR_HIP, std::string(#x) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+#define GTA_LAUNCHED(name)                                                                      \
+  do {                                                                                          \
+    hipError_t e_ = hipGetLastError();                                                          \
+    if (e_ != hipSuccess) return fail(GTA_ERR_HIP, std::string(name) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+__host__ __device__ inline bool aligned(const void* p, int bytes) { return (reinterpret_cast<uintptr_t>(p) % bytes) == 0; }
+
+// ---------------------------------------------------------------------------
+// special functions (SF post-ops) and binary ops
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sf_apply(int sf, float v) {
+  switch (sf) {
+    case GTA_SF_NONE: return v;
+    case GTA_SF_RELU: return v > 0.f ? v : 0.f;
+    case GTA_SF_EXP_LEAKY_RELU: return expf(v > 0.f ? v : 0.2f * v);
+    case GTA_SF_ELU: return v > 0.f ? v : expm1f(v);
+    case GTA_SF_EXP: return expf(v);
+    case GTA_SF_LEAKY_RELU: return v > 0.f ? v : 0.2f * v;
+    case GTA_SF_SIGMOID: return 1.f / (1.f + expf(-v));
+    case GTA_SF_TANH: return tanhf(v);
+    case GTA_SF_RECIP: return 1.f / v;
+    default: return v;
+  }
+}
+
+__device__ __forceinline__ float bin_apply(int bin, float a, float b) {
+  switch (bin) {
+    case GTA_BIN_ADD: return a + b;
+    case GTA_BIN_MUL: return a * b;
+    case GTA_BIN_DIV: return a / b;
+    case GTA_BIN_SUB: return a - b;
+    default: return a;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// vector helpers
+// ---------------------------------------------------------------------------
+template <int VW> struct Vec;
+template <> struct Vec<1> {
+  float v[1];
+  __device__ __forceinline__ void load(const float* p) { v[0] = *p; }
+  __device__ __forceinline__ void store(float* p) const { *p = v[0]; }
+};
+template <> struct Vec<2> {
+  float v[2];
+  __device__ __forceinline__ void load(const float* p) {
+    float2 t = *reinterpret_cast<const float2*>(p);
+    v[0] = t.x; v[1] = t.y;
+  }
+  __device__ __forceinline__ void store(float* p) const { *reinterpret_cast<float2*>(p) = make_float2(v[0], v[1]); }
+};
+template <> struct Vec<4> {
+  float v[4];
+  __device__ __forceinline__ void load(const float* p) {
+    float4 t = *reinterpret_cast<const float4*>(p);
+    v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w;
+  }
+  __device__ __forceinline__ void store(float* p) const {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+};
+
+__device__ __forceinline__ int wave_id_uniform() {
+  return __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+}
+
+// ---------------------------------------------------------------------------
+// Aggregate plan (row chunks).  Layout inside the caller's plan buffer:
+//   int64 hdr[8]            : n_items, n_split, chunk, max_items, n_rows
+//   int32 item_row[max_items]
+//   int64 item_beg[max_items]
+//   int32 split_row[n_rows], int32 split_first[n_rows], int32 split_cnt[n_rows]
+//   int64 offs[n_rows]      : exclusive scan of chunks per row (scratch)
+// ---------------------------------------------------------------------------
+struct PlanView {
+  int64_t* hdr;
+  int32_t* item_row;
+  int64_t* item_beg;
+  int32_t* split_row;
+  int32_t* split_first;
+  int32_t* split_cnt;
+  int64_t* offs;
+};
+
+inline int64_t round16(int64_t b) { return (b + 15) / 16 * 16; }
+inline int64_t max_items_for(int64_t n_rows, int64_t nnz, int64_t chunk) {
+  return n_rows + (nnz + chunk - 1) / chunk;
+}
+
+PlanView plan_view(void* base, int64_t n_rows, int64_t max_items) {
+  char* p = static_cast<char*>(base);
+  PlanView v;
+  v.hdr = reinterpret_cast<int64_t*>(p); p += round16(8 * sizeof(int64_t));
+  v.item_row = reinterpret_cast<int32_t*>(p); p += round16(max_items * 4);
+  v.item_beg = reinterpret_cast<int64_t*>(p); p += round16(max_items * 8);
+  v.split_row = reinterpret_cast<int32_t*>(p); p += round16(n_rows * 4);
+  v.split_first = reinterpret_cast<int32_t*>(p); p += round16(n_rows * 4);
+  v.split_cnt = reinterpret_cast<int32_t*>(p); p += round16(n_rows * 4);
+  v.offs = reinterpret_cast<int64_t*>(p); p += round16((n_rows + 1) * 8);
+  return v;
+}
+
+int64_t plan_bytes_for(int64_t n_rows, int64_t max_items) {
+  return round16(8 * 8) + round16(max_items * 4) + round16(max_items * 8) + 3 * round16(n_rows * 4) +
+         round16((n_rows + 1) * 8);
+}
+
+__device__ __forceinline__ int64_t chunks_of(int64_t deg, int64_t chunk) {
+  return deg <= chunk ? 1 : (deg + chunk - 1) / chunk;
+}
+
+// single-workgroup exclusive scan of per-row chunk counts (plan build only)
+__global__ void __launch_bounds__(1024) k_plan_scan(const int64_t* __restrict__ indptr, int64_t n_rows, int64_t chunk,
+                                                     int64_t* __restrict__ offs, int64_t* __restrict__ hdr) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (n_rows + 1023) / 1024;
+  const int64_t b = min<int64_t>(n_rows, t * per), e = min<int64_t>(n_rows, b + per);
+  int64_t s = 0;
+  for (int64_t r = b; r < e; ++r) s += chunks_of(indptr[r + 1] - indptr[r], chunk);
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    int64_t v = (t >= off) ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += v;
+    __syncthreads();
+  }
+  int64_t run = (t == 0) ? 0 : part[t - 1];
+  for (int64_t r = b; r < e; ++r) {
+    offs[r] = run;
+    run += chunks_of(indptr[r + 1] - indptr[r], chunk);
+  }
+  if (t == 1023) {
+    hdr[0] = part[1023];  // n_items
+    hdr[1] = 0;           // n_split (filled by k_plan_fill)
+    hdr[2] = chunk;
+    hdr[3] = n_rows;
+  }
+}
+
+__global__ void k_plan_fill(const int64_t* __restrict__ indptr, int64_t n_rows, int64_t chunk, PlanView v) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  const int64_t b = indptr[r], deg = indptr[r + 1] - b;
+  const int64_t nc = chunks_of(deg, chunk), off = v.offs[r];
+  for (int64_t j = 0; j < nc; ++j) {
+    v.item_row[off + j] = static_cast<int32_t>(r);
+    v.item_beg[off + j] = b + j * chunk;
+  }
+  if (nc > 1) {  // compaction order is arbitrary; each split row's sum order is fixed
+    unsigned long long s = atomicAdd(reinterpret_cast<unsigned long long*>(&v.hdr[1]), 1ull);
+    v.split_row[s] = static_cast<int32_t>(r);
+    v.split_first[s] = static_cast<int32_t>(off);
+    v.split_cnt[s] = static_cast<int32_t>(nc);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K6/K7/K2 aggregate.
+//   One wavefront per work item (a whole row, or a <=chunk slice of a long row).
+//   LPE lanes cover one edge's feature slice (VW floats per lane per vector,
+//   NV vectors per lane); 64/LPE edges share one wave instruction.  The edge
+//   loop issues U independent row loads before consuming any (latency hiding),
+//   source indices are fetched 64 at a time with one coalesced load and
+//   broadcast by readlane (LPE==64: wave-uniform row base in SGPRs) or
+//   ds_bpermute.  Accumulation is fp32 in VGPRs, in a fixed order: results are
+//   bitwise reproducible run to run (no atomics).
+// ---------------------------------------------------------------------------
+enum { XM_IDX = 0, XM_EDGE = 1 };
+enum { WM_NONE = 0, WM_HEAD = 1, WM_FULL = 2 };
+
+template <int LPE, int VW, int NV, int XMODE, int WMODE>
+__global__ void __launch_bounds__(kBlock)
+k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
+            PlanView plan, int use_plan, int64_t chunk, int x_is_row,
+            const float* __restrict__ x, int64_t ldx, int F,
+            const float* __restrict__ w, int64_t ldw, int gsz,
+            const float* __restrict__ row_scale, float* __restrict__ y, int64_t ldy, int accumulate,
+            float* __restrict__ partial) {
+  constexpr int EPI = kWave / LPE;                 // edges per wave instruction
+  constexpr int UR = (16 / (NV * VW)) < 2 ? 2 : ((16 / (NV * VW)) > 8 ? 8 : 16 / (NV * VW));
+  constexpr int STEP = UR * EPI;                    // edges per unrolled step
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t item = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  const int64_t n_items = use_plan ? plan.hdr[0] : n_rows;
+  if (item >= n_items) return;
+
+  int64_t row, eb, ee;
+  bool split = false;
+  if (use_plan) {
+    row = plan.item_row[item];
+    eb = plan.item_beg[item];
+    const int64_t rb = indptr[row], re = indptr[row + 1];
+    ee = min(eb + chunk, re);
+    split = (re - rb) > chunk;
+  } else {
+    row = item;
+    eb = indptr[row];
+    ee = indptr[row + 1];
+  }
+  const int sub = (LPE == kWave) ? 0 : lane / LPE;
+  const int cl = (LPE == kWave) ? lane : lane % LPE;
+  const float scale = (row_scale != nullptr && !split) ? row_scale[row] : 1.f;
+
+  for (int c0 = 0; c0 < F; c0 += LPE * VW * NV) {
+    int col[NV], hcol[NV];
+    bool cval[NV];
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int c = c0 + (v * LPE + cl) * VW;
+      cval[v] = c < F;
+      col[v] = cval[v] ? c : 0;
+      hcol[v] = (WMODE == WM_HEAD) ? col[v] / gsz : 0;
+    }
+    float acc[NV][VW];
+#pragma unroll
+    for (int v = 0; v < NV; ++v)
+#pragma unroll
+      for (int k = 0; k < VW; ++k) acc[v][k] = 0.f;
+
+    for (int64_t e0 = eb; e0 < ee; e0 += kWave) {
+      const int n = static_cast<int>(min<int64_t>(kWave, ee - e0));
+      int idxv = 0;
+      if (XMODE == XM_IDX && !x_is_row) idxv = indices[e0 + min(lane, n - 1)];
+      for (int s = 0; s < n; s += STEP) {
+        Vec<VW> xv[UR][NV];
+        float wh[UR][NV];
+        Vec<VW> wf[(WMODE == WM_FULL) ? UR : 1][(WMODE == WM_FULL) ? NV : 1];
+        bool valid[UR];
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+          const int j = s + u * EPI + sub;
+          valid[u] = j < n;
+          const int jj = j < n ? j : n - 1;
+          int64_t xr;
+          if (XMODE == XM_EDGE) {
+            xr = e0 + jj;
+          } else if (x_is_row) {
+            xr = row;
+          } else if (LPE == kWave) {
+            xr = __builtin_amdgcn_readlane(idxv, jj);
+          } else {
+            xr = __shfl(idxv, jj);
+          }
+          const float* xp = x + xr * ldx;
+#pragma unroll
+          for (int v = 0; v < NV; ++v) xv[u][v].load(xp + col[v]);
+          if (WMODE == WM_HEAD) {
+            const float* wp = w + (e0 + jj) * ldw;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) wh[u][v] = wp[hcol[v]];
+          } else if (WMODE == WM_FULL) {
+            const float* wp = w + (e0 + jj) * ldw;
+#pragma unroll
+            for (int v = 0; v < NV; ++v) wf[u][v].load(wp + col[v]);
+          }
+        }
+#pragma unroll
+        for (int u = 0; u < UR; ++u) {
+#pragma unroll
+          for (int v = 0; v < NV; ++v) {
+#pragma unroll
+            for (int k = 0; k < VW; ++k) {
+              float t;
+              if (WMODE == WM_HEAD) t = wh[u][v] * xv[u][v].v[k];
+              else if (WMODE == WM_FULL) t = wf[u][v].v[k] * xv[u][v].v[k];
+              else t = xv[u][v].v[k];
+              acc[v][k] += valid[u] ? t : 0.f;
+            }
+          }
+        }
+      }
+    }
+    if (LPE < kWave) {  // fold the EPI edge slots (fixed butterfly order)
+#pragma unroll
+      for (int off = LPE; off < kWave; off <<= 1)
+#pragma unroll
+        for (int v = 0; v < NV; ++v)
+#pragma unroll
+          for (int k = 0; k < VW; ++k) acc[v][k] += __shfl_xor(acc[v][k], off);
+    }
+    if (sub == 0) {
+#pragma unroll
+      for (int v = 0; v < NV; ++v) {
+        if (!cval[v]) continue;
+        Vec<VW> o;
+        if (split) {
+#pragma unroll
+          for (int k = 0; k < VW; ++k) o.v[k] = acc[v][k];
+          o.store(partial + item * static_cast<int64_t>(F) + col[v]);
+        } else {
+          float* yp = y + row * ldy + col[v];
+          if (accumulate) {
+            Vec<VW> old;
+            old.load(yp);
+#pragma unroll
+            for (int k = 0; k < VW; ++k) o.v[k] = old.v[k] + scale * acc[v][k];
+          } else {
+#pragma unroll
+            for (int k = 0; k < VW; ++k) o.v[k] = scale * acc[v][k];
+          }
+          o.store(yp);
+        }
+      }
+    }
+  }
+}
+
+// sum the chunk partials of split rows, in chunk order
+__global__ void __launch_bounds__(kBlock)
+k_aggregate_combine(PlanView plan, int F, const float* __restrict__ row_scale, float* __restrict__ y, int64_t ldy,
+                    int accumulate, const float* __restrict__ partial) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t s = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (s >= plan.hdr[1]) return;
+  const int64_t row = plan.split_row[s];
+  const int64_t first = plan.split_first[s];
+  const int cnt = plan.split_cnt[s];
+  const float scale = row_scale ? row_scale[row] : 1.f;
+  for (int c = lane; c < F; c += kWave) {
+    float a = 0.f;
+    for (int j = 0; j < cnt; ++j) a += partial[(first + j) * F + c];
+    float* yp = y + row * ldy + c;
+    *yp = accumulate ? (*yp + scale * a) : scale * a;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K1 scatter: byte-exact row copies node -> edge, one wave per destination row
+// ---------------------------------------------------------------------------
+template <typename UNIT>
+__global__ void __launch_bounds__(kBlock)
+k_scatter(int dir, const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
+          const UNIT* __restrict__ x, int64_t ldx_u, int64_t row_u, UNIT* __restrict__ out, int64_t ldo_u) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  const int64_t eb = indptr[row], ee = indptr[row + 1];
+  const int64_t total = (ee - eb) * row_u;
+  for (int64_t t = lane; t < total; t += kWave) {
+    const int64_t el = t / row_u, c = t - el * row_u;
+    const int64_t e = eb + el;
+    const int64_t src = (dir == GTA_DIR_R) ? row : indices[e];
+    out[e * ldo_u + c] = x[src * ldx_u + c];
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K3 apply_edge / K5 apply_node: element-wise with head broadcast + SF
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t edge_row(int mode, int64_t e, int64_t row, const int32_t* indices) {
+  return mode == GTA_IDX_EDGE ? e : (mode == GTA_IDX_SRC ? static_cast<int64_t>(indices[e]) : row);
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_apply_edge(int bin, int sf, const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+             int64_t n_rows, const float* __restrict__ a, int a_mode, int64_t lda, int Fa,
+             const float* __restrict__ b, int b_mode, int64_t ldb, int Fb, float* __restrict__ out,
+             int64_t ldo, int Fo) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  const int64_t eb = indptr[row], ee = indptr[row + 1];
+  const int64_t total = (ee - eb) * Fo;
+  const int ga = Fo / Fa, gb = (b != nullptr) ? Fo / Fb : 1;
+  for (int64_t t = lane; t < total; t += kWave) {
+    const int64_t el = t / Fo;
+    const int c = static_cast<int>(t - el * Fo);
+    const int64_t e = eb + el;
+    float va = a[edge_row(a_mode, e, row, indices) * lda + c / ga];
+    if (b != nullptr) {
+      const int64_t rb = (ldb == 0) ? 0 : edge_row(b_mode, e, row, indices);
+      va = bin_apply(bin, va, b[rb * ldb + c / gb]);
+    }
+    out[e * ldo + c] = sf_apply(sf, va);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_apply_node(int bin, int sf, int64_t n, const float* __restrict__ a, int64_t lda, int Fa,
+             const float* __restrict__ b, int64_t ldb, int Fb, float* __restrict__ out, int64_t ldo, int Fo) {
+  const int64_t total = n * Fo;
+  const int ga = Fo / Fa, gb = (b != nullptr) ? Fo / Fb : 1;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    const int64_t i = t / Fo;
+    const int c = static_cast<int>(t - i * Fo);
+    float va = a[i * lda + c / ga];
+    if (b != nullptr) va = bin_apply(bin, va, b[i * ldb + c / gb]);
+    out[i * ldo + c] = sf_apply(sf, va);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// K4 UPDATE: out = sf(X[r(m)] . W), fp32 via v_mfma_f32_16x16x4_f32.
+// Block tile 64x64, BK = 16, 4 waves as 2x2, each wave 32x32 = 2x2 MFMA tiles.
+// MFMA 16x16x4 f32 maps (cdna_hip_programming.md §3): lane l holds
+//   A[i = l&15][k = l>>4], B[k = l>>4][j = l&15]; D col = l&15, row = 4*(l>>4)+r.
+// ---------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+__global__ void __launch_bounds__(kBlock)
+k_mm_f32(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
+         const float* __restrict__ w, int64_t ldw, int N, int sf, float* __restrict__ out, int64_t ldo) {
+  constexpr int BM = 64, BN = 64, BK = 16;
+  __shared__ float As[BM][BK + 1];
+  __shared__ float Bs[BK][BN + 4];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int64_t m0 = static_cast<int64_t>(blockIdx.x) * BM;
+  const int n0 = blockIdx.y * BN;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // A loader: row = t/4, k = (t%4)*4 .. +3 ; B loader: k = t/16, n = (t%16)*4 .. +3
+  const int ar = t >> 2, ak = (t & 3) * 4;
+  const int64_t am = m0 + ar;
+  const bool arow_ok = am < M;
+  const int64_t asrc = arow_ok ? (row_idx ? static_cast<int64_t>(row_idx[am]) : am) : 0;
+  const float* ap = x + asrc * ldx;
+  const int bk = t >> 4, bn = (t & 15) * 4;
+
+  for (int k0 = 0; k0 < K; k0 += BK) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = k0 + ak + q;
+      As[ar][ak + q] = (arow_ok && k < K) ? ap[k] : 0.f;
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = k0 + bk, n = n0 + bn + q;
+      Bs[bk][bn + q] = (k < K && n < N) ? w[static_cast<int64_t>(k) * ldw + n] : 0.f;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int kk = 0; kk < BK; kk += 4) {
+      float af[2], bf[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = As[wr * 32 + i * 16 + (lane & 15)][kk + (lane >> 4)];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) bf[j] = Bs[kk + (lane >> 4)][wc * 32 + j * 16 + (lane & 15)];
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(af[i], bf[j], acc[i][j], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wc * 32 + j * 16 + (lane & 15);
+        if (m < M && n < N) out[m * ldo + n] = sf_apply(sf, acc[i][j][r]);
+      }
+}
+
+// bf16 UPDATE via v_mfma_f32_16x16x32_bf16 (fp32 accumulate).  Block 64x64,
+// BK = 32.  Lane l holds A[row l&15][k = 8(l>>4)+j] and B[k = 8(l>>4)+j][col l&15],
+// j = 0..7 (cdna_hip_programming.md §3); B is staged transposed in LDS so both
+// fragments are one 16-B LDS read.
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+
+__global__ void __launch_bounds__(kBlock)
+k_mm_bf16(const uint16_t* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
+          const uint16_t* __restrict__ w, int64_t ldw, int N, int sf, float* __restrict__ out, int64_t ldo) {
+  constexpr int BM = 64, BN = 64, BK = 32, PAD = 8;
+  __shared__ __attribute__((aligned(16))) uint16_t As[BM][BK + PAD];
+  __shared__ __attribute__((aligned(16))) uint16_t Bt[BN][BK + PAD];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int wr = wv >> 1, wc = wv & 1;
+  const int64_t m0 = static_cast<int64_t>(blockIdx.x) * BM;
+  const int n0 = blockIdx.y * BN;
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int ar = t >> 2, ak = (t & 3) * 8;  // A: 64 rows x 32 k, 8 per thread
+  const int64_t am = m0 + ar;
+  const bool arow_ok = am < M;
+  const int64_t asrc = arow_ok ? (row_idx ? static_cast<int64_t>(row_idx[am]) : am) : 0;
+  const uint16_t* ap = x + asrc * ldx;
+  const bool avec = ((ldx & 7) == 0) && aligned(x, 16);
+  const int bk = t >> 3, bn = (t & 7) * 8;  // B: 32 k x 64 n, 8 per thread
+
+  for (int k0 = 0; k0 < K; k0 += BK) {
+    if (avec && arow_ok && k0 + ak + 8 <= K) {
+      *reinterpret_cast<uint4*>(&As[ar][ak]) = *reinterpret_cast<const uint4*>(ap + k0 + ak);
+    } else {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int k = k0 + ak + q;
+        As[ar][ak + q] = (arow_ok && k < K) ? ap[k] : static_cast<uint16_t>(0);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int k = k0 + bk, n = n0 + bn + q;
+      Bt[bn + q][bk] = (k < K && n < N) ? w[static_cast<int64_t>(k) * ldw + n] : static_cast<uint16_t>(0);
+    }
+    __syncthreads();
+    bf16x8 af[2], bfr[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      af[i] = *reinterpret_cast<const bf16x8*>(&As[wr * 32 + i * 16 + (lane & 15)][8 * (lane >> 4)]);
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      bfr[j] = *reinterpret_cast<const bf16x8*>(&Bt[wc * 32 + j * 16 + (lane & 15)][8 * (lane >> 4)]);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    __syncthreads();
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t m = m0 + wr * 32 + i * 16 + (lane >> 4) * 4 + r;
+        const int n = n0 + wc * 32 + j * 16 + (lane & 15);
+        if (m < M && n < N) out[m * ldo + n] = sf_apply(sf, acc[i][j][r]);
+      }
+}
+
+// ---------------------------------------------------------------------------
+// f2: tile-nnz histogram (integer atomics: result is order independent)
+// ---------------------------------------------------------------------------
+__global__ void __launch_bounds__(kBlock)
+k_tile_nnz(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
+           int64_t n_cols, int64_t T, int32_t* __restrict__ counts) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  int32_t* base = counts + (row / T) * n_cols;
+  for (int64_t e = indptr[row] + lane; e < indptr[row + 1]; e += kWave) {
+    const int32_t j = indices[e];
+    if (j != row) atomicAdd(base + j, 1);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// host-side dispatch of the aggregate template family
+// ---------------------------------------------------------------------------
+struct AggArgs {
+  const int64_t* indptr; const int32_t* indices; int64_t n_rows;
+  PlanView plan; int use_plan; int64_t chunk; int x_is_row;
+  const float* x; int64_t ldx; int F;
+  const float* w; int64_t ldw; int gsz;
+  const float* row_scale; float* y; int64_t ldy; int accumulate; float* partial;
+};
+
+template <int LPE, int VW, int NV, int XM, int WM>
+void launch_agg(const AggArgs& a, int64_t n_items_bound, hipStream_t s) {
+  const int64_t blocks = (n_items_bound + kWavesPerBlock - 1) / kWavesPerBlock;
+  k_aggregate<LPE, VW, NV, XM, WM><<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
+      a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, a.x_is_row, a.x, a.ldx, a.F, a.w, a.ldw, a.gsz,
+      a.row_scale, a.y, a.ldy, a.accumulate, a.partial);
+}
+
+template <int LPE, int VW, int NV, int XM>
+bool dispatch_w(int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
+  switch (wm) {
+    case WM_NONE: launch_agg<LPE, VW, NV, XM, WM_NONE>(a, nb, s); return true;
+    case WM_HEAD: launch_agg<LPE, VW, NV, XM, WM_HEAD>(a, nb, s); return true;
+    case WM_FULL: launch_agg<LPE, VW, NV, XM, WM_FULL>(a, nb, s); return true;
+  }
+  return false;
+}
+
+template <int LPE, int VW, int NV>
+bool dispatch_x(int xm, int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
+  return xm == XM_EDGE ? dispatch_w<LPE, VW, NV, XM_EDGE>(wm, a, nb, s) : dispatch_w<LPE, VW, NV, XM_IDX>(wm, a, nb, s);
+}
+
+template <int VW>
+bool dispatch_lpe(int lpe, int nv, int xm, int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
+  switch (lpe) {
+    case 64:
+      if (nv == 1) return dispatch_x<64, VW, 1>(xm, wm, a, nb, s);
+      if (nv == 2) return dispatch_x<64, VW, 2>(xm, wm, a, nb, s);
+      return dispatch_x<64, VW, 4>(xm, wm, a, nb, s);
+    case 32: return dispatch_x<32, VW, 1>(xm, wm, a, nb, s);
+    case 16: return dispatch_x<16, VW, 1>(xm, wm, a, nb, s);
+    case 8: return dispatch_x<8, VW, 1>(xm, wm, a, nb, s);
+    default: return dispatch_x<4, VW, 1>(xm, wm, a, nb, s);
+  }
+}
+
+int g_force_lpe = 0;  // tuning hook (gta_debug_set), 0 = automatic
+int g_force_vw = 0;
+
+}  // namespace
+
+// ===========================================================================
+// extern "C" ABI
+// ===========================================================================
+extern "C" {
+
+int gta_abi_version(void) { return GTA_ABI_VERSION; }
+const char* gta_last_error(void) { return g_err.c_str(); }
+
+// not in gta.h: benchmarking hook to pin the aggregate kernel variant
+int gta_debug_set(const char* key, int64_t value) {
+  std::string k(key ? key : "");
+  if (k == "agg_lpe") { g_force_lpe = static_cast<int>(value); return 0; }
+  if (k == "agg_vw") { g_force_vw = static_cast<int>(value); return 0; }
+  return fail(GTA_ERR_ARG, "gta_debug_set: unknown key " + k);
+}
+
+int64_t gta_aggregate_plan_bytes(int64_t n_rows, int64_t nnz, int64_t chunk) {
+  if (n_rows < 0 || nnz < 0 || chunk <= 0) return fail(GTA_ERR_ARG, "plan_bytes: bad sizes");
+  return plan_bytes_for(n_rows, max_items_for(n_rows, nnz, chunk));
+}
+
+int64_t gta_aggregate_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t chunk, int64_t F) {
+  if (n_rows < 0 || nnz < 0 || chunk <= 0 || F <= 0) return fail(GTA_ERR_ARG, "workspace_bytes: bad sizes");
+  return max_items_for(n_rows, nnz, chunk) * F * static_cast<int64_t>(sizeof(float));
+}
+
+int gta_aggregate_plan_build(const int64_t* indptr, int64_t n_rows, int64_t nnz, int64_t chunk, void* plan,
+                             int64_t plan_bytes, void* stream) {
+  if (!indptr || !plan || n_rows <= 0 || chunk <= 0 || (chunk % kWave) != 0)
+    return fail(GTA_ERR_ARG, "plan_build: need indptr, plan, n_rows > 0 and chunk a positive multiple of 64");
+  const int64_t mi = max_items_for(n_rows, nnz, chunk);
+  if (plan_bytes < plan_bytes_for(n_rows, mi)) return fail(GTA_ERR_ARG, "plan_build: plan buffer too small");
+  if (n_rows > INT32_MAX || mi > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "plan_build: > 2^31 rows/items");
+  PlanView v = plan_view(plan, n_rows, mi);
+  hipStream_t s = S(stream);
+  k_plan_scan<<<1, 1024, 0, s>>>(indptr, n_rows, chunk, v.offs, v.hdr);
+  GTA_LAUNCHED("k_plan_scan");
+  k_plan_fill<<<dim3(static_cast<unsigned>((n_rows + 255) / 256)), dim3(256), 0, s>>>(indptr, n_rows, chunk, v);
+  GTA_LAUNCHED("k_plan_fill");
+  return GTA_OK;
+}
+
+int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int x_mode,
+                     const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
+                  const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
+                  int64_t plan_chunk, void* workspace, void* stream) {
+  if (!indptr || !x || !y || n_rows < 0 || nnz < 0 || F <= 0) return fail(GTA_ERR_ARG, "aggregate: bad arguments");
+  if (x_mode != GTA_IDX_EDGE && x_mode != GTA_IDX_SRC && x_mode != GTA_IDX_DST)
+    return fail(GTA_ERR_ARG, "aggregate: bad x_mode");
+  if (x_mode == GTA_IDX_SRC && !indices) return fail(GTA_ERR_ARG, "aggregate: x_mode SRC needs indices");
+  if (F > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "aggregate: F too large");
+  if (n_rows == 0) return GTA_OK;
+  int wm = WM_NONE, gsz = 1;
+  if (w) {
+    if (heads <= 0 || F % heads != 0) return fail(GTA_ERR_ARG, "aggregate: heads must divide F");
+    wm = (heads == F) ? WM_FULL : WM_HEAD;
+    gsz = static_cast<int>(F / heads);
+  }
+  const int xm = (x_mode == GTA_IDX_EDGE) ? XM_EDGE : XM_IDX;
+  // widest vector that keeps every access aligned
+  auto ok_vw = [&](int vw) {
+    if (F % vw || ldx % vw || ldy % vw || !aligned(x, 4 * vw) || !aligned(y, 4 * vw)) return false;
+    if (wm == WM_HEAD && gsz % vw) return false;
+    if (wm == WM_FULL && (ldw % vw || !aligned(w, 4 * vw))) return false;
+    return true;
+  };
+  int vw = ok_vw(4) ? 4 : (ok_vw(2) ? 2 : 1);
+  if (g_force_vw && g_force_vw <= vw && ok_vw(g_force_vw)) vw = g_force_vw;
+  const int64_t lanes = (F + vw - 1) / vw;
+  int lpe, nv = 1;
+  if (lanes >= kWave) {
+    lpe = kWave;
+    nv = lanes >= 4 * kWave ? 4 : (lanes > kWave ? 2 : 1);
+    if (vw == 4 && F == 128 && !g_force_lpe) { vw = 2; }  // 64 lanes x float2 covers 128 exactly
+  } else {
+    lpe = 4;
+    while (lpe < lanes) lpe <<= 1;
+  }
+  if (g_force_lpe == 32 && F == 128 && ok_vw(4)) { lpe = 32; vw = 4; nv = 1; }
+  if (g_force_lpe == 64 && F == 128 && ok_vw(2)) { lpe = 64; vw = 2; nv = 1; }
+
+  AggArgs a{};
+  a.indptr = indptr; a.indices = indices; a.n_rows = n_rows;
+  a.use_plan = plan != nullptr; a.chunk = plan_chunk; a.x_is_row = (x_mode == GTA_IDX_DST);
+  a.x = x; a.ldx = ldx; a.F = static_cast<int>(F); a.w = w; a.ldw = ldw; a.gsz = gsz;
+  a.row_scale = row_scale; a.y = y; a.ldy = ldy; a.accumulate = accumulate;
+  a.partial = static_cast<float*>(workspace);
+  int64_t bound = n_rows;
+  if (plan) {
+    if (plan_chunk <= 0 || !workspace) return fail(GTA_ERR_ARG, "aggregate: plan needs chunk and workspace");
+    bound = max_items_for(n_rows, nnz, plan_chunk);
+    a.plan = plan_view(const_cast<void*>(plan), n_rows, bound);
+  }
+  hipStream_t s = S(stream);
+  bool ok = false;
+  switch (vw) {
+    case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, a, bound, s); break;
+    case 2: ok = dispatch_lpe<2>(lpe, nv, xm, wm, a, bound, s); break;
+    default: ok = dispatch_lpe<1>(lpe, nv, xm, wm, a, bound, s); break;
+  }
+  if (!ok) return fail(GTA_ERR_UNSUPPORTED, "aggregate: no kernel variant");
+  GTA_LAUNCHED("k_aggregate");
+  if (plan) {
+    const int64_t sb = (nnz + plan_chunk - 1) / plan_chunk;  // >= number of split rows
+    if (sb > 0) {
+      const int64_t blocks = (sb + kWavesPerBlock - 1) / kWavesPerBlock;
+      k_aggregate_combine<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
+          a.plan, a.F, row_scale, y, ldy, accumulate, a.partial);
+      GTA_LAUNCHED("k_aggregate_combine");
+    }
+  }
+  return GTA_OK;
+}
+
+int gta_gather_add(const int64_t* indptr, int64_t n_rows, int64_t nnz, const float* xe, int64_t ldxe, int64_t F,
+                   float* y, int64_t ldy, int accumulate, void* stream) {
+  return gta_aggregate(indptr, nullptr, n_rows, nnz, GTA_IDX_EDGE, xe, ldxe, F, nullptr, 0, 0, nullptr, y, ldy,
+                          accumulate, nullptr, 0, nullptr, stream);
+}
+
+int gta_scatter(int dir, const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, const void* x,
+                int64_t ldx, int64_t F, int dtype, void* out, int64_t ldo, void* stream) {
+  if (!indptr || !x || !out || n_rows < 0 || F <= 0) return fail(GTA_ERR_ARG, "scatter: bad arguments");
+  if (dir != GTA_DIR_R && dir != GTA_DIR_C) return fail(GTA_ERR_ARG, "scatter: bad dir");
+  if (dir == GTA_DIR_C && !indices) return fail(GTA_ERR_ARG, "scatter C needs indices");
+  const int esz = (dtype == GTA_BF16) ? 2 : (dtype == GTA_F32 ? 4 : 0);
+  if (!esz) return fail(GTA_ERR_ARG, "scatter: bad dtype");
+  if (n_rows == 0 || nnz == 0) return GTA_OK;
+  const int64_t rowb = F * esz, ldxb = ldx * esz, ldob = ldo * esz;
+  int unit = 16;
+  while (unit > 2 && (rowb % unit || ldxb % unit || ldob % unit || !aligned(x, unit) || !aligned(out, unit))) unit >>= 1;
+  const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock)), blk(kBlock);
+  hipStream_t s = S(stream);
+  switch (unit) {
+    case 16:
+      k_scatter<uint4><<<grid, blk, 0, s>>>(dir, indptr, indices, n_rows, static_cast<const uint4*>(x), ldxb / 16,
+                                            rowb / 16, static_cast<uint4*>(out), ldob / 16);
+      break;
+    case 8:
+      k_scatter<uint2><<<grid, blk, 0, s>>>(dir, indptr, indices, n_rows, static_cast<const uint2*>(x), ldxb / 8,
+                                            rowb / 8, static_cast<uint2*>(out), ldob / 8);
+      break;
+    case 4:
+      k_scatter<uint32_t><<<grid, blk, 0, s>>>(dir, indptr, indices, n_rows, static_cast<const uint32_t*>(x),
+                                               ldxb / 4, rowb / 4, static_cast<uint32_t*>(out), ldob / 4);
+      break;
+    default:
+      k_scatter<uint16_t><<<grid, blk, 0, s>>>(dir, indptr, indices, n_rows, static_cast<const uint16_t*>(x),
+                                               ldxb / 2, rowb / 2, static_cast<uint16_t*>(out), ldob / 2);
+  }
+  GTA_LAUNCHED("k_scatter");
+  return GTA_OK;
+}
+
+static int check_bcast(int64_t Fa, int64_t Fb, bool has_b, int64_t* Fo) {
+  *Fo = Fa;
+  if (!has_b) return 0;
+  *Fo = Fa > Fb ? Fa : Fb;
+  if (Fa <= 0 || Fb <= 0 || (*Fo % Fa) || (*Fo % Fb)) return -1;
+  return 0;
+}
+
+int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
+                   const float* a, int a_mode, int64_t lda, int64_t Fa, const float* b, int b_mode, int64_t ldb,
+                   int64_t Fb, float* out, int64_t ldo, void* stream) {
+  if (!indptr || !a || !out || n_rows < 0 || Fa <= 0) return fail(GTA_ERR_ARG, "apply_edge: bad arguments");
+  if ((a_mode == GTA_IDX_SRC || (b && b_mode == GTA_IDX_SRC)) && !indices)
+    return fail(GTA_ERR_ARG, "apply_edge: SRC operand needs indices");
+  int64_t Fo;
+  if (check_bcast(Fa, Fb, b != nullptr, &Fo)) return fail(GTA_ERR_ARG, "apply_edge: widths must divide");
+  if (n_rows == 0 || nnz == 0) return GTA_OK;
+  const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+  k_apply_edge<<<grid, dim3(kBlock), 0, S(stream)>>>(bin, sf, indptr, indices, n_rows, a, a_mode, lda,
+                                                     static_cast<int>(Fa), b, b_mode, ldb, static_cast<int>(Fb), out,
+                                                     ldo, static_cast<int>(Fo));
+  GTA_LAUNCHED("k_apply_edge");
+  return GTA_OK;
+}
+
+int gta_apply_node(int bin, int sf, int64_t n, const float* a, int64_t lda, int64_t Fa, const float* b, int64_t ldb,
+                   int64_t Fb, float* out, int64_t ldo, void* stream) {
+  if (!a || !out || n < 0 || Fa <= 0) return fail(GTA_ERR_ARG, "apply_node: bad arguments");
+  int64_t Fo;
+  if (check_bcast(Fa, Fb, b != nullptr, &Fo)) return fail(GTA_ERR_ARG, "apply_node: widths must divide");
+  if (n == 0) return GTA_OK;
+  const int64_t total = n * Fo;
+  const int64_t blocks = std::min<int64_t>((total + kBlock - 1) / kBlock, 256 * 16);
+  k_apply_node<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, S(stream)>>>(
+      bin, sf, n, a, lda, static_cast<int>(Fa), b, ldb, static_cast<int>(Fb), out, ldo, static_cast<int>(Fo));
+  GTA_LAUNCHED("k_apply_node");
+  return GTA_OK;
+}
+
+int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* w,
+                  int64_t ldw, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream) {
+  if (!x || !w || !out || M < 0 || K <= 0 || N <= 0) return fail(GTA_ERR_ARG, "update_mm: bad arguments");
+  if (K > INT32_MAX || N > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "update_mm: K/N too large");
+  if (M == 0) return GTA_OK;
+  const dim3 grid(static_cast<unsigned>((M + 63) / 64), static_cast<unsigned>((N + 63) / 64));
+  if (dtype == GTA_F32) {
+    k_mm_f32<<<grid, dim3(kBlock), 0, S(stream)>>>(static_cast<const float*>(x), ldx, row_idx, M,
+                                                   static_cast<int>(K), static_cast<const float*>(w), ldw,
+                                                   static_cast<int>(N), sf, out, ldo);
+  } else if (dtype == GTA_BF16) {
+    k_mm_bf16<<<grid, dim3(kBlock), 0, S(stream)>>>(static_cast<const uint16_t*>(x), ldx, row_idx, M,
+                                                    static_cast<int>(K), static_cast<const uint16_t*>(w), ldw,
+                                                    static_cast<int>(N), sf, out, ldo);
+  } else {
+    return fail(GTA_ERR_ARG, "update_mm: bad dtype");
+  }
+  GTA_LAUNCHED("k_mm");
+  return GTA_OK;
+}
+
+int gta_tile_nnz(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols, int64_t T,
+                 int32_t* counts, void* stream) {
+  if (!indptr || !indices || !counts || n_rows < 0 || n_cols <= 0 || T <= 0)
+    return fail(GTA_ERR_ARG, "tile_nnz: bad arguments");
+  if (n_rows == 0) return GTA_OK;
+  const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+  k_tile_nnz<<<grid, dim3(kBlock), 0, S(stream)>>>(indptr, indices, n_rows, n_cols, T, counts);
+  GTA_LAUNCHED("k_tile_nnz");
+  return GTA_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,161 @@
+"""CSR graph container and deterministic synthetic graph generators.
+
+Layout (the reference's row-tile axis, code/preprocessing.py:26-38): CSR sorted
+by DESTINATION row (direction R), `indices` = SOURCE column of each edge
+(direction C).  indptr int64 [N+1], indices int32 [E]; edge tensors are [E, F]
+in CSR order.  The reference holds adjacency only as a dense .npy
+(code/preprocessing.py:14) or a CSR .npz it never uses (code/simulator.py:63-73);
+this CSR is the device-resident form of the same matrix (rows = dst, cols = src).
+
+Synthetic shapes: Cora N=2708/E=10556, Flickr 89250/899756,
+Reddit 232965/114615892, ogbn-products 2449029/123718280.  Degrees are
+lognormal (sigma 1) scaled to the exact edge count; sources are uniform
+(or "locality": near the destination id).
+"""
+import math
+
+import torch
+
+SHAPES = {
+    "cora": (2708, 10556),
+    "flickr": (89250, 899756),
+    "reddit": (232965, 114615892),
+    "products": (2449029, 123718280),
+}
+
+
+class Graph:
+    """Destination-sorted CSR.  All tensors live on one device."""
+
+    def __init__(self, indptr, indices, n_cols=None):
+        if indptr.dtype != torch.int64 or indices.dtype != torch.int32:
+            raise TypeError("indptr must be int64 and indices int32")
+        if indptr.device != indices.device:
+            raise ValueError("indptr and indices on different devices")
+        self.indptr = indptr.contiguous()
+        self.indices = indices.contiguous()
+        self.n_rows = indptr.numel() - 1
+        self.n_cols = self.n_rows if n_cols is None else int(n_cols)
+        self.nnz = indices.numel()
+        self._plans = {}
+        self._row_of_edge = None
+        self._deg = None
+
+    @property
+    def device(self):
+        return self.indptr.device
+
+    def to(self, device):
+        return Graph(self.indptr.to(device), self.indices.to(device), self.n_cols)
+
+    def degrees(self):
+        if self._deg is None:
+            self._deg = (self.indptr[1:] - self.indptr[:-1])
+        return self._deg
+
+    def row_of_edge(self):
+        """int32 [E]: destination row of each edge (for scatter-R gathers in edge GEMMs)."""
+        if self._row_of_edge is None:
+            rows = torch.arange(self.n_rows, device=self.device, dtype=torch.int32)
+            self._row_of_edge = torch.repeat_interleave(rows, self.degrees())
+        return self._row_of_edge
+
+    def plan(self, chunk=512):
+        """Cached device-side aggregate plan (row chunks of <= chunk edges)."""
+        if chunk not in self._plans:
+            from . import ops
+            self._plans[chunk] = ops.AggregatePlan(self, chunk)
+        return self._plans[chunk]
+
+    def numpy(self):
+        return self.indptr.cpu().numpy(), self.indices.cpu().numpy()
+
+    def __repr__(self):
+        return f"Graph(N={self.n_rows}, E={self.nnz}, device={self.device})"
+
+
+def from_numpy(indptr, indices, device="cpu", n_cols=None):
+    return Graph(torch.as_tensor(indptr, dtype=torch.int64).to(device),
+                 torch.as_tensor(indices, dtype=torch.int32).to(device), n_cols)
+
+
+def lognormal_degrees(n, e, seed=0, sigma=1.0, device="cpu"):
+    """Per-row degrees ~ lognormal(sigma), scaled so that sum == e exactly."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    z = torch.randn(n, generator=g, device=device, dtype=torch.float64)
+    raw = torch.exp(sigma * z)
+    scaled = raw * (e / raw.sum())
+    deg = torch.floor(scaled).to(torch.int64)
+    rem = int(e - int(deg.sum().item()))
+    if rem > 0:  # hand the remainder to the rows with the largest fractional parts
+        frac = scaled - deg.to(torch.float64)
+        top = torch.topk(frac, rem).indices
+        deg[top] += 1
+    return deg
+
+
+def synthetic(n, e, seed=0, kind="lognormal", sigma=1.0, device="cpu", sort_cols=True, dedupe=False,
+              locality_width=None):
+    """Deterministic synthetic CSR of n nodes / ~e edges.
+
+    kind: "lognormal" (degree skew, Reddit-like) or "uniform" (equal degrees).
+    locality_width: None = uniform random sources; else sources within +-width of the row.
+    dedupe: drop duplicate (dst, src) pairs and self loops (then nnz <= e).
+    """
+    device = torch.device(device)
+    if kind == "uniform":
+        deg = torch.full((n,), e // n, dtype=torch.int64, device=device)
+        deg[: e - int(deg.sum())] += 1
+    elif kind == "lognormal":
+        deg = lognormal_degrees(n, e, seed=seed, sigma=sigma, device=device)
+    else:
+        raise ValueError(kind)
+    g = torch.Generator(device=device)
+    g.manual_seed(seed + 1)
+    rows = torch.repeat_interleave(torch.arange(n, device=device, dtype=torch.int64), deg)
+    if locality_width is None:
+        cols = torch.randint(0, n, (e,), generator=g, device=device, dtype=torch.int64)
+    else:
+        off = torch.randint(-locality_width, locality_width + 1, (e,), generator=g, device=device,
+                            dtype=torch.int64)
+        cols = torch.remainder(rows + off, n)
+    if dedupe:
+        keep = cols != rows
+        rows, cols = rows[keep], cols[keep]
+    if sort_cols or dedupe:
+        key = rows * n + cols
+        key = torch.unique(key) if dedupe else torch.sort(key).values
+        rows = torch.div(key, n, rounding_mode="floor")
+        cols = key - rows * n
+        del key
+    counts = torch.bincount(rows, minlength=n)
+    indptr = torch.zeros(n + 1, dtype=torch.int64, device=device)
+    indptr[1:] = torch.cumsum(counts, 0)
+    return Graph(indptr, cols.to(torch.int32))
+
+
+def dataset_graph(name, seed=0, device="cpu", **kw):
+    n, e = SHAPES[name]
+    return synthetic(n, e, seed=seed, device=device, **kw)
+
+
+def gcn_norm_weights(graph):
+    """w_e = 1/sqrt(d_dst * d_src) (GCN edge weight); degrees = in-degree, min 1."""
+    deg = graph.degrees().to(torch.float32).clamp_min(1.0)
+    dst = graph.row_of_edge().long()
+    src = graph.indices.long()
+    return (deg[dst] * deg[src]).rsqrt()
+
+
+def mean_weights(graph):
+    """SAGE-mean row scale 1/deg(i) (0-degree rows scale by 1)."""
+    return 1.0 / graph.degrees().to(torch.float32).clamp_min(1.0)
+
+
+def ceil_div(a, b):
+    return -(-a // b)
+
+
+def tiles(n_rows, T):
+    return math.ceil(n_rows / T)

@@ -1,0 +1,261 @@
+"""ISA ops on device tensors -> libgta (include/gta.h).  No CPU fallback.
+
+One function per ISA op / fused pattern of the GTA stream:
+  scatter      ISA `scatter`  (template/ISA_defination.yaml:33-44)        -> gta_scatter
+  gather_add   ISA `gather`   (template/ISA_defination.yaml:46-61)        -> gta_gather_add
+  aggregate    fused applyedge MUL -> gather ADD (+ removed scatter FETCH)
+               (hardware_info.yaml Inst_fused :35-38, code/interpreter.py:575-636, 764-802) -> gta_aggregate
+  apply_edge   applyedge ADD/MUL/SF (genGraphOP.py:36, 55-60)              -> gta_apply_edge
+  apply_node   applynode ADD/MUL/SF (genGraphOP.py:62, 94-95, 103-108)     -> gta_apply_node
+  update_mm    applynode/applyedge MM, `j,ij->i` (ISA_defination.yaml:1-31) -> gta_update_mm
+  tile_nnz     calculate_sparsity (code/preprocessing.py:12-40)            -> gta_tile_nnz
+Shapes and strides are validated on the host before any launch.
+"""
+import torch
+
+from . import _lib
+from ._lib import check
+
+_MODES = {"edge": _lib.IDX_EDGE, "src": _lib.IDX_SRC, "dst": _lib.IDX_DST}
+_BINS = {None: _lib.BIN_NONE, "NONE": _lib.BIN_NONE, "ADD": _lib.BIN_ADD, "MUL": _lib.BIN_MUL,
+         "DIV": _lib.BIN_DIV, "SUB": _lib.BIN_SUB}
+
+
+def _L():
+    return _lib.load()
+
+
+def _stream(dev):
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _need_gpu(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise _lib.GTAError("libgta ops take device (HIP) tensors; got a CPU tensor -- there is no CPU path")
+
+
+def _rows(t, name, dtype=torch.float32):
+    if t.dtype != dtype:
+        raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
+    if t.dim() != 2 or t.stride(1) != 1 or t.stride(0) < t.shape[1]:
+        raise ValueError(f"{name}: need a row-major 2-D tensor with unit column stride")
+    return t.stride(0)
+
+
+def _sf(sf):
+    if sf is None:
+        return 0
+    if isinstance(sf, int):
+        return sf
+    return _lib.SF[sf.upper()]
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+class AggregatePlan:
+    """Device plan that splits rows longer than `chunk` edges over several wavefronts."""
+
+    def __init__(self, graph, chunk=512):
+        _need_gpu(graph.indptr)
+        if chunk <= 0 or chunk % 64:
+            raise ValueError("chunk must be a positive multiple of 64")
+        L = _L()
+        self.graph, self.chunk = graph, int(chunk)
+        nbytes = check(L.gta_aggregate_plan_bytes(graph.n_rows, graph.nnz, self.chunk), "plan_bytes")
+        self.buf = torch.empty(int(nbytes), dtype=torch.uint8, device=graph.device)
+        check(L.gta_aggregate_plan_build(_ptr(graph.indptr), graph.n_rows, graph.nnz, self.chunk,
+                                         _ptr(self.buf), int(nbytes), _stream(graph.device)), "plan_build")
+        self._ws = {}
+
+    def workspace(self, F):
+        if F not in self._ws:
+            L = _L()
+            nb = check(L.gta_aggregate_workspace_bytes(self.graph.n_rows, self.graph.nnz, self.chunk, F),
+                       "workspace_bytes")
+            self._ws[F] = torch.empty(int(nb), dtype=torch.uint8, device=self.graph.device)
+        return self._ws[F]
+
+    def n_items(self):
+        return int(self.buf[:8].view(torch.int64).item())
+
+    def n_split(self):
+        return int(self.buf[8:16].view(torch.int64).item())
+
+
+def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumulate=False, plan=None):
+    """y[i] (+)= row_scale[i] * sum_{e in row i} w(e) * x[idx(e)]  (K6/K7/K2).
+
+    x_mode: "src" (x is [N_src, F], fused scatter C), "dst" (fused scatter R),
+            "edge" (x is an edge tensor [E, F]).
+    w: None, or [E, H] with H | F (H == F: full-width edge weights).
+    plan: None (one wavefront per row), an AggregatePlan, or an int chunk (cached plan).
+    """
+    _need_gpu(x, w, row_scale, out, graph.indptr)
+    F = x.shape[1]
+    ldx = _rows(x, "x")
+    if x_mode == "edge" and x.shape[0] < graph.nnz:
+        raise ValueError("edge-mode x must have E rows")
+    if x_mode == "src" and x.shape[0] < graph.n_cols:
+        raise ValueError("src-mode x must have n_cols rows")
+    if x_mode == "dst" and x.shape[0] < graph.n_rows:
+        raise ValueError("dst-mode x must have n_rows rows")
+    ldw, heads = 0, 0
+    if w is not None:
+        if w.dim() == 1:
+            w = w.view(-1, 1)
+        ldw = _rows(w, "w")
+        heads = w.shape[1]
+        if w.shape[0] < graph.nnz or F % heads:
+            raise ValueError(f"w must be [E, H] with H | F (got {tuple(w.shape)}, F={F})")
+    if row_scale is not None and (row_scale.dtype != torch.float32 or row_scale.numel() < graph.n_rows
+                                  or not row_scale.is_contiguous()):
+        raise ValueError("row_scale must be contiguous float32 [N]")
+    if out is None:
+        out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=x.device)
+    ldy = _rows(out, "out")
+    if out.shape[0] < graph.n_rows or out.shape[1] != F:
+        raise ValueError("out must be [N, F]")
+    if isinstance(plan, int):
+        plan = graph.plan(plan)
+    pbuf = ws = None
+    chunk = 0
+    if plan is not None:
+        if plan.graph is not graph:
+            raise ValueError("plan built for another graph")
+        pbuf, ws, chunk = plan.buf, plan.workspace(F), plan.chunk
+    check(_L().gta_aggregate(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz, _MODES[x_mode],
+                             _ptr(x), ldx, F, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy,
+                             int(bool(accumulate)), _ptr(pbuf), chunk, _ptr(ws), _stream(x.device)), "aggregate")
+    return out
+
+
+def gather_add(graph, xe, out=None, accumulate=False):
+    """y[i] (+)= sum_{e in row i} xe[e]   (gather R, ADD)."""
+    _need_gpu(xe, out, graph.indptr)
+    ldx = _rows(xe, "xe")
+    F = xe.shape[1]
+    if xe.shape[0] < graph.nnz:
+        raise ValueError("xe must be [E, F]")
+    if out is None:
+        out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=xe.device)
+    ldy = _rows(out, "out")
+    check(_L().gta_gather_add(_ptr(graph.indptr), graph.n_rows, graph.nnz, _ptr(xe), ldx, F, _ptr(out), ldy,
+                              int(bool(accumulate)), _stream(xe.device)), "gather_add")
+    return out
+
+
+def scatter(graph, x, direction, out=None):
+    """out[e] = x[dst(e)] (direction "R") or x[src(e)] (direction "C"); bit-exact copy."""
+    _need_gpu(x, out, graph.indptr)
+    if x.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError("scatter supports float32 / bfloat16")
+    ldx = _rows(x, "x", x.dtype)
+    F = x.shape[1]
+    d = {"R": _lib.DIR_R, "C": _lib.DIR_C}[direction]
+    need = graph.n_rows if d == _lib.DIR_R else graph.n_cols
+    if x.shape[0] < need:
+        raise ValueError(f"scatter {direction}: x has {x.shape[0]} rows < {need}")
+    if out is None:
+        out = torch.empty(graph.nnz, F, dtype=x.dtype, device=x.device)
+    ldo = _rows(out, "out", x.dtype)
+    dt = _lib.GTA_F32 if x.dtype == torch.float32 else _lib.GTA_BF16
+    check(_L().gta_scatter(d, _ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz, _ptr(x), ldx, F, dt,
+                           _ptr(out), ldo, _stream(x.device)), "scatter")
+    return out
+
+
+def _out_width(Fa, Fb):
+    if Fb is None:
+        return Fa
+    Fo = max(Fa, Fb)
+    if Fo % Fa or Fo % Fb:
+        raise ValueError(f"operand widths {Fa} and {Fb} do not broadcast")
+    return Fo
+
+
+def apply_edge(graph, bin, sf, a, a_mode="edge", b=None, b_mode="edge", out=None, b_broadcast_row=False):
+    """out[e] = sf(a[ia(e)] bin b[ib(e)]) with head broadcast of the narrower operand."""
+    _need_gpu(a, b, out, graph.indptr)
+    lda = _rows(a, "a")
+    ldb = _rows(b, "b") if b is not None else 0
+    if b_broadcast_row:
+        ldb = 0
+    Fo = _out_width(a.shape[1], None if b is None else b.shape[1])
+    if out is None:
+        out = torch.empty(graph.nnz, Fo, dtype=torch.float32, device=a.device)
+    ldo = _rows(out, "out")
+    if out.shape[1] != Fo:
+        raise ValueError("out width mismatch")
+    for t, m, name in ((a, a_mode, "a"), (b, b_mode, "b")):
+        if t is None or (name == "b" and b_broadcast_row):
+            continue
+        need = {"edge": graph.nnz, "src": graph.n_cols, "dst": graph.n_rows}[m]
+        if t.shape[0] < need:
+            raise ValueError(f"apply_edge {name}: {m}-mode operand needs {need} rows")
+    check(_L().gta_apply_edge(_BINS[bin], _sf(sf), _ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz,
+                              _ptr(a), _MODES[a_mode], lda, a.shape[1], _ptr(b), _MODES[b_mode], ldb,
+                              0 if b is None else b.shape[1], _ptr(out), ldo, _stream(a.device)), "apply_edge")
+    return out
+
+
+def apply_node(bin, sf, a, b=None, out=None, b_broadcast_row=False):
+    """out[i] = sf(a[i] bin b[i]); b_broadcast_row: b is a single row for all i (e.g. (1+eps))."""
+    _need_gpu(a, b, out)
+    lda = _rows(a, "a")
+    ldb = _rows(b, "b") if b is not None else 0
+    if b is not None and not b_broadcast_row and b.shape[0] < a.shape[0]:
+        raise ValueError("apply_node: b has fewer rows than a")
+    if b_broadcast_row:
+        ldb = 0
+    n = a.shape[0]
+    Fo = _out_width(a.shape[1], None if b is None else b.shape[1])
+    if out is None:
+        out = torch.empty(n, Fo, dtype=torch.float32, device=a.device)
+    ldo = _rows(out, "out")
+    check(_L().gta_apply_node(_BINS[bin], _sf(sf), n, _ptr(a), lda, a.shape[1], _ptr(b), ldb,
+                              0 if b is None else b.shape[1], _ptr(out), ldo, _stream(a.device)), "apply_node")
+    return out
+
+
+def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
+    """out[m] = sf(x[r(m)] . w); x, w both float32 or both bfloat16; out float32.
+
+    row_idx: None (r(m) = m, M = x.shape[0]) or int32 [M] of x rows (gather-GEMM)."""
+    _need_gpu(x, w, row_idx, out)
+    if x.dtype != w.dtype or x.dtype not in (torch.float32, torch.bfloat16):
+        raise TypeError("update_mm: x and w must both be float32 or both bfloat16")
+    ldx = _rows(x, "x", x.dtype)
+    ldw = _rows(w, "w", w.dtype)
+    K, N = w.shape
+    if x.shape[1] != K:
+        raise ValueError(f"update_mm: x width {x.shape[1]} != W rows {K}")
+    if row_idx is not None:
+        if row_idx.dtype != torch.int32 or not row_idx.is_contiguous():
+            raise TypeError("row_idx must be contiguous int32")
+        M = row_idx.numel() if m is None else m
+    else:
+        M = x.shape[0] if m is None else m
+    if out is None:
+        out = torch.empty(M, N, dtype=torch.float32, device=x.device)
+    ldo = _rows(out, "out")
+    dt = _lib.GTA_F32 if x.dtype == torch.float32 else _lib.GTA_BF16
+    check(_L().gta_update_mm(_ptr(x), ldx, _ptr(row_idx), M, K, _ptr(w), ldw, N, dt, _sf(sf), _ptr(out), ldo,
+                             _stream(x.device)), "update_mm")
+    return out
+
+
+def tile_nnz(graph, T):
+    """int32 [ceil(N/T), n_cols]: edges per (T-row tile, source column), self loops excluded."""
+    _need_gpu(graph.indptr)
+    nt = -(-graph.n_rows // T)
+    counts = torch.zeros(nt, graph.n_cols, dtype=torch.int32, device=graph.device)
+    check(_L().gta_tile_nnz(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols, T, _ptr(counts),
+                            _stream(graph.device)), "tile_nnz")
+    return counts
+
+
+def set_debug(key, value):
+    check(_L().gta_debug_set(key.encode(), int(value)), "debug_set")

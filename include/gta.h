@@ -1,0 +1,161 @@
+/*
+ * gta.h -- C ABI of libgta, the MI355X (gfx950) execution backend for GTA's
+ * message-passing ISA.
+ *
+ * The reference has no native code: its "execution" of an instruction stream
+ * is the Python cycle model `simulate(tile_size_list, dataset, network, layer,
+ * isReorder, isSinput) -> (cycles, rw)` (reference code/simulator.py:370-502),
+ * fed by the stream that `interpret()` writes (code/interpreter.py:805-849).
+ * Every entry point below executes, on real tensors, one ISA op or one fused
+ * pattern of that stream; the Python executor
+ * (gta_graph_tensor_acclelrator_for_general_gnn_amd/executor.py) walks the
+ * stream block by block and calls them.  Each function cites the reference
+ * construct whose semantics it executes.
+ *
+ * Conventions
+ *  - Plain pointers and sizes only; all pointers are DEVICE pointers owned by
+ *    the caller.  The library allocates nothing; plan/workspace sizes are
+ *    queried with the *_bytes functions.
+ *  - Graph = CSR sorted by DESTINATION row ("R" direction, the reference's
+ *    row tile axis, code/preprocessing.py:26-38): int64 indptr[n_rows+1],
+ *    int32 indices[nnz] = SOURCE column of each edge ("C" direction).
+ *    Edge e of row i is the e-th entry of the CSR; edge tensors are [nnz, F]
+ *    in CSR order.
+ *  - Dense tensors are row-major with a leading dimension (elements).
+ *  - Every call is asynchronous and stream-ordered on `stream` (a hipStream_t
+ *    passed as void*; NULL = the default stream).  No host globals besides the
+ *    thread-local error string: calls are reentrant per stream.
+ *  - Return 0 on success, <0 on error; gta_last_error() gives the message of
+ *    the calling thread's last failure.
+ */
+#ifndef GTA_H_
+#define GTA_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GTA_ABI_VERSION 1
+
+/* status codes */
+enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
+
+/* dtypes */
+enum { GTA_F32 = 0, GTA_BF16 = 1 };
+
+/* Scatter direction (reference ISA `scatter` DIRECTION dst/src,
+ * template/ISA_defination.yaml:33-44; op ORDER R/C in the op YAML). */
+enum { GTA_DIR_R = 0, /* edge takes its DESTINATION row's feature */
+       GTA_DIR_C = 1  /* edge takes its SOURCE column's feature   */ };
+
+/* How an edge-indexed operand addresses its rows. */
+enum { GTA_IDX_EDGE = 0, /* row e of an edge tensor [nnz, F]            */
+       GTA_IDX_SRC = 1,  /* row indices[e] of a node tensor (scatter C) */
+       GTA_IDX_DST = 2   /* row i (edge's destination) (scatter R)      */ };
+
+/* Binary element-wise compute types of applyedge/applynode (COMP_TYPE in the
+ * op YAML, vTCAD/GraphOP/genGraphOP.py:4-25).  DIV is the "/" of
+ * template/GAT_op.png op 9 (typed MUL in the YAML). */
+enum { GTA_BIN_NONE = 0, GTA_BIN_ADD = 1, GTA_BIN_MUL = 2, GTA_BIN_DIV = 3, GTA_BIN_SUB = 4 };
+
+/* Special functions (COMP_TYPE "SF", unit SF_ALU, code/interpreter.py:7).
+ * The reference never fixes which function an SF is; these are the build's
+ * choices, applied as a post-op of the producing kernel. */
+enum { GTA_SF_NONE = 0, GTA_SF_RELU = 1, GTA_SF_EXP_LEAKY_RELU = 2 /* exp(leaky_relu(x,0.2)) */,
+       GTA_SF_ELU = 3, GTA_SF_EXP = 4, GTA_SF_LEAKY_RELU = 5, GTA_SF_SIGMOID = 6,
+       GTA_SF_TANH = 7, GTA_SF_RECIP = 8 };
+
+int gta_abi_version(void);
+const char* gta_last_error(void);
+
+/* ---- K1 SCATTER (node -> edge copy) -------------------------------------
+ * out[e, :] = x[dir==R ? dst(e) : src(e), :]          (bit-exact copy)
+ * Reference: ISA `scatter` template/ISA_defination.yaml:33-44; lowered as
+ * LOAD_N + FETCH + STORE_E, code/interpreter.py:49-53, 62-68, 367-372. */
+int gta_scatter(int dir, const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
+                const void* x, int64_t ldx, int64_t F, int dtype, void* out, int64_t ldo, void* stream);
+
+/* ---- K6/K7/K2 AGGREGATE (fused applyedge MUL -> gather ADD) -------------
+ *   y[i, c] (+)= row_scale[i] * sum_{e in row i} w(e, c) * x[idx(e), c]
+ * x_mode = GTA_IDX_SRC: the fused scatter-C FETCH (weighted/unweighted SpMM,
+ *          COMP_MUL_COMP_ADD of block [3,11,12] in GAT, [0,1,2] in GCN/SAGE/GIN);
+ *          GTA_IDX_EDGE: a plain gather ADD of an edge tensor (K2);
+ *          GTA_IDX_DST : the fused scatter-R FETCH.
+ * w: NULL (unweighted, pattern [scatter,gather] (NONE,ADD)) or [nnz, ldw]
+ *    with `heads` columns: column c uses w[e, c / (F/heads)]  (heads | F;
+ *    heads == F is a full-width edge tensor, heads == 1 a scalar edge weight).
+ * row_scale: NULL or float[n_rows] (e.g. 1/deg for SAGE-mean).
+ * plan: NULL (one wavefront per row) or a plan built by
+ *       gta_aggregate_plan_build with the same graph and plan_chunk; rows
+ *       longer than plan_chunk are split over several wavefronts whose
+ *       partials are summed in a fixed order (deterministic; no atomics).
+ * workspace: >= gta_aggregate_workspace_bytes(...) when plan != NULL.
+ * Reference: hardware_info.yaml Inst_fused [applyedge,gather] [MUL,ADD]
+ * ("FinalVersion For Paper/hardware_info.yaml":35-38), inst_fusion_x2
+ * code/interpreter.py:575-636, fuse_fetch :764-802; gather ISA
+ * template/ISA_defination.yaml:46-61. */
+int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
+                  int x_mode, const float* x, int64_t ldx, int64_t F,
+                  const float* w, int64_t ldw, int64_t heads,
+                  const float* row_scale, float* y, int64_t ldy, int accumulate,
+                  const void* plan, int64_t plan_chunk, void* workspace, void* stream);
+
+/* plan/workspace sizing: chunk must be a positive multiple of 64 */
+int64_t gta_aggregate_plan_bytes(int64_t n_rows, int64_t nnz, int64_t chunk);
+int gta_aggregate_plan_build(const int64_t* indptr, int64_t n_rows, int64_t nnz, int64_t chunk,
+                             void* plan, int64_t plan_bytes, void* stream);
+int64_t gta_aggregate_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t chunk, int64_t F);
+
+/* ---- K2 GATHER ADD (edge -> node) ---------------------------------------
+ * y[i, :] (+)= sum_{e in row i} xe[e, :]    == gta_aggregate(x_mode=EDGE, w=NULL)
+ * Reference: gather ISA template/ISA_defination.yaml:46-61; LOAD_E + Virtual
+ * LOAD_N + COMP_ADD + STORE_N, code/interpreter.py:329-334, 373-375. */
+int gta_gather_add(const int64_t* indptr, int64_t n_rows, int64_t nnz, const float* xe, int64_t ldxe,
+                   int64_t F, float* y, int64_t ldy, int accumulate, void* stream);
+
+/* ---- K3 APPLYEDGE element-wise -----------------------------------------
+ * out[e, c] = sf( a[ia(e), c_a] (bin) b[ib(e), c_b] )   for c < max(Fa, Fb)
+ * ia/ib per GTA_IDX_*; the narrower operand is broadcast in contiguous
+ * groups (head broadcast: c_b = c / (Fa/Fb)).  b may be NULL (bin ignored).
+ * ldb == 0 broadcasts one row of b to every edge.
+ * Reference: applyedge ops of vTCAD/GraphOP/genGraphOP.py:36, 55-60, 113-118. */
+int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
+                   const float* a, int a_mode, int64_t lda, int64_t Fa,
+                   const float* b, int b_mode, int64_t ldb, int64_t Fb,
+                   float* out, int64_t ldo, void* stream);
+
+/* ---- K5 APPLYNODE element-wise -----------------------------------------
+ * out[i, c] = sf( a[i, c_a] (bin) b[i, c_b] ), same broadcast rules, ldb == 0
+ * broadcasts one row (e.g. the (1+eps) scalar of GIN op 3).
+ * Reference: applynode ops genGraphOP.py:62, 94-95, 103-108. */
+int gta_apply_node(int bin, int sf, int64_t n, const float* a, int64_t lda, int64_t Fa,
+                   const float* b, int64_t ldb, int64_t Fb, float* out, int64_t ldo, void* stream);
+
+/* ---- K4 UPDATE / MVM on MFMA (applynode MM, applyedge MM) -------------
+ * out[m, :] = sf( x[r(m), :] . W )   x: [*, K] (dtype), W: [K, N] row-major
+ * (dtype), out: [M, N] fp32.  row_idx NULL => r(m) = m, else r(m) =
+ * row_idx[m] (the fused [scatter, applyedge] (NONE,MM) gather-GEMM).
+ * fp32 runs on v_mfma_f32_16x16x4_f32 (exact f32), bf16 on
+ * v_mfma_f32_16x16x32_bf16 with fp32 accumulation.
+ * Reference: applynode ISA `j,ij->i` template/ISA_defination.yaml:1-31;
+ * LOAD_W + COMP_MM code/interpreter.py:335-343. */
+int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K,
+                  const void* w, int64_t ldw, int64_t N, int dtype, int sf,
+                  float* out, int64_t ldo, void* stream);
+
+/* ---- f2 TILE-NNZ metadata ----------------------------------------------
+ * counts[t, j] = #{ e : dst(e) in [t*T, (t+1)*T), src(e) == j, dst(e) != j }
+ * for t < ceil(n_rows/T), j < n_cols (int32 [ceil(n_rows/T), n_cols]).
+ * Every CSR entry counts, so a duplicate-free CSR gives the dense
+ * count_nonzero of the reference; the caller zeroes counts first.
+ * Reference: calculate_sparsity code/preprocessing.py:12-40 (dense
+ * count_nonzero per T x 1 block after removing self loops). */
+int gta_tile_nnz(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
+                 int64_t T, int32_t* counts, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GTA_H_ */

@@ -1,0 +1,37 @@
+#!/bin/bash
+# One gpurun call: GPU parity tests -> bench -> rocprofv3 kernel trace.
+# Every GPU step has its own time limit; any fault/abort/timeout ends the script.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+STEPS=${STEPS:-"tests bench prof"}
+stop_if_fatal() {  # $1 = rc, $2 = step name; test failures (rc 1) are not fatal
+  if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then echo "FATAL rc=$1 in $2; stopping"; exit "$1"; fi
+}
+for s in $STEPS; do
+  case $s in
+    tests)
+      timeout -k 10 ${T_TESTS:-700} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+      rc=$?; echo "pytest_gpu rc=$rc"; tail -5 gpurun_out/pytest_gpu.log; stop_if_fatal $rc tests ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+      rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log; stop_if_fatal $rc smoke ;;
+    bench)
+      timeout -k 10 ${T_BENCH:-600} python bench.py ${BENCH_ARGS} > gpurun_out/bench.log 2>&1
+      rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log; stop_if_fatal $rc bench ;;
+    prof)
+      export TMPDIR=/tmp
+      timeout -k 10 ${T_PROF:-600} rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
+        -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/prof.log 2>&1
+      rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.log; stop_if_fatal $rc prof ;;
+    pmc)
+      export TMPDIR=/tmp
+      timeout -k 10 ${T_PROF:-600} rocprofv3 --kernel-trace --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch -o run \
+        -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/pmc_fetch.log 2>&1
+      rc=$?; echo "pmc fetch rc=$rc"; stop_if_fatal $rc pmc
+      timeout -k 10 ${T_PROF:-600} rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run \
+        -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/pmc_write.log 2>&1
+      rc=$?; echo "pmc write rc=$rc"; stop_if_fatal $rc pmc ;;
+    *) echo "unknown step $s";;
+  esac
+done
+echo "gpu_round done"

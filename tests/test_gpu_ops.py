@@ -1,0 +1,211 @@
+"""GPU parity of every libgta kernel against the fp64 oracle (oracle/isa_ref.py).
+
+Tolerances (written here):
+  scatter / tile_nnz              bit-exact
+  aggregate / gather / edge ops   |d| <= 1e-5 * sum|terms| + 1e-6   (fp32 accumulation)
+  fp32 MFMA UPDATE                |d| <= 1e-5 * sum|x||w| + 1e-6
+  bf16 MFMA UPDATE                vs fp64 of the bf16-rounded inputs, |d| <= 1e-5 * sum|x||w| + 1e-6
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G, ops
+from oracle import isa_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _graph(n, e, seed=0, kind="lognormal", heavy_row=None, empty_rows=0, dev=None):
+    g = G.synthetic(n, e, seed=seed, kind=kind)
+    ip, ix = g.numpy()
+    if heavy_row is not None or empty_rows:
+        rng = np.random.default_rng(seed)
+        deg = np.diff(ip).copy()
+        if empty_rows:
+            deg[rng.choice(n, empty_rows, replace=False)] = 0
+        if heavy_row is not None:
+            deg[n // 2] = heavy_row
+        ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+        ix = rng.integers(0, n, int(ip[-1])).astype(np.int32)
+    gd = G.from_numpy(ip, ix, device=dev)
+    return gd, ip, ix
+
+
+def _check(got, ref, scale, what):
+    got = got.detach().cpu().numpy().astype(np.float64)
+    err = np.abs(got - ref)
+    bound = 1e-5 * scale + 1e-6
+    bad = err > bound
+    assert not bad.any(), f"{what}: {bad.sum()} elements out of tolerance, max err {err.max():.3e}"
+
+
+CASES = [  # (n, e, F, heads)
+    (300, 4000, 128, 8),     # metric shape (8 heads x 16)
+    (300, 4000, 128, 16),    # genGraphOP GAT layer-1 alpha width 16
+    (300, 4000, 128, 1),     # scalar edge weight (GCN)
+    (300, 4000, 128, 128),   # full-width edge tensor
+    (257, 3000, 602, 1),     # Reddit feature width, SAGE original order
+    (200, 2500, 1433, 1),    # Cora feature width (odd)
+    (300, 4000, 16, 16),     # GAT edge-softmax width
+    (300, 4000, 64, 4),
+    (300, 4000, 3, 1),
+    (300, 4000, 100, 4),     # products width
+]
+
+
+@pytest.mark.parametrize("n,e,F,heads", CASES)
+@pytest.mark.parametrize("plan", [None, 64])
+def test_aggregate_src_weighted(dev, n, e, F, heads, plan):
+    g, ip, ix = _graph(n, e, seed=F + heads, heavy_row=700, empty_rows=5, dev=dev)
+    rng = np.random.default_rng(1)
+    x = rng.standard_normal((n, F)).astype(np.float32)
+    w = rng.random((g.nnz, heads)).astype(np.float32)
+    y = ops.aggregate(g, torch.from_numpy(x).to(dev), "src", torch.from_numpy(w).to(dev), plan=plan)
+    ref = isa_ref.aggregate(ip, ix, x, "src", w)
+    _check(y, ref, isa_ref.aggregate_abs(ip, ix, x, "src", w), f"aggregate F={F} H={heads} plan={plan}")
+
+
+@pytest.mark.parametrize("F", [1, 16, 128, 602])
+@pytest.mark.parametrize("plan", [None, 128])
+def test_aggregate_unweighted_rowscale_accumulate(dev, F, plan):
+    n, e = 400, 6000
+    g, ip, ix = _graph(n, e, seed=11, heavy_row=1000, empty_rows=3, dev=dev)
+    rng = np.random.default_rng(2)
+    x = rng.standard_normal((n, F)).astype(np.float32)
+    y0 = rng.standard_normal((n, F)).astype(np.float32)
+    scale = (1.0 / np.maximum(np.diff(ip), 1)).astype(np.float32)
+    yd = torch.from_numpy(y0).to(dev)
+    ops.aggregate(g, torch.from_numpy(x).to(dev), "src", None, row_scale=torch.from_numpy(scale).to(dev), out=yd,
+                  accumulate=True, plan=plan)
+    ref = y0 + isa_ref.aggregate(ip, ix, x, "src", None, scale)
+    _check(yd, ref, isa_ref.aggregate_abs(ip, ix, x, "src", None, scale) + np.abs(y0), "aggregate acc")
+
+
+@pytest.mark.parametrize("F", [16, 128, 5])
+def test_gather_add_and_edge_mode(dev, F):
+    n, e = 300, 5000
+    g, ip, ix = _graph(n, e, seed=3, empty_rows=4, dev=dev)
+    rng = np.random.default_rng(4)
+    xe = rng.standard_normal((g.nnz, F)).astype(np.float32)
+    y = ops.gather_add(g, torch.from_numpy(xe).to(dev))
+    ref = isa_ref.gather_add(ip, xe)
+    _check(y, ref, isa_ref.gather_add(ip, np.abs(xe)), "gather_add")
+    w = rng.random((g.nnz, F)).astype(np.float32)
+    y2 = ops.aggregate(g, torch.from_numpy(xe).to(dev), "edge", torch.from_numpy(w).to(dev), plan=64)
+    _check(y2, isa_ref.aggregate(ip, ix, xe, "edge", w), isa_ref.aggregate_abs(ip, ix, xe, "edge", w), "edge-mode")
+
+
+def test_aggregate_dst_mode(dev):
+    n, e, F = 200, 3000, 32
+    g, ip, ix = _graph(n, e, seed=7, dev=dev)
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((n, F)).astype(np.float32)
+    w = rng.random((g.nnz, 4)).astype(np.float32)
+    y = ops.aggregate(g, torch.from_numpy(x).to(dev), "dst", torch.from_numpy(w).to(dev))
+    _check(y, isa_ref.aggregate(ip, ix, x, "dst", w), isa_ref.aggregate_abs(ip, ix, x, "dst", w), "dst-mode")
+
+
+def test_aggregate_deterministic(dev):
+    g, ip, ix = _graph(2000, 60000, seed=9, heavy_row=5000, dev=dev)
+    x = torch.randn(2000, 128, device=dev)
+    w = torch.rand(g.nnz, 8, device=dev)
+    a = ops.aggregate(g, x, "src", w, plan=256)
+    b = ops.aggregate(g, x, "src", w, plan=256)
+    assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("F", [1, 3, 16, 128, 602])
+@pytest.mark.parametrize("direction", ["R", "C"])
+def test_scatter_bit_exact(dev, dtype, F, direction):
+    n, e = 300, 4000
+    g, ip, ix = _graph(n, e, seed=F, empty_rows=3, dev=dev)
+    x = torch.randn(n, F, device=dev).to(dtype)
+    out = ops.scatter(g, x, direction)
+    ref = isa_ref.scatter(ip, ix, x.float().cpu().numpy(), direction)
+    assert torch.equal(out.float().cpu(), torch.from_numpy(ref).float())
+
+
+@pytest.mark.parametrize("bin_kind,sf,a_mode,b_mode,Fa,Fb", [
+    ("ADD", "EXP_LEAKY_RELU", "dst", "src", 16, 16),   # GAT ops 4-7 fused: exp(lrelu(eL[dst] + eR[src]))
+    ("DIV", None, "edge", "dst", 16, 16),              # GAT op 9 with op 10 (scatter R of the sums)
+    ("MUL", None, "src", "edge", 128, 16),             # GAT op 11 (alpha head broadcast)
+    ("MUL", None, "src", "edge", 602, 1),              # GCN/SAGE/GIN op 1 with a scalar edge weight
+    ("ADD", "RELU", "edge", "edge", 7, 7),
+    (None, "ELU", "edge", None, 12, None),
+])
+def test_apply_edge(dev, bin_kind, sf, a_mode, b_mode, Fa, Fb):
+    n, e = 250, 3000
+    g, ip, ix = _graph(n, e, seed=Fa, empty_rows=3, dev=dev)
+    rng = np.random.default_rng(6)
+    rows = {"edge": g.nnz, "src": n, "dst": n}
+    a = rng.standard_normal((rows[a_mode], Fa)).astype(np.float32)
+    b = None if Fb is None else (rng.random((rows[b_mode], Fb)) + 0.5).astype(np.float32)
+    out = ops.apply_edge(g, bin_kind, sf, torch.from_numpy(a).to(dev), a_mode,
+                         None if b is None else torch.from_numpy(b).to(dev), b_mode or "edge")
+    ref = isa_ref.apply_edge(ip, ix, bin_kind, sf, a, a_mode, b, b_mode or "edge")
+    got = out.cpu().numpy().astype(np.float64)
+    assert np.allclose(got, ref, rtol=2e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("bin_kind,sf,Fa,Fb,bcast", [
+    ("ADD", None, 128, 128, False), ("MUL", None, 602, 1, True), ("DIV", "ELU", 128, 16, False),
+    (None, "RELU", 64, None, False), ("ADD", "SIGMOID", 10, 10, False), (None, "TANH", 3, None, False),
+])
+def test_apply_node(dev, bin_kind, sf, Fa, Fb, bcast):
+    rng = np.random.default_rng(7)
+    n = 777
+    a = rng.standard_normal((n, Fa)).astype(np.float32)
+    b = None if Fb is None else (rng.random((1 if bcast else n, Fb)) + 0.5).astype(np.float32)
+    out = ops.apply_node(bin_kind, sf, torch.from_numpy(a).to(dev), None if b is None else torch.from_numpy(b).to(dev),
+                         b_broadcast_row=bcast)
+    ref = isa_ref.apply_node(bin_kind, sf, a, b, b_broadcast_row=bcast)
+    assert np.allclose(out.cpu().numpy(), ref, rtol=2e-6, atol=1e-6)
+
+
+@pytest.mark.parametrize("M,K,N", [(2708, 1433, 128), (1000, 602, 128), (777, 128, 16), (64, 64, 64),
+                                   (5, 3, 7), (3000, 100, 128), (513, 130, 65)])
+@pytest.mark.parametrize("gathered", [False, True])
+def test_update_mm_f32(dev, M, K, N, gathered):
+    rng = np.random.default_rng(M + K)
+    x = rng.standard_normal((M + 10, K)).astype(np.float32)
+    w = rng.standard_normal((K, N)).astype(np.float32)
+    idx = rng.integers(0, M + 10, M).astype(np.int32) if gathered else None
+    out = ops.update_mm(torch.from_numpy(x).to(dev), torch.from_numpy(w).to(dev),
+                        None if idx is None else torch.from_numpy(idx).to(dev), m=None if gathered else M)
+    ref = isa_ref.mm(x, w, idx) if gathered else isa_ref.mm(x[:M], w)
+    scale = (np.abs(x[idx] if gathered else x[:M]).astype(np.float64) @ np.abs(w).astype(np.float64))
+    _check(out, ref, scale, "update_mm f32")
+
+
+@pytest.mark.parametrize("M,K,N", [(2449, 100, 128), (1000, 128, 128), (333, 37, 50), (64, 256, 64)])
+def test_update_mm_bf16(dev, M, K, N):
+    rng = np.random.default_rng(K)
+    x = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32)).to(torch.bfloat16)
+    w = torch.from_numpy(rng.standard_normal((K, N)).astype(np.float32)).to(torch.bfloat16)
+    out = ops.update_mm(x.to(dev), w.to(dev), sf="RELU")
+    xf, wf = x.float().numpy(), w.float().numpy()
+    ref = isa_ref.mm(xf, wf, sf_kind="RELU")
+    scale = np.abs(xf).astype(np.float64) @ np.abs(wf).astype(np.float64)
+    _check(out, ref, scale, "update_mm bf16")
+
+
+def test_tile_nnz_gpu_matches_reference_golden(dev, golden_dir):
+    z = np.load(os.path.join(golden_dir, "cora_graph.npz"))
+    tiles = np.load(os.path.join(golden_dir, "cora_tiles.npz"))
+    g = G.from_numpy(z["indptr"], z["indices"], device=dev)
+    for T in (64, 512, 2752):
+        got = ops.tile_nnz(g, T).cpu().numpy()
+        assert np.array_equal(got, tiles[f"T{T}"])
+
+
+def test_plan_items_and_splits(dev):
+    g, ip, ix = _graph(100, 2000, seed=1, heavy_row=1000, dev=dev)
+    p = ops.AggregatePlan(g, 256)
+    deg = np.diff(ip)
+    chunks = np.where(deg <= 256, 1, -(-deg // 256))
+    assert p.n_items() == int(chunks.sum())
+    assert p.n_split() == int((deg > 256).sum())

@@ -1,0 +1,43 @@
+import numpy as np
+import torch
+
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G
+
+
+def test_synthetic_is_valid_csr_and_deterministic():
+    g1 = G.synthetic(1000, 20000, seed=5)
+    g2 = G.synthetic(1000, 20000, seed=5)
+    assert torch.equal(g1.indptr, g2.indptr) and torch.equal(g1.indices, g2.indices)
+    assert g1.nnz == 20000 and int(g1.indptr[-1]) == 20000
+    ip, ix = g1.numpy()
+    assert np.all(np.diff(ip) >= 0) and ix.min() >= 0 and ix.max() < 1000
+    for r in range(0, 1000, 97):  # sorted within rows
+        seg = ix[ip[r]:ip[r + 1]]
+        assert np.all(np.diff(seg) >= 0)
+
+
+def test_lognormal_degrees_sum_and_skew():
+    d = G.lognormal_degrees(10000, 4_920_000, seed=0)
+    assert int(d.sum()) == 4_920_000
+    assert float(d.max()) > 5 * float(d.float().mean())
+
+
+def test_dedupe_and_locality():
+    g = G.synthetic(200, 3000, seed=1, dedupe=True)
+    ip, ix = g.numpy()
+    rows = np.repeat(np.arange(200), np.diff(ip))
+    assert np.all(rows != ix)
+    assert len(set(zip(rows.tolist(), ix.tolist()))) == g.nnz
+    gl = G.synthetic(1000, 5000, seed=2, locality_width=4)
+    ip, ix = gl.numpy()
+    rows = np.repeat(np.arange(1000), np.diff(ip))
+    dist = np.minimum(np.abs(rows - ix), 1000 - np.abs(rows - ix))
+    assert dist.max() <= 4
+
+
+def test_norm_weights():
+    g = G.synthetic(100, 1000, seed=3)
+    w = G.gcn_norm_weights(g)
+    assert w.shape == (1000,) and torch.all(w > 0)
+    s = G.mean_weights(g)
+    assert s.shape == (100,)
