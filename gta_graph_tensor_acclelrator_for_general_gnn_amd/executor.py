@@ -1,0 +1,422 @@
+"""HIP executor for GTA instruction streams -- the drop-in for the reference's simulate().
+
+Reference boundary: `interpret()` writes Results/Insts/<net>-<ds>-<layer>-<map>.yaml
+(code/interpreter.py:805-849) and `simulate(tile_size_list, dataset, network,
+layer, isReorder, isSinput) -> (cycles, rw)` replays it as a cycle model
+(code/simulator.py:370-502).  `execute()` takes the same leading arguments,
+reads the same two YAML files, and runs the stream on real device tensors:
+
+  * blocks run in dependency order (the stream's block order is the
+    compiler's component sort, code/compiler.py:60, not a schedule);
+  * inside a block, ops run in data-flow order and are mapped onto libgta
+    kernels following the stream's own fusion decisions:
+      - a scatter whose FETCH was removed (fuse_fetch, code/interpreter.py:764-802)
+        is never materialised: its consumer gathers rows by index
+        (GTA_IDX_SRC for ORDER C, GTA_IDX_DST for ORDER R);
+      - a COMP_MUL_COMP_ADD / COMP_MM_COMP_ADD pair (inst_fusion_x2, :575-636;
+        hardware_info.yaml Inst_fused) becomes one aggregate kernel (MUL) or
+        an edge GEMM + gather (MM);
+      - scatters with a STORE_E are materialised with gta_scatter;
+  * numerics the YAML leaves open come from semantics.py.
+Returns ExecResult(values per op, outputs of sink ops, elapsed_s, alg_bytes).
+"""
+import time
+
+import torch
+
+from . import ir, ops
+from .semantics import Semantics
+
+
+class NodeT:
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t
+
+
+class EdgeT:
+    __slots__ = ("t",)
+
+    def __init__(self, t):
+        self.t = t
+
+
+class Scat:
+    """A scatter kept virtual: edge e reads row idx(e) of node tensor t (mode 'src' or 'dst')."""
+    __slots__ = ("t", "mode")
+
+    def __init__(self, t, mode):
+        self.t, self.mode = t, mode
+
+
+class Deferred:
+    """An applyedge MUL/MM fused into its gather consumer (evaluated by the gather)."""
+    __slots__ = ("op",)
+
+    def __init__(self, op):
+        self.op = op
+
+
+class ExecResult:
+    def __init__(self, values, outputs, elapsed_s, alg_bytes, launches):
+        self.values, self.outputs = values, outputs
+        self.elapsed_s, self.alg_bytes, self.launches = elapsed_s, alg_bytes, launches
+
+    def __repr__(self):
+        return (f"ExecResult(outputs={sorted(self.outputs)}, elapsed_s={self.elapsed_s:.6f}, "
+                f"alg_bytes={self.alg_bytes}, launches={self.launches})")
+
+
+class Executor:
+    def __init__(self, opgraph, stream, graph, tensors, semantics=None, plan_chunk=512):
+        self.g = opgraph
+        self.stream = stream
+        self.graph = graph
+        self.tensors = dict(tensors)
+        self.sem = semantics or Semantics()
+        self.plan_chunk = plan_chunk
+        self.values = {}
+        self.alg_bytes = 0
+        self.launches = 0
+
+    # ---------------------------------------------------------------- inputs
+    def _ext(self, op, slot):
+        return self.tensors.get(f"ext:{op.idx}:{slot}")
+
+    def _source(self, op, slot):
+        src = self.g.inputs[op.idx][slot]
+        if src.kind == "op":
+            if src.op not in self.values:
+                raise RuntimeError(f"op {op.idx} reads op {src.op} before it was produced")
+            return self.values[src.op]
+        t = self._ext(op, slot)
+        if src.kind == "ext":
+            if t is None:
+                raise KeyError(f"op {op.idx} slot {slot}: external input 'ext:{op.idx}:{slot}' not given")
+            return self._wrap_ext(t)
+        if t is not None:  # explicit override of the model input for this slot
+            return self._wrap_ext(t)
+        if op.type == "applyedge":
+            t = self.tensors.get("x_edge")
+            if t is None:
+                raise KeyError(f"edge op {op.idx} reads the model input: give 'x_edge' or 'ext:{op.idx}:{slot}'")
+            return EdgeT(t)
+        return NodeT(self.tensors["x"])
+
+    def _wrap_ext(self, t):
+        if t.dim() == 1:
+            t = t.view(-1, 1)
+        if t.shape[0] == self.graph.nnz and t.shape[0] != self.graph.n_rows:
+            return EdgeT(t)
+        if t.shape[0] == 1:
+            return ("row", t)
+        if t.shape[0] == self.graph.n_rows and t.shape[0] != self.graph.nnz:
+            return NodeT(t)
+        return EdgeT(t)  # ambiguous N == E: edge tensor
+
+    def _inputs(self, op):
+        return [self._source(op, s) for s in range(len(self.g.inputs[op.idx]))]
+
+    # ---------------------------------------------------------- materialise
+    def _edge_operand(self, v):
+        """-> (tensor, mode, broadcast_row) usable by apply_edge / aggregate."""
+        if isinstance(v, Deferred):
+            v = self._materialize_deferred(v)
+        if isinstance(v, EdgeT):
+            return v.t, "edge", False
+        if isinstance(v, Scat):
+            return v.t, v.mode, False
+        if isinstance(v, tuple) and v[0] == "row":
+            return v[1], "edge", True
+        raise TypeError(f"not an edge operand: {type(v).__name__}")
+
+    def _to_edge_tensor(self, v):
+        if isinstance(v, EdgeT):
+            return v.t
+        if isinstance(v, Scat):
+            self._count(self.graph.nnz * v.t.shape[1] * 4 * 2 + self.graph.nnz * 4)
+            return ops.scatter(self.graph, v.t, "C" if v.mode == "src" else "R")
+        if isinstance(v, Deferred):
+            return self._materialize_deferred(v).t
+        raise TypeError(type(v).__name__)
+
+    def _materialize_deferred(self, d):
+        op = self.g.ops[d.op]
+        v = self._eval_applyedge(op, fused=False)
+        self.values[d.op] = v
+        return v
+
+    def _count(self, nbytes):
+        self.alg_bytes += int(nbytes)
+        self.launches += 1
+
+    # ---------------------------------------------------------------- eval
+    def _binary(self, op):
+        b = self.sem.bin_of(op)
+        return b
+
+    def _eval_applyedge(self, op, fused):
+        ins = self._inputs(op)
+        E = self.graph.nnz
+        if op.comp == "MM":
+            return EdgeT(self._edge_mm(op, ins[0]))
+        if op.comp == "SF":
+            a, am, _ = self._edge_operand(ins[0])
+            out = ops.apply_edge(self.graph, None, self.sem.sf_of(op), a, am)
+            self._count(E * (a.shape[1] * 8))
+            return EdgeT(out)
+        bin_ = self._binary(op)
+        if len(ins) == 1:  # unary ADD/MUL: identity unless an extra operand is supplied
+            extra = self._ext(op, 1)
+            ins = ins + ([self._wrap_ext(extra)] if extra is not None else [])
+            if len(ins) == 1:
+                return EdgeT(self._to_edge_tensor(ins[0]))
+        x, y = ins[0], ins[1]
+        if bin_ == "RDIV":
+            x, y, bin_ = y, x, "DIV"
+        a, am, arow = self._edge_operand(x)
+        b, bm, brow = self._edge_operand(y)
+        if arow and not brow:  # keep the broadcast row in the b slot (ADD/MUL commute)
+            if bin_ in ("ADD", "MUL"):
+                a, am, b, bm, arow, brow = b, bm, a, am, False, True
+            else:
+                a = self._to_edge_tensor(("row", a)) if False else a.expand(E, a.shape[1]).contiguous()
+                am, arow = "edge", False
+        out = ops.apply_edge(self.graph, bin_, None, a, am, b, bm, b_broadcast_row=brow)
+        self._count(E * out.shape[1] * 4 * 3)
+        return EdgeT(out)
+
+    def _edge_mm(self, op, v):
+        W = self.tensors[f"w:{op.idx}"]
+        if isinstance(v, Scat):
+            idx = self.graph.indices if v.mode == "src" else self.graph.row_of_edge()
+            x, row_idx = v.t, idx
+        else:
+            x, row_idx = self._to_edge_tensor(v), None
+        x, W = self._mm_dtypes(x, W)
+        out = ops.update_mm(x, W, row_idx, m=self.graph.nnz if row_idx is None else None)
+        self._count(self.graph.nnz * (x.shape[1] * x.element_size() + W.shape[1] * 4))
+        return out
+
+    @staticmethod
+    def _mm_dtypes(x, W):
+        if W.dtype == torch.bfloat16 and x.dtype != torch.bfloat16:
+            x = x.to(torch.bfloat16)
+        if W.dtype == torch.float32 and x.dtype != torch.float32:
+            x = x.float()
+        return x, W
+
+    def _eval_gather(self, op):
+        if op.order != "R":
+            raise NotImplementedError("gather ORDER C (to source) is not emitted by genGraphOP")
+        v = self._source(op, 0)
+        n, E = self.graph.n_rows, self.graph.nnz
+        if isinstance(v, Deferred):
+            p = self.g.ops[v.op]
+            pins = self._inputs(p)
+            if p.comp == "MM":
+                xe = self._edge_mm(p, pins[0])
+                y = ops.gather_add(self.graph, xe)
+                self._count(E * xe.shape[1] * 4 + n * xe.shape[1] * 4)
+                return NodeT(y)
+            bin_ = self._binary(p)
+            if len(pins) == 1:
+                extra = self._ext(p, 1)
+                pins = pins + ([self._wrap_ext(extra)] if extra is not None else [])
+            if len(pins) == 1:
+                v = pins[0]
+            elif bin_ == "MUL":
+                return NodeT(self._weighted_aggregate(pins[0], pins[1]))
+            else:  # a non-MUL fused pair: evaluate the producer, then gather
+                v = self._materialize_deferred(v)
+        if isinstance(v, Scat):
+            y = ops.aggregate(self.graph, v.t, v.mode, None, plan=self._plan())
+            self._count(E * (4 + v.t.shape[1] * 4) + n * (8 + v.t.shape[1] * 4))
+            return NodeT(y)
+        xe = self._to_edge_tensor(v)
+        y = ops.aggregate(self.graph, xe, "edge", None, plan=self._plan())
+        self._count(E * xe.shape[1] * 4 + n * (8 + xe.shape[1] * 4))
+        return NodeT(y)
+
+    def _plan(self):
+        return self.plan_chunk if self.plan_chunk else None
+
+    def _weighted_aggregate(self, u, v):
+        """sum_e u(e) (.) v(e): the wider operand is the feature row, the narrower the (head) weight."""
+        n, E = self.graph.n_rows, self.graph.nnz
+
+        def width(z):
+            if isinstance(z, tuple):
+                return z[1].shape[1]
+            return z.t.shape[1] if not isinstance(z, Deferred) else 0
+
+        x, w = (u, v) if width(u) >= width(v) else (v, u)
+        if isinstance(w, tuple) and w[0] == "row":  # constant row weight: aggregate then scale (linear)
+            y = self._unweighted(x)
+            return ops.apply_node("MUL", None, y, w[1], b_broadcast_row=True)
+        wt = self._to_edge_tensor(w)
+        if isinstance(x, Scat):
+            xt, mode = x.t, x.mode
+        else:
+            xt, mode = self._to_edge_tensor(x), "edge"
+        if xt.shape[1] % wt.shape[1]:
+            raise ValueError(f"weighted aggregate: weight width {wt.shape[1]} does not divide {xt.shape[1]}")
+        y = ops.aggregate(self.graph, xt, mode, wt, plan=self._plan())
+        self._count(E * (4 + 4 * wt.shape[1] + 4 * xt.shape[1]) + n * (8 + 4 * xt.shape[1]))
+        return y
+
+    def _unweighted(self, x):
+        if isinstance(x, Scat):
+            return ops.aggregate(self.graph, x.t, x.mode, None, plan=self._plan())
+        return ops.aggregate(self.graph, self._to_edge_tensor(x), "edge", None, plan=self._plan())
+
+    def _eval_applynode(self, op):
+        ins = self._inputs(op)
+        n = self.graph.n_rows
+        if op.comp == "MM":
+            W = self.tensors[f"w:{op.idx}"]
+            x = self._node(ins[0])
+            x, W = self._mm_dtypes(x, W)
+            y = ops.update_mm(x, W)
+            self._count(n * (x.shape[1] * x.element_size() + W.shape[1] * 4) + W.numel() * W.element_size())
+            return NodeT(y)
+        if op.comp == "SF":
+            a = self._node(ins[0])
+            y = ops.apply_node(None, self.sem.sf_of(op), a)
+            self._count(n * a.shape[1] * 8)
+            return NodeT(y)
+        bin_ = self._binary(op)
+        if len(ins) == 1:
+            extra = self._ext(op, 1)
+            if extra is None:
+                return NodeT(self._node(ins[0]))
+            ins = ins + [self._wrap_ext(extra)]
+        x, y = ins[0], ins[1]
+        if bin_ == "RDIV":
+            x, y, bin_ = y, x, "DIV"
+        if isinstance(x, tuple) and bin_ in ("ADD", "MUL"):
+            x, y = y, x
+        a = self._node(x)
+        brow = isinstance(y, tuple)
+        b = y[1] if brow else self._node(y)
+        out = ops.apply_node(bin_, None, a, b, b_broadcast_row=brow)
+        self._count(n * out.shape[1] * 4 * 3)
+        return NodeT(out)
+
+    def _node(self, v):
+        if isinstance(v, NodeT):
+            return v.t
+        if isinstance(v, tuple) and v[0] == "row":
+            return v[1].expand(self.graph.n_rows, v[1].shape[1]).contiguous()
+        raise TypeError(f"applynode operand is not a node tensor ({type(v).__name__})")
+
+    def _eval(self, op, block):
+        fused_into = {p: c for p, c, _ in block.fused}
+        if op.type == "scatter":
+            v = self._source(op, 0)
+            if isinstance(v, tuple):
+                v = NodeT(self._node(v))
+            if not isinstance(v, NodeT):
+                raise TypeError(f"scatter op {op.idx} needs a node tensor")
+            s = Scat(v.t, "src" if op.order == "C" else "dst")
+            if op.idx in block.stored:
+                return EdgeT(self._to_edge_tensor(s))
+            return s
+        if op.type == "applyedge":
+            c = fused_into.get(op.idx)
+            if c is not None and self.g.ops[c].type == "gather" and op.comp in ("MUL", "MM"):
+                return Deferred(op.idx)
+            return self._eval_applyedge(op, fused=False)
+        if op.type == "gather":
+            return self._eval_gather(op)
+        if op.type == "applynode":
+            return self._eval_applynode(op)
+        raise ValueError(op.type)
+
+    # ---------------------------------------------------------------- run
+    def block_order(self):
+        owner = {}
+        for b in self.stream.blocks:
+            for o in b.ops:
+                owner.setdefault(o, b.index)
+        deps = {b.index: set() for b in self.stream.blocks}
+        for b in self.stream.blocks:
+            for o in b.ops:
+                for p in self.g.producers(o):
+                    if p in owner and owner[p] != b.index:
+                        deps[b.index].add(owner[p])
+        order, done = [], set()
+        pending = [b.index for b in self.stream.blocks]
+        while pending:
+            for i in pending:
+                if deps[i] <= done:
+                    order.append(i)
+                    done.add(i)
+                    pending.remove(i)
+                    break
+            else:
+                raise ValueError(f"stream blocks have a cyclic dependency: {pending}")
+        return order
+
+    def run(self):
+        covered = set()
+        for b in self.stream.blocks:
+            covered.update(b.ops)
+        missing = set(range(len(self.g))) - covered
+        if missing:
+            raise ValueError(f"stream does not cover ops {sorted(missing)}")
+        for bi in self.block_order():
+            block = self.stream.blocks[bi]
+            for i in self.g.topo(block.ops):
+                self.values[i] = self._eval(self.g.ops[i], block)
+        outputs = {}
+        for op in self.g.ops:
+            if not op.out_list:
+                v = self.values[op.idx]
+                outputs[op.idx] = self._final(v)
+        return outputs
+
+    def _final(self, v):
+        if isinstance(v, (NodeT, EdgeT)):
+            return v.t
+        if isinstance(v, Scat):
+            return self._to_edge_tensor(v)
+        if isinstance(v, Deferred):
+            return self._materialize_deferred(v).t
+        return v
+
+    def tensor_of(self, op_idx):
+        return self._final(self.values[op_idx])
+
+
+def run_stream(opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, sync=True):
+    ex = Executor(opgraph, stream, graph, tensors, semantics, plan_chunk)
+    dev = graph.device
+    if sync:
+        torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    outputs = ex.run()
+    if sync:
+        torch.cuda.synchronize(dev)
+    dt = time.perf_counter() - t0
+    return ExecResult(ex.values, outputs, dt, ex.alg_bytes, ex.launches), ex
+
+
+def execute(tile_size_list, dataset, network, layer, isReorder, isSinput=False, *, graph, tensors,
+            inst_root="Results/Insts", op_root="Network", inst_path=None, op_path=None, semantics=None,
+            plan_chunk=512):
+    """Drop-in for simulate(tile_size_list, dataset, network, layer, isReorder, isSinput)
+    (code/simulator.py:370): same leading arguments, same files, real execution.
+
+    tile_size_list / isSinput are accepted for signature parity; the tiles are
+    already encoded in the stream (Tile_Size/Tile_Times) and Sinput only
+    changes the reference's cost model (code/simulator.py:292-295, 312-313)."""
+    del tile_size_list, isSinput
+    sem = semantics or Semantics.for_network(network, isReorder)
+    op_path = op_path or ir.op_yaml_path(network, dataset, layer, isReorder, op_root)
+    inst_path = inst_path or ir.inst_path(network, dataset, layer, isReorder, inst_root)
+    g = ir.OpGraph.load(op_path, sem.inputs)
+    s = ir.Stream.load(inst_path)
+    res, _ = run_stream(g, s, graph, tensors, sem, plan_chunk)
+    return res

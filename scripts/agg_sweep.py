@@ -1,0 +1,73 @@
+"""Interleaved A/B sweep of aggregate-kernel variants on the Reddit-shaped metric workload.
+
+All variants run in ONE process, round-robin over R rounds (cdna_hip_programming.md
+§5.4 rule 24); prints median/min kernel ms per variant and writes JSON to gpurun_out/.
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--variants", default="lpe32:c512,lpe64:c512,lpe32:c256,lpe32:c1024,lpe32:c2048,lpe32:none")
+    ap.add_argument("--n", type=int, default=bench.N_REDDIT)
+    ap.add_argument("--e", type=int, default=bench.E_REDDIT)
+    ap.add_argument("--locality", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    g, x, alpha = bench.make_inputs(args.n, args.e, dev)
+    y = torch.empty(g.n_rows, bench.F, device=dev)
+    variants = []
+    for v in args.variants.split(","):
+        lpe, c = v.split(":")
+        lpe = int(lpe.replace("lpe", ""))
+        chunk = None if c == "none" else int(c.replace("c", ""))
+        variants.append((v, lpe, chunk))
+    plans = {c: (g.plan(c) if c else None) for _, _, c in variants}
+    times = {v: [] for v, _, _ in variants}
+    ref = None
+    for r in range(args.rounds):
+        for name, lpe, chunk in variants:
+            ops.set_debug("agg_lpe", lpe)
+            ops.aggregate(g, x, "src", alpha, out=y, plan=plans[chunk])  # warm
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(args.reps):
+                ops.aggregate(g, x, "src", alpha, out=y, plan=plans[chunk])
+            e.record()
+            torch.cuda.synchronize()
+            times[name].append(s.elapsed_time(e) / args.reps)
+            if r == 0:
+                if ref is None:
+                    ref = y.clone()
+                else:
+                    d = (y - ref).abs().max().item()
+                    assert d < 1e-3, f"variant {name} differs from the first by {d}"
+    ab = bench.alg_bytes(g.n_rows, g.nnz)
+    out = {}
+    for name in times:
+        med = float(np.median(times[name]))
+        out[name] = {"median_ms": med, "min_ms": float(np.min(times[name])),
+                     "alg_GBps": ab / (med / 1e3) / 1e9, "edges_per_s": g.nnz / (med / 1e3)}
+        print(f"{name:16s} median {med:7.3f} ms  min {out[name]['min_ms']:7.3f}  "
+              f"{out[name]['alg_GBps']:7.0f} GB/s alg  {out[name]['edges_per_s']/1e9:6.2f} Gedges/s", flush=True)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "agg_sweep.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

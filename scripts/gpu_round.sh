@@ -31,6 +31,9 @@ for s in $STEPS; do
       timeout -k 10 ${T_PROF:-600} rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run \
         -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/pmc_write.log 2>&1
       rc=$?; echo "pmc write rc=$rc"; stop_if_fatal $rc pmc ;;
+    sweep)
+      timeout -k 10 ${T_SWEEP:-600} python scripts/agg_sweep.py ${SWEEP_ARGS} > gpurun_out/sweep.log 2>&1
+      rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.log | tail -12; stop_if_fatal $rc sweep ;;
     *) echo "unknown step $s";;
   esac
 done

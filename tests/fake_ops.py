@@ -1,0 +1,57 @@
+"""TEST-ONLY stand-in for gta...ops on CPU tensors, computed by the fp64 oracle.
+
+Used by CPU tests to exercise the executor's block planning / fusion mapping
+without a GPU (monkeypatched over executor.ops).  Never used by the product.
+"""
+import numpy as np
+import torch
+
+from oracle import isa_ref
+
+
+def _np(t):
+    return None if t is None else t.detach().cpu().double().numpy()
+
+
+def _t(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))
+
+
+def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumulate=False, plan=None):
+    ip, ix = graph.numpy()
+    y = isa_ref.aggregate(ip, ix, _np(x), x_mode, _np(w), _np(row_scale))
+    if out is not None:
+        y = y + (_np(out) if accumulate else 0)
+        out.copy_(_t(y))
+        return out
+    return _t(y)
+
+
+def gather_add(graph, xe, out=None, accumulate=False):
+    return aggregate(graph, xe, "edge", None, out=out, accumulate=accumulate)
+
+
+def scatter(graph, x, direction, out=None):
+    ip, ix = graph.numpy()
+    return torch.from_numpy(isa_ref.scatter(ip, ix, x.detach().cpu().numpy(), direction))
+
+
+def apply_edge(graph, bin, sf, a, a_mode="edge", b=None, b_mode="edge", out=None, b_broadcast_row=False):
+    ip, ix = graph.numpy()
+    return _t(isa_ref.apply_edge(ip, ix, bin, sf, _np(a), a_mode, _np(b), b_mode, b_broadcast_row))
+
+
+def apply_node(bin, sf, a, b=None, out=None, b_broadcast_row=False):
+    return _t(isa_ref.apply_node(bin, sf, _np(a), _np(b), b_broadcast_row))
+
+
+def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
+    xr = _np(x)
+    if row_idx is None and m is not None:
+        xr = xr[:m]
+    return _t(isa_ref.mm(xr, _np(w), None if row_idx is None else row_idx.cpu().numpy(), sf))
+
+
+def tile_nnz(graph, T):
+    ip, ix = graph.numpy()
+    return torch.from_numpy(isa_ref.tile_nnz(ip, ix, graph.n_cols, T).astype(np.int32))

@@ -1,0 +1,96 @@
+"""IR parsing of every golden stream/op graph, and the executor's block planning on CPU.
+
+The executor is driven through tests/fake_ops.py (oracle-backed, CPU) so the
+mapping of blocks/fused COMPs to kernels is checked here without a GPU; the
+same streams run on the real kernels in test_gpu_executor.py.
+"""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import executor, graph as G, ir, workloads
+from gta_graph_tensor_acclelrator_for_general_gnn_amd.semantics import Semantics
+from oracle.exec_ref import execute_ref
+
+from . import fake_ops
+
+
+def _streams(manifest, dataset="cora"):
+    return [s for s in manifest["streams"] if "file" in s and s["dataset"] == dataset]
+
+
+def test_every_op_yaml_parses(golden_dir, manifest):
+    for rec in manifest["ops"]:
+        g = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["file"]),
+                            Semantics.for_network(rec["network"], rec["reorder"]).inputs)
+        assert len(g) >= 4
+        g.topo()  # acyclic after resolution
+
+
+def test_parse_metric_stream(golden_dir):
+    s = ir.Stream.load(os.path.join(golden_dir, "streams", "GAT-reddit-layer1-original-h512.yaml"))
+    blk = [b for b in s if set(b.ops) == {3, 11, 12}][0]
+    assert blk.fused == [(11, 12, ["MUL", "ADD"])]
+    comp = [i for i in blk.insts if i.kind == "comp"][0]
+    assert comp.type == "COMP_MUL_COMP_ADD" and comp.id == "11_applyedge_0_12_gather_0"
+    assert comp.tile_times == 106232040 and comp.tile_size == 512
+    assert not any(i.type == "FETCH" for i in blk.insts)  # fuse_fetch removed the scatter's FETCH
+    assert blk.stored == [12]
+
+
+def test_block_order_is_dependency_order(golden_dir, manifest):
+    for rec in _streams(manifest):
+        sem = Semantics.for_network(rec["network"], rec["reorder"])
+        g = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+        s = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+        ex = executor.Executor(g, s, None, {}, sem)
+        order = ex.block_order()
+        seen = set()
+        for bi in order:
+            b = s.blocks[bi]
+            for o in b.ops:
+                for p in g.producers(o):
+                    assert p in seen or p in b.ops, (rec["file"], o, p)
+            seen.update(b.ops)
+
+
+def _cora_graph(golden_dir):
+    z = np.load(os.path.join(golden_dir, "cora_graph.npz"))
+    return G.from_numpy(z["indptr"], z["indices"]), z["indptr"], z["indices"]
+
+
+def compare(values_ex, ref, ops_to_check, rtol=1e-4):
+    for i in ops_to_check:
+        got = values_ex[i].detach().cpu().double().numpy()
+        exp = ref[i][1]
+        assert got.shape == exp.shape, (i, got.shape, exp.shape)
+        nan_g, nan_e = ~np.isfinite(got), ~np.isfinite(exp)
+        assert np.array_equal(nan_g, nan_e), f"op {i}: non-finite pattern differs"
+        got, exp = got[~nan_e], exp[~nan_e]
+        if exp.size == 0:
+            continue
+        scale = np.abs(exp).max() + 1e-30
+        err = np.abs(got - exp).max() / scale
+        assert err <= rtol, f"op {i}: normalised max err {err:.2e}"
+
+
+@pytest.mark.parametrize("idx", range(0, 160, 1))
+def test_executor_plans_every_golden_stream(golden_dir, manifest, monkeypatch, idx):
+    streams = _streams(manifest)
+    if idx >= len(streams):
+        pytest.skip("fewer streams")
+    rec = streams[idx]
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    g, ip, ix = _cora_graph(golden_dir)
+    sem = Semantics.for_network(rec["network"], rec["reorder"])
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    tensors = workloads.make_tensors(og, g, rec["network"], seed=idx)
+    ex = executor.Executor(og, st, g, tensors, sem, plan_chunk=0)
+    outs = ex.run()
+    ref = execute_ref(og, sem, ip, ix, {k: v.numpy() for k, v in tensors.items()})
+    vals = {i: ex.tensor_of(i) for i in range(len(og))}
+    compare(vals, ref, range(len(og)))
+    assert set(outs) == {op.idx for op in og.ops if not op.out_list}
