@@ -207,7 +207,13 @@ __global__ void k_plan_fill(const int64_t* __restrict__ indptr, int64_t n_rows, 
 enum { XM_IDX = 0, XM_EDGE = 1 };
 enum { WM_NONE = 0, WM_HEAD = 1, WM_FULL = 2 };
 
-template <int LPE, int VW, int NV, int XMODE, int WMODE>
+template <bool NT, typename T>
+__device__ __forceinline__ T ld_stream(const T* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+
+template <int LPE, int VW, int NV, int XMODE, int WMODE, bool NT>
 __global__ void __launch_bounds__(kBlock)
 k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
             PlanView plan, int use_plan, int64_t chunk, int x_is_row,
@@ -256,10 +262,15 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
 #pragma unroll
       for (int k = 0; k < VW; ++k) acc[v][k] = 0.f;
 
+    // source indices arrive 64 at a time; the next block's are prefetched while
+    // this block's rows are in flight (clamped address: the load is unconditional)
+    const bool use_idx = (XMODE == XM_IDX) && !x_is_row;
+    int idxv = 0;
+    if (use_idx && eb < ee) idxv = ld_stream<NT>(indices + min(eb + lane, ee - 1));
     for (int64_t e0 = eb; e0 < ee; e0 += kWave) {
       const int n = static_cast<int>(min<int64_t>(kWave, ee - e0));
-      int idxv = 0;
-      if (XMODE == XM_IDX && !x_is_row) idxv = indices[e0 + min(lane, n - 1)];
+      int idxn = 0;
+      if (use_idx) idxn = ld_stream<NT>(indices + min(e0 + kWave + lane, ee - 1));
       for (int s = 0; s < n; s += STEP) {
         Vec<VW> xv[UR][NV];
         float wh[UR][NV];
@@ -286,7 +297,7 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
           if (WMODE == WM_HEAD) {
             const float* wp = w + (e0 + jj) * ldw;
 #pragma unroll
-            for (int v = 0; v < NV; ++v) wh[u][v] = wp[hcol[v]];
+            for (int v = 0; v < NV; ++v) wh[u][v] = ld_stream<NT>(wp + hcol[v]);
           } else if (WMODE == WM_FULL) {
             const float* wp = w + (e0 + jj) * ldw;
 #pragma unroll
@@ -308,6 +319,7 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
           }
         }
       }
+      idxv = idxn;
     }
     if (LPE < kWave) {  // fold the EPI edge slots (fixed butterfly order)
 #pragma unroll
@@ -597,45 +609,51 @@ struct AggArgs {
   const float* row_scale; float* y; int64_t ldy; int accumulate; float* partial;
 };
 
-template <int LPE, int VW, int NV, int XM, int WM>
+template <int LPE, int VW, int NV, int XM, int WM, bool NT>
 void launch_agg(const AggArgs& a, int64_t n_items_bound, hipStream_t s) {
   const int64_t blocks = (n_items_bound + kWavesPerBlock - 1) / kWavesPerBlock;
-  k_aggregate<LPE, VW, NV, XM, WM><<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
+  k_aggregate<LPE, VW, NV, XM, WM, NT><<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
       a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, a.x_is_row, a.x, a.ldx, a.F, a.w, a.ldw, a.gsz,
       a.row_scale, a.y, a.ldy, a.accumulate, a.partial);
 }
 
 template <int LPE, int VW, int NV, int XM>
-bool dispatch_w(int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
+bool dispatch_w(int wm, bool nt, const AggArgs& a, int64_t nb, hipStream_t s) {
   switch (wm) {
-    case WM_NONE: launch_agg<LPE, VW, NV, XM, WM_NONE>(a, nb, s); return true;
-    case WM_HEAD: launch_agg<LPE, VW, NV, XM, WM_HEAD>(a, nb, s); return true;
-    case WM_FULL: launch_agg<LPE, VW, NV, XM, WM_FULL>(a, nb, s); return true;
+    case WM_NONE: launch_agg<LPE, VW, NV, XM, WM_NONE, false>(a, nb, s); return true;
+    case WM_HEAD:
+      // non-temporal index/weight streams only where they pay: the SpMM (XM_IDX) form
+      if (XM == XM_IDX && nt) launch_agg<LPE, VW, NV, XM, WM_HEAD, true>(a, nb, s);
+      else launch_agg<LPE, VW, NV, XM, WM_HEAD, false>(a, nb, s);
+      return true;
+    case WM_FULL: launch_agg<LPE, VW, NV, XM, WM_FULL, false>(a, nb, s); return true;
   }
   return false;
 }
 
 template <int LPE, int VW, int NV>
-bool dispatch_x(int xm, int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
-  return xm == XM_EDGE ? dispatch_w<LPE, VW, NV, XM_EDGE>(wm, a, nb, s) : dispatch_w<LPE, VW, NV, XM_IDX>(wm, a, nb, s);
+bool dispatch_x(int xm, int wm, bool nt, const AggArgs& a, int64_t nb, hipStream_t s) {
+  return xm == XM_EDGE ? dispatch_w<LPE, VW, NV, XM_EDGE>(wm, false, a, nb, s)
+                       : dispatch_w<LPE, VW, NV, XM_IDX>(wm, nt, a, nb, s);
 }
 
 template <int VW>
-bool dispatch_lpe(int lpe, int nv, int xm, int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
+bool dispatch_lpe(int lpe, int nv, int xm, int wm, bool nt, const AggArgs& a, int64_t nb, hipStream_t s) {
   switch (lpe) {
     case 64:
-      if (nv == 1) return dispatch_x<64, VW, 1>(xm, wm, a, nb, s);
-      if (nv == 2) return dispatch_x<64, VW, 2>(xm, wm, a, nb, s);
-      return dispatch_x<64, VW, 4>(xm, wm, a, nb, s);
-    case 32: return dispatch_x<32, VW, 1>(xm, wm, a, nb, s);
-    case 16: return dispatch_x<16, VW, 1>(xm, wm, a, nb, s);
-    case 8: return dispatch_x<8, VW, 1>(xm, wm, a, nb, s);
-    default: return dispatch_x<4, VW, 1>(xm, wm, a, nb, s);
+      if (nv == 1) return dispatch_x<64, VW, 1>(xm, wm, nt, a, nb, s);
+      if (nv == 2) return dispatch_x<64, VW, 2>(xm, wm, nt, a, nb, s);
+      return dispatch_x<64, VW, 4>(xm, wm, nt, a, nb, s);
+    case 32: return dispatch_x<32, VW, 1>(xm, wm, nt, a, nb, s);
+    case 16: return dispatch_x<16, VW, 1>(xm, wm, nt, a, nb, s);
+    case 8: return dispatch_x<8, VW, 1>(xm, wm, nt, a, nb, s);
+    default: return dispatch_x<4, VW, 1>(xm, wm, nt, a, nb, s);
   }
 }
 
-int g_force_lpe = 0;  // tuning hook (gta_debug_set), 0 = automatic
+int g_force_lpe = 0;  // tuning hooks (gta_debug_set); 0 = automatic
 int g_force_vw = 0;
+int g_agg_nt = 0;     // non-temporal index/weight loads in the SpMM form
 
 }  // namespace
 
@@ -652,6 +670,7 @@ int gta_debug_set(const char* key, int64_t value) {
   std::string k(key ? key : "");
   if (k == "agg_lpe") { g_force_lpe = static_cast<int>(value); return 0; }
   if (k == "agg_vw") { g_force_vw = static_cast<int>(value); return 0; }
+  if (k == "agg_nt") { g_agg_nt = static_cast<int>(value); return 0; }
   return fail(GTA_ERR_ARG, "gta_debug_set: unknown key " + k);
 }
 
@@ -707,12 +726,15 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
   };
   int vw = ok_vw(4) ? 4 : (ok_vw(2) ? 2 : 1);
   if (g_force_vw && g_force_vw <= vw && ok_vw(g_force_vw)) vw = g_force_vw;
+  // one edge per wave instruction (LPE = 64, wave-uniform row base) whenever the
+  // row fills 64 lanes at >= 8 B/lane: measured 3 % faster than two edges per
+  // instruction at float4 for F = 128 (profiles/r01_agg_sweep_1.json)
+  if (vw == 4 && F < 4 * kWave && F >= 2 * kWave && ok_vw(2)) vw = 2;
   const int64_t lanes = (F + vw - 1) / vw;
   int lpe, nv = 1;
   if (lanes >= kWave) {
     lpe = kWave;
     nv = lanes >= 4 * kWave ? 4 : (lanes > kWave ? 2 : 1);
-    if (vw == 4 && F == 128 && !g_force_lpe) { vw = 2; }  // 64 lanes x float2 covers 128 exactly
   } else {
     lpe = 4;
     while (lpe < lanes) lpe <<= 1;
@@ -735,9 +757,9 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
   hipStream_t s = S(stream);
   bool ok = false;
   switch (vw) {
-    case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, a, bound, s); break;
-    case 2: ok = dispatch_lpe<2>(lpe, nv, xm, wm, a, bound, s); break;
-    default: ok = dispatch_lpe<1>(lpe, nv, xm, wm, a, bound, s); break;
+    case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, g_agg_nt != 0, a, bound, s); break;
+    case 2: ok = dispatch_lpe<2>(lpe, nv, xm, wm, g_agg_nt != 0, a, bound, s); break;
+    default: ok = dispatch_lpe<1>(lpe, nv, xm, wm, g_agg_nt != 0, a, bound, s); break;
   }
   if (!ok) return fail(GTA_ERR_UNSUPPORTED, "aggregate: no kernel variant");
   GTA_LAUNCHED("k_aggregate");

@@ -22,7 +22,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
-    ap.add_argument("--variants", default="lpe32:c512,lpe64:c512,lpe32:c256,lpe32:c1024,lpe32:c2048,lpe32:none")
+    ap.add_argument("--variants", default="lpe64:c512,lpe64:c512:nt,lpe32:c512,lpe32:c512:nt,lpe64:c1024,"
+                                             "lpe64:c1024:nt,lpe64:c256")
     ap.add_argument("--n", type=int, default=bench.N_REDDIT)
     ap.add_argument("--e", type=int, default=bench.E_REDDIT)
     ap.add_argument("--locality", action="store_true")
@@ -32,16 +33,18 @@ def main():
     y = torch.empty(g.n_rows, bench.F, device=dev)
     variants = []
     for v in args.variants.split(","):
-        lpe, c = v.split(":")
-        lpe = int(lpe.replace("lpe", ""))
-        chunk = None if c == "none" else int(c.replace("c", ""))
-        variants.append((v, lpe, chunk))
-    plans = {c: (g.plan(c) if c else None) for _, _, c in variants}
-    times = {v: [] for v, _, _ in variants}
+        parts = v.split(":")
+        lpe = int(parts[0].replace("lpe", ""))
+        chunk = None if parts[1] == "none" else int(parts[1].replace("c", ""))
+        nt = int("nt" in parts[2:])
+        variants.append((v, lpe, chunk, nt))
+    plans = {c: (g.plan(c) if c else None) for _, _, c, _ in variants}
+    times = {v[0]: [] for v in variants}
     ref = None
     for r in range(args.rounds):
-        for name, lpe, chunk in variants:
+        for name, lpe, chunk, nt in variants:
             ops.set_debug("agg_lpe", lpe)
+            ops.set_debug("agg_nt", nt)
             ops.aggregate(g, x, "src", alpha, out=y, plan=plans[chunk])  # warm
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
