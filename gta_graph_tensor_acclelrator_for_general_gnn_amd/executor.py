@@ -59,13 +59,22 @@ class Deferred:
 
 
 class ExecResult:
+    """Real outputs + measured time, and the reference's modelled (cycles, rw) for the same stream."""
+
     def __init__(self, values, outputs, elapsed_s, alg_bytes, launches):
         self.values, self.outputs = values, outputs
         self.elapsed_s, self.alg_bytes, self.launches = elapsed_s, alg_bytes, launches
+        self.model_cycles = None  # simulate()'s first result (code/simulator.py:502), if requested
+        self.model_rw = None      # simulate()'s second result: modelled DRAM bytes
+
+    def simulate_tuple(self):
+        """(cycles, rw) in the shape the reference's simulate() returns."""
+        return self.model_cycles, self.model_rw
 
     def __repr__(self):
         return (f"ExecResult(outputs={sorted(self.outputs)}, elapsed_s={self.elapsed_s:.6f}, "
-                f"alg_bytes={self.alg_bytes}, launches={self.launches})")
+                f"alg_bytes={self.alg_bytes}, launches={self.launches}, model=({self.model_cycles}, "
+                f"{self.model_rw}))")
 
 
 class Executor:
@@ -403,20 +412,48 @@ def run_stream(opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, 
     return ExecResult(ex.values, outputs, dt, ex.alg_bytes, ex.launches), ex
 
 
+SPARSITY = {"cora": 0.012, "pubmed": 0.1, "flickr": 0.46, "reddit": 1}  # code/simulator.py:381-392
+
+
+def attach_model(res, stream_records, tile_size_list, graph, model="rw", isSinput=False, dataset=None):
+    """Fill res.model_rw (closed form) and, for model == "full", res.model_cycles via the exact
+    cost-model restatement (costmodel.py).  Tile nnz come from the GPU (gta_tile_nnz); like the
+    reference's dense adjacency they assume a duplicate-free CSR."""
+    from . import costmodel
+    if model is None:
+        return res
+    n = graph.n_rows
+    cache = {}
+
+    def tiles_for(T):
+        if T not in cache:
+            cache[T] = ops.tile_nnz(graph, int(T)).flatten().cpu().tolist()
+        return cache[T]
+    if model == "full":
+        res.model_cycles, res.model_rw = costmodel.simulate_stream(
+            stream_records, tile_size_list, n, tiles_for, isSinput, SPARSITY.get(dataset, 1))
+    else:
+        e_tiles = int(ops.tile_nnz(graph, n).sum().item())
+        res.model_rw = costmodel.model_rw(stream_records, n, e_tiles)
+    return res
+
+
 def execute(tile_size_list, dataset, network, layer, isReorder, isSinput=False, *, graph, tensors,
             inst_root="Results/Insts", op_root="Network", inst_path=None, op_path=None, semantics=None,
-            plan_chunk=512):
+            plan_chunk=512, model="rw"):
     """Drop-in for simulate(tile_size_list, dataset, network, layer, isReorder, isSinput)
     (code/simulator.py:370): same leading arguments, same files, real execution.
 
-    tile_size_list / isSinput are accepted for signature parity; the tiles are
-    already encoded in the stream (Tile_Size/Tile_Times) and Sinput only
-    changes the reference's cost model (code/simulator.py:292-295, 312-313)."""
-    del tile_size_list, isSinput
+    Returns ExecResult: the sink ops' device tensors, measured elapsed_s, and the
+    reference's modelled numbers for the same stream: model_rw (always, closed
+    form) and model_cycles (model="full"; exact restatement of the cycle loop,
+    Python-speed, meant for Cora/Flickr-sized graphs).  `res.simulate_tuple()`
+    is what simulate() would have returned."""
     sem = semantics or Semantics.for_network(network, isReorder)
     op_path = op_path or ir.op_yaml_path(network, dataset, layer, isReorder, op_root)
     inst_path = inst_path or ir.inst_path(network, dataset, layer, isReorder, inst_root)
     g = ir.OpGraph.load(op_path, sem.inputs)
-    s = ir.Stream.load(inst_path)
+    records = ir.read_yaml(inst_path)
+    s = ir.Stream(records)
     res, _ = run_stream(g, s, graph, tensors, sem, plan_chunk)
-    return res
+    return attach_model(res, records, tile_size_list, graph, model, isSinput, dataset)

@@ -74,6 +74,26 @@ def test_executor_drop_in_signature(golden_dir, manifest, cora, dev, tmp_path, m
     assert out.shape == (2708, 128) and torch.isfinite(out).all()
 
 
+def test_execute_reports_reference_simulate_numbers(golden_dir, manifest, cora, dev, tmp_path, monkeypatch):
+    """Same call, same stream, same graph: model (cycles, rw) == the reference simulate() output."""
+    import shutil
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import lowering
+    ip, ix = cora
+    gd = G.from_numpy(ip, ix, device=dev)
+    monkeypatch.chdir(tmp_path)
+    for case in manifest["simulate"]:
+        net, ds, layer, m = case["key"].split("-")
+        os.makedirs(f"Network/{net}/{net}-{ds}/{net}-{m}", exist_ok=True)
+        shutil.copy(os.path.join(golden_dir, "ops", f"{net}-{ds}-{layer}-{m}.yaml"),
+                    f"Network/{net}/{net}-{ds}/{net}-{m}/{net}-{layer}-{m}.yaml")
+        lowering.interpret(ds, net, m == "trans", layer, case["op_array"], case["tile_size_list"])
+        og = ir.OpGraph.load(f"Network/{net}/{net}-{ds}/{net}-{m}/{net}-{layer}-{m}.yaml")
+        tensors = workloads.make_tensors(og, gd, net, seed=1)
+        res = executor.execute(case["tile_size_list"], ds, net, layer, m == "trans", False, graph=gd,
+                               tensors=tensors, model="full")
+        assert res.simulate_tuple() == (case["cycles"], case["rw"]), case["key"]
+
+
 def test_executor_deterministic(golden_dir, manifest, cora, dev):
     rec = [s for s in manifest["streams"] if s.get("file") == "GAT-reddit-layer1-original-h512.yaml"][0]
     ip, ix = cora
