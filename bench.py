@@ -107,10 +107,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # rehearsal knobs for a 1-GPU box: GTA_DIST_BACKEND=gloo GTA_SINGLE_DEVICE=1 (all ranks on cuda:0)
+    backend = os.environ.get("GTA_DIST_BACKEND", "nccl")
+    if os.environ.get("GTA_SINGLE_DEVICE"):
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(backend)
     if args.lpe:
         ops.set_debug("agg_lpe", args.lpe)
 
@@ -165,6 +172,19 @@ def main():
     ms_per_step = dt * 1e3 / args.steps
     value = nnz_total / (ms_per_step / 1e3)
 
+    # size-independent parity checks on the full workload (outside the timed region):
+    # N=1: a repeat run is bitwise identical; N>1: the all-reduced Y equals the 1-GPU aggregate
+    y_mine = y.clone()
+    if world > 1:
+        ref = ops.aggregate(g, x, "src", alpha, plan=args.chunk)
+        err = float((y_mine - ref).abs().max().item())
+        scale = float(ref.abs().max().item())
+        parity = {"check": "allreduced shards vs 1-GPU aggregate", "max_abs_err": err, "max_abs_ref": scale,
+                  "ok": err <= 1e-4 * scale + 1e-5}
+    else:
+        step()
+        parity = {"check": "repeat run bitwise identical", "ok": bool(torch.equal(y, y_mine))}
+
     # roofline of the dominant kernel (this rank's shard)
     ab = alg_bytes(gl.n_rows, gl.nnz)
     achieved = ab / (kern_ms / 1e3) / 1e9
@@ -197,6 +217,7 @@ def main():
                    "parallelism": f"edge-partition by source column x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
                    "plan_chunk": args.chunk, "row_chunks": n_chunks},
         "achieved_GBps": nnz_total and alg_bytes(g.n_rows, nnz_total) / (ms_per_step / 1e3) / 1e9,
+        "parity": parity,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": ab},

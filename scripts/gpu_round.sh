@@ -31,6 +31,11 @@ for s in $STEPS; do
       timeout -k 10 ${T_PROF:-600} rocprofv3 --kernel-trace --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write -o run \
         -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/pmc_write.log 2>&1
       rc=$?; echo "pmc write rc=$rc"; stop_if_fatal $rc pmc ;;
+    bench2)
+      GTA_DIST_BACKEND=gloo GTA_SINGLE_DEVICE=1 timeout -k 10 ${T_BENCH:-600} python -m torch.distributed.run \
+        --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 \
+        > gpurun_out/bench2.log 2>&1
+      rc=$?; echo "bench2 rc=$rc"; grep '^{' gpurun_out/bench2.log | tail -1; stop_if_fatal $rc bench2 ;;
     sweep)
       timeout -k 10 ${T_SWEEP:-600} python scripts/agg_sweep.py ${SWEEP_ARGS} > gpurun_out/sweep.log 2>&1
       rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.log | tail -12; stop_if_fatal $rc sweep ;;
