@@ -1,0 +1,52 @@
+"""The BASELINE.json configurations as runnable workloads (synthetic graphs of the named shapes).
+
+  gcn-cora     2-layer GCN on Cora (hidden 128): layer 1 (1433->128) then layer 2 (128->64)
+  gat8-flickr  GAT layer 1 on Flickr (89,250 nodes / 899,756 edges), 8 heads, F=500
+  sage-reddit  GraphSAGE-mean layer 1 on Reddit (232,965 / 114,615,892), F=602
+  gin-products GIN layer 1 on an ogbn-products-shaped CSR (2,449,029 / 123,718,280), F=100,
+               both MLP GEMMs in bf16 on MFMA (fp32 accumulation)
+(config 0 -- V2/GAT_Cora.yaml through compile/interpret on the CPU -- is the golden-stream
+suite: tests/test_lowering.py, test_compiler.py.)
+"""
+import torch
+
+from . import graph as G, pipeline, workloads
+
+CONFIGS = {
+    "gcn-cora": dict(network="GCN", dataset="cora", feature=1433, layers=(1, 2)),
+    "gat8-flickr": dict(network="GAT", dataset="flickr", feature=500, layers=(1,), heads=8),
+    "sage-reddit": dict(network="GraphSAGE", dataset="reddit", feature=602, layers=(1,)),
+    "gin-products": dict(network="GIN", dataset="products", feature=100, layers=(1,), bf16=True),
+}
+
+
+def build(name, device, seed=0, graph=None):
+    """-> (list of pipeline.Layer, graph, tensors of the first layer)."""
+    c = CONFIGS[name]
+    g = graph if graph is not None else G.dataset_graph(c["dataset"], seed=seed, device=device)
+    layers = []
+    meta = None
+    for i, L in enumerate(c["layers"]):
+        feat = c["feature"] if L == 1 else [0, c["feature"], 128, 64, 16][L]
+        lay = pipeline.Layer(c["network"], L, g, feat, heads=c.get("heads", 16), metadata=meta)
+        meta = meta or lay.metadata
+        layers.append(lay)
+    dtype_w = torch.bfloat16 if c.get("bf16") else torch.float32
+    tensors = [workloads.make_tensors(lay.opgraph, g, c["network"], seed=seed + k, dtype_w=dtype_w)
+               for k, lay in enumerate(layers)]
+    return layers, g, tensors
+
+
+def run(name, device, seed=0):
+    """Run every layer of the config, feeding each layer's sink output into the next as x."""
+    layers, g, tensors = build(name, device, seed)
+    results = []
+    x = None
+    for lay, t in zip(layers, tensors):
+        if x is not None:
+            t["x"] = x
+        res, ex = lay.run(t)
+        results.append((lay, res, ex))
+        sinks = sorted(res.outputs)
+        x = res.outputs[sinks[-1]]
+    return results, g

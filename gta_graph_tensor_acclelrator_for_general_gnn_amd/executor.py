@@ -77,6 +77,9 @@ class ExecResult:
                 f"{self.model_rw}))")
 
 
+MAX_MATERIALIZE_BYTES = 96 << 30  # refuse to materialise a single edge tensor larger than this
+
+
 class Executor:
     def __init__(self, opgraph, stream, graph, tensors, semantics=None, plan_chunk=512):
         self.g = opgraph
@@ -144,6 +147,10 @@ class Executor:
         if isinstance(v, EdgeT):
             return v.t
         if isinstance(v, Scat):
+            nbytes = self.graph.nnz * v.t.shape[1] * v.t.element_size()
+            if nbytes > MAX_MATERIALIZE_BYTES:
+                raise MemoryError(f"stream materialises a {nbytes / 2**30:.0f} GiB edge tensor (scatter not fused "
+                                  "with its consumer); choose a fusion partition that keeps it virtual")
             self._count(self.graph.nnz * v.t.shape[1] * 4 * 2 + self.graph.nnz * 4)
             return ops.scatter(self.graph, v.t, "C" if v.mode == "src" else "R")
         if isinstance(v, Deferred):

@@ -36,6 +36,9 @@ for s in $STEPS; do
         --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 \
         > gpurun_out/bench2.log 2>&1
       rc=$?; echo "bench2 rc=$rc"; grep '^{' gpurun_out/bench2.log | tail -1; stop_if_fatal $rc bench2 ;;
+    layers)
+      timeout -k 10 ${T_LAYERS:-600} python scripts/layer_bench.py > gpurun_out/layers.log 2>&1
+      rc=$?; echo "layers rc=$rc"; tail -6 gpurun_out/layers.log; stop_if_fatal $rc layers ;;
     sweep)
       timeout -k 10 ${T_SWEEP:-600} python scripts/agg_sweep.py ${SWEEP_ARGS} > gpurun_out/sweep.log 2>&1
       rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.log | tail -12; stop_if_fatal $rc sweep ;;

@@ -1,0 +1,47 @@
+"""Time full BASELINE-config layers through the executor (secondary numbers, not the headline)."""
+import json
+import os
+import sys
+import time
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import configs  # noqa: E402
+
+
+def main(names=None, reps=5):
+    dev = torch.device("cuda:0")
+    out = {}
+    for name in (names or list(configs.CONFIGS)):
+        t0 = time.perf_counter()
+        layers, g, tensors = configs.build(name, dev)
+        build_s = time.perf_counter() - t0
+        times = []
+        for r in range(reps + 1):
+            torch.cuda.synchronize()
+            t1 = time.perf_counter()
+            x = None
+            for lay, t in zip(layers, tensors):
+                if x is not None:
+                    t["x"] = x
+                res, _ = lay.run(t)
+                x = res.outputs[sorted(res.outputs)[-1]]
+            torch.cuda.synchronize()
+            if r:
+                times.append(time.perf_counter() - t1)
+        ms = 1e3 * sorted(times)[len(times) // 2]
+        out[name] = {"N": g.n_rows, "E": g.nnz, "layers": [l.layer for l in layers],
+                     "op_array": [l.op_array for l in layers], "tile_size_list": [l.tile_size_list for l in layers],
+                     "ms_per_forward": ms, "edges_per_s": g.nnz * len(layers) / (ms / 1e3), "build_s": build_s}
+        print(name, json.dumps(out[name]), flush=True)
+        del layers, g, tensors
+        torch.cuda.empty_cache()
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "layer_bench.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main(sys.argv[1:] or None)
