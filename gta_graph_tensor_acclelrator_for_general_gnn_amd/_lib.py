@@ -13,7 +13,7 @@ LIB_PATH = os.path.join(_HERE, "libgta.so")
 ABI_VERSION = 1
 
 # enum mirrors of include/gta.h
-GTA_F32, GTA_BF16 = 0, 1
+GTA_F32, GTA_BF16, GTA_F32_BF16 = 0, 1, 2
 DIR_R, DIR_C = 0, 1
 IDX_EDGE, IDX_SRC, IDX_DST = 0, 1, 2
 BIN_NONE, BIN_ADD, BIN_MUL, BIN_DIV, BIN_SUB = 0, 1, 2, 3, 4

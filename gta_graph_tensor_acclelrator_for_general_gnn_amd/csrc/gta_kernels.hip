@@ -517,8 +517,14 @@ k_mm_f32(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ r
 // fragments are one 16-B LDS read.
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
+__device__ __forceinline__ uint16_t to_bf16_bits(float f) {
+  return __builtin_bit_cast(uint16_t, __float2bfloat16(f));  // round to nearest even
+}
+__device__ __forceinline__ uint16_t to_bf16_bits(uint16_t b) { return b; }
+
+template <typename TA>
 __global__ void __launch_bounds__(kBlock)
-k_mm_bf16(const uint16_t* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
+k_mm_bf16(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const uint16_t* __restrict__ w, int64_t ldw, int N, int sf, float* __restrict__ out, int64_t ldo) {
   constexpr int BM = 64, BN = 64, BK = 32, PAD = 8;
   __shared__ __attribute__((aligned(16))) uint16_t As[BM][BK + PAD];
@@ -537,8 +543,9 @@ k_mm_bf16(const uint16_t* __restrict__ x, int64_t ldx, const int32_t* __restrict
   const int64_t am = m0 + ar;
   const bool arow_ok = am < M;
   const int64_t asrc = arow_ok ? (row_idx ? static_cast<int64_t>(row_idx[am]) : am) : 0;
-  const uint16_t* ap = x + asrc * ldx;
-  const bool avec = ((ldx & 7) == 0) && aligned(x, 16);
+  const TA* ap = x + asrc * ldx;
+  constexpr bool kBf16A = sizeof(TA) == 2;
+  const bool avec = kBf16A && ((ldx & 7) == 0) && aligned(x, 16);
   const int bk = t >> 3, bn = (t & 7) * 8;  // B: 32 k x 64 n, 8 per thread
 
   for (int k0 = 0; k0 < K; k0 += BK) {
@@ -548,7 +555,7 @@ k_mm_bf16(const uint16_t* __restrict__ x, int64_t ldx, const int32_t* __restrict
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         const int k = k0 + ak + q;
-        As[ar][ak + q] = (arow_ok && k < K) ? ap[k] : static_cast<uint16_t>(0);
+        As[ar][ak + q] = (arow_ok && k < K) ? to_bf16_bits(ap[k]) : static_cast<uint16_t>(0);
       }
     }
 #pragma unroll
@@ -865,9 +872,13 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
                                                    static_cast<int>(K), static_cast<const float*>(w), ldw,
                                                    static_cast<int>(N), sf, out, ldo);
   } else if (dtype == GTA_BF16) {
-    k_mm_bf16<<<grid, dim3(kBlock), 0, S(stream)>>>(static_cast<const uint16_t*>(x), ldx, row_idx, M,
-                                                    static_cast<int>(K), static_cast<const uint16_t*>(w), ldw,
-                                                    static_cast<int>(N), sf, out, ldo);
+    k_mm_bf16<uint16_t><<<grid, dim3(kBlock), 0, S(stream)>>>(static_cast<const uint16_t*>(x), ldx, row_idx, M,
+                                                              static_cast<int>(K), static_cast<const uint16_t*>(w),
+                                                              ldw, static_cast<int>(N), sf, out, ldo);
+  } else if (dtype == GTA_F32_BF16) {
+    k_mm_bf16<float><<<grid, dim3(kBlock), 0, S(stream)>>>(static_cast<const float*>(x), ldx, row_idx, M,
+                                                           static_cast<int>(K), static_cast<const uint16_t*>(w), ldw,
+                                                           static_cast<int>(N), sf, out, ldo);
   } else {
     return fail(GTA_ERR_ARG, "update_mm: bad dtype");
   }

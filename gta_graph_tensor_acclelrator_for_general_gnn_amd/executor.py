@@ -58,6 +58,20 @@ class Deferred:
         self.op = op
 
 
+class Lazy:
+    """An intermediate whose only consumer was fused with it (e.g. an SF post-op);
+    computed on demand if anything else ever asks for it."""
+    __slots__ = ("fn", "v")
+
+    def __init__(self, fn):
+        self.fn, self.v = fn, None
+
+    def force(self):
+        if self.v is None:
+            self.v = self.fn()
+        return self.v
+
+
 class ExecResult:
     """Real outputs + measured time, and the reference's modelled (cycles, rw) for the same stream."""
 
@@ -91,6 +105,16 @@ class Executor:
         self.values = {}
         self.alg_bytes = 0
         self.launches = 0
+        # execution-level fusion beyond the stream's (results bitwise unchanged):
+        #   elide_scatter_stores: a STORE_E'd scatter read back by a later block is read by index
+        #   fuse_sf: an SF whose producer feeds only it runs as the producer's post-op
+        self.elide_scatter_stores = True
+        self.fuse_sf = True
+        self.consumers = {i: [] for i in range(len(opgraph))}
+        for i in range(len(opgraph)):
+            for src in opgraph.inputs[i]:
+                if src.kind == "op":
+                    self.consumers[src.op].append(i)
 
     # ---------------------------------------------------------------- inputs
     def _ext(self, op, slot):
@@ -101,7 +125,8 @@ class Executor:
         if src.kind == "op":
             if src.op not in self.values:
                 raise RuntimeError(f"op {op.idx} reads op {src.op} before it was produced")
-            return self.values[src.op]
+            v = self.values[src.op]
+            return v.force() if isinstance(v, Lazy) else v
         t = self._ext(op, slot)
         if src.kind == "ext":
             if t is None:
@@ -172,11 +197,11 @@ class Executor:
         b = self.sem.bin_of(op)
         return b
 
-    def _eval_applyedge(self, op, fused):
+    def _eval_applyedge(self, op, fused=False, post_sf=None):
         ins = self._inputs(op)
         E = self.graph.nnz
         if op.comp == "MM":
-            return EdgeT(self._edge_mm(op, ins[0]))
+            return EdgeT(self._edge_mm(op, ins[0], post_sf))
         if op.comp == "SF":
             a, am, _ = self._edge_operand(ins[0])
             out = ops.apply_edge(self.graph, None, self.sem.sf_of(op), a, am)
@@ -199,11 +224,11 @@ class Executor:
             else:
                 a = self._to_edge_tensor(("row", a)) if False else a.expand(E, a.shape[1]).contiguous()
                 am, arow = "edge", False
-        out = ops.apply_edge(self.graph, bin_, None, a, am, b, bm, b_broadcast_row=brow)
+        out = ops.apply_edge(self.graph, bin_, post_sf, a, am, b, bm, b_broadcast_row=brow)
         self._count(E * out.shape[1] * 4 * 3)
         return EdgeT(out)
 
-    def _edge_mm(self, op, v):
+    def _edge_mm(self, op, v, post_sf=None):
         W = self.tensors[f"w:{op.idx}"]
         if isinstance(v, Scat):
             idx = self.graph.indices if v.mode == "src" else self.graph.row_of_edge()
@@ -211,14 +236,14 @@ class Executor:
         else:
             x, row_idx = self._to_edge_tensor(v), None
         x, W = self._mm_dtypes(x, W)
-        out = ops.update_mm(x, W, row_idx, m=self.graph.nnz if row_idx is None else None)
+        out = ops.update_mm(x, W, row_idx, sf=post_sf, m=self.graph.nnz if row_idx is None else None)
         self._count(self.graph.nnz * (x.shape[1] * x.element_size() + W.shape[1] * 4))
         return out
 
     @staticmethod
     def _mm_dtypes(x, W):
-        if W.dtype == torch.bfloat16 and x.dtype != torch.bfloat16:
-            x = x.to(torch.bfloat16)
+        # fp32 activations with bf16 weights go straight in: the GEMM rounds x to bf16
+        # while staging it into LDS (GTA_F32_BF16); only bf16 x with fp32 W is widened
         if W.dtype == torch.float32 and x.dtype != torch.float32:
             x = x.float()
         return x, W
@@ -287,14 +312,14 @@ class Executor:
             return ops.aggregate(self.graph, x.t, x.mode, None, plan=self._plan())
         return ops.aggregate(self.graph, self._to_edge_tensor(x), "edge", None, plan=self._plan())
 
-    def _eval_applynode(self, op):
+    def _eval_applynode(self, op, post_sf=None):
         ins = self._inputs(op)
         n = self.graph.n_rows
         if op.comp == "MM":
             W = self.tensors[f"w:{op.idx}"]
             x = self._node(ins[0])
             x, W = self._mm_dtypes(x, W)
-            y = ops.update_mm(x, W)
+            y = ops.update_mm(x, W, sf=post_sf)
             self._count(n * (x.shape[1] * x.element_size() + W.shape[1] * 4) + W.numel() * W.element_size())
             return NodeT(y)
         if op.comp == "SF":
@@ -316,7 +341,7 @@ class Executor:
         a = self._node(x)
         brow = isinstance(y, tuple)
         b = y[1] if brow else self._node(y)
-        out = ops.apply_node(bin_, None, a, b, b_broadcast_row=brow)
+        out = ops.apply_node(bin_, post_sf, a, b, b_broadcast_row=brow)
         self._count(n * out.shape[1] * 4 * 3)
         return NodeT(out)
 
@@ -336,19 +361,41 @@ class Executor:
             if not isinstance(v, NodeT):
                 raise TypeError(f"scatter op {op.idx} needs a node tensor")
             s = Scat(v.t, "src" if op.order == "C" else "dst")
-            if op.idx in block.stored:
+            # a STORE_E'd scatter is only materialised when nothing reads it back (a sink):
+            # every consumer kernel gathers by index, which is the same bytes
+            if op.idx in block.stored and not (self.elide_scatter_stores and self.consumers[op.idx]):
                 return EdgeT(self._to_edge_tensor(s))
             return s
         if op.type == "applyedge":
             c = fused_into.get(op.idx)
             if c is not None and self.g.ops[c].type == "gather" and op.comp in ("MUL", "MM"):
                 return Deferred(op.idx)
-            return self._eval_applyedge(op, fused=False)
+        sf_child = self._sf_child(op, block)
+        if sf_child is not None:
+            ev = self._eval_applyedge if op.type == "applyedge" else self._eval_applynode
+            self.values[sf_child.idx] = ev(op, post_sf=self.sem.sf_of(sf_child))
+            return Lazy(lambda: ev(op))
+        if op.type == "applyedge":
+            return self._eval_applyedge(op)
         if op.type == "gather":
             return self._eval_gather(op)
         if op.type == "applynode":
             return self._eval_applynode(op)
         raise ValueError(op.type)
+
+    def _sf_child(self, op, block):
+        """The SF op this op's output feeds exclusively (same kind, same block), if fusable."""
+        if not self.fuse_sf or op.type not in ("applyedge", "applynode") or op.comp == "SF" or not op.out_list:
+            return None
+        cons = self.consumers[op.idx]
+        if len(cons) != 1:
+            return None
+        c = self.g.ops[cons[0]]
+        if c.comp != "SF" or c.type != op.type or c.idx not in block.ops:
+            return None
+        if op.comp in ("ADD", "MUL") and len(self.g.inputs[op.idx]) < 2 and self._ext(op, 1) is None:
+            return None  # identity pass-through: no kernel to carry the post-op
+        return c
 
     # ---------------------------------------------------------------- run
     def block_order(self):
@@ -385,6 +432,8 @@ class Executor:
         for bi in self.block_order():
             block = self.stream.blocks[bi]
             for i in self.g.topo(block.ops):
+                if i in self.values:  # produced early as a fused post-op
+                    continue
                 self.values[i] = self._eval(self.g.ops[i], block)
         outputs = {}
         for op in self.g.ops:
@@ -394,6 +443,8 @@ class Executor:
         return outputs
 
     def _final(self, v):
+        if isinstance(v, Lazy):
+            v = v.force()
         if isinstance(v, (NodeT, EdgeT)):
             return v.t
         if isinstance(v, Scat):

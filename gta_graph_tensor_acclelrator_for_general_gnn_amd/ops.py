@@ -221,12 +221,14 @@ def apply_node(bin, sf, a, b=None, out=None, b_broadcast_row=False):
 
 
 def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
-    """out[m] = sf(x[r(m)] . w); x, w both float32 or both bfloat16; out float32.
+    """out[m] = sf(x[r(m)] . w); x/w float32, bfloat16, or float32 x with bfloat16 w (x rounded
+    to bf16 on its way into LDS); out float32.
 
     row_idx: None (r(m) = m, M = x.shape[0]) or int32 [M] of x rows (gather-GEMM)."""
     _need_gpu(x, w, row_idx, out)
-    if x.dtype != w.dtype or x.dtype not in (torch.float32, torch.bfloat16):
-        raise TypeError("update_mm: x and w must both be float32 or both bfloat16")
+    mixed = x.dtype == torch.float32 and w.dtype == torch.bfloat16
+    if not mixed and (x.dtype != w.dtype or x.dtype not in (torch.float32, torch.bfloat16)):
+        raise TypeError("update_mm: x/w must be f32/f32, bf16/bf16, or f32 x with bf16 w")
     ldx = _rows(x, "x", x.dtype)
     ldw = _rows(w, "w", w.dtype)
     K, N = w.shape
@@ -241,7 +243,7 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
     if out is None:
         out = torch.empty(M, N, dtype=torch.float32, device=x.device)
     ldo = _rows(out, "out")
-    dt = _lib.GTA_F32 if x.dtype == torch.float32 else _lib.GTA_BF16
+    dt = _lib.GTA_F32_BF16 if mixed else (_lib.GTA_F32 if x.dtype == torch.float32 else _lib.GTA_BF16)
     check(_L().gta_update_mm(_ptr(x), ldx, _ptr(row_idx), M, K, _ptr(w), ldw, N, dt, _sf(sf), _ptr(out), ldo,
                              _stream(x.device)), "update_mm")
     return out

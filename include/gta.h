@@ -42,8 +42,9 @@ extern "C" {
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
 
-/* dtypes */
-enum { GTA_F32 = 0, GTA_BF16 = 1 };
+/* dtypes; GTA_F32_BF16 (update_mm only): fp32 x rounded to bf16 (RNE) as it is
+ * staged into LDS, bf16 W -- no separate cast pass over x */
+enum { GTA_F32 = 0, GTA_BF16 = 1, GTA_F32_BF16 = 2 };
 
 /* Scatter direction (reference ISA `scatter` DIRECTION dst/src,
  * template/ISA_defination.yaml:33-44; op ORDER R/C in the op YAML). */
@@ -135,7 +136,7 @@ int gta_apply_node(int bin, int sf, int64_t n, const float* a, int64_t lda, int6
 
 /* ---- K4 UPDATE / MVM on MFMA (applynode MM, applyedge MM) -------------
  * out[m, :] = sf( x[r(m), :] . W )   x: [*, K] (dtype), W: [K, N] row-major
- * (dtype), out: [M, N] fp32.  row_idx NULL => r(m) = m, else r(m) =
+ * (dtype; GTA_F32_BF16 = fp32 x, bf16 W), out: [M, N] fp32.  row_idx NULL => r(m) = m, else r(m) =
  * row_idx[m] (the fused [scatter, applyedge] (NONE,MM) gather-GEMM).
  * fp32 runs on v_mfma_f32_16x16x4_f32 (exact f32), bf16 on
  * v_mfma_f32_16x16x32_bf16 with fp32 accumulation.

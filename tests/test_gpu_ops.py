@@ -209,3 +209,16 @@ def test_plan_items_and_splits(dev):
     chunks = np.where(deg <= 256, 1, -(-deg // 256))
     assert p.n_items() == int(chunks.sum())
     assert p.n_split() == int((deg > 256).sum())
+
+
+@pytest.mark.parametrize("M,K,N", [(2449, 100, 128), (1000, 602, 128), (333, 37, 50)])
+def test_update_mm_f32_x_bf16_w(dev, M, K, N):
+    """GTA_F32_BF16: fp32 x is rounded to bf16 (RNE) while staged; reference = fp64 of the rounded inputs."""
+    rng = np.random.default_rng(K + 7)
+    x = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32))
+    w = torch.from_numpy(rng.standard_normal((K, N)).astype(np.float32)).to(torch.bfloat16)
+    out = ops.update_mm(x.to(dev), w.to(dev), sf="RELU")
+    xr = x.to(torch.bfloat16).float().numpy()
+    wf = w.float().numpy()
+    ref = isa_ref.mm(xr, wf, sf_kind="RELU")
+    _check(out, ref, np.abs(xr).astype(np.float64) @ np.abs(wf).astype(np.float64), "update_mm f32xbf16")
