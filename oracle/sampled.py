@@ -32,6 +32,8 @@ class SampledChecker:
     def value_at(self, v, kind, idx):
         """Rows idx (node or edge ids) of an executor value object."""
         from gta_graph_tensor_acclelrator_for_general_gnn_amd import executor as X
+        if isinstance(v, X.Lazy):
+            v = v.force()
         if isinstance(v, X.NodeT):
             if kind != "node":
                 raise TypeError("node value read per edge")
@@ -102,6 +104,8 @@ class SampledChecker:
             if op.idx in skip_ops:
                 continue
             v = self.ex.values.get(op.idx)
+            if isinstance(v, X.Lazy):  # fused-away intermediate: materialise it to check it too
+                v = v.force()
             if not isinstance(v, (X.NodeT, X.EdgeT)):
                 continue
             kind = "node" if isinstance(v, X.NodeT) else "edge"
