@@ -356,6 +356,223 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
   }
 }
 
+// ---------------------------------------------------------------------------
+// Lean aggregate for rows that exactly fill a wavefront (F = 64 * VW): one edge
+// per wave instruction, wave-uniform row base.  Per unrolled step of U edges:
+//   * U row loads issued back to back, no per-edge validity select (full steps
+//     only; the < U remainder runs a separate one-edge loop);
+//   * weights (heads mode, GL = lanes per head = (F/H)/VW) come in ONE coalesced
+//     load per GL edges in a head-transposed layout -- lane l holds
+//     w[e0 + (l % GL), l / GL], i.e. its own head for GL different edges -- and
+//     each edge's weight reaches its head's lanes by a ds_swizzle broadcast
+//     inside the GL-lane group (no memory traffic, no VMEM per edge);
+//   * fma accumulation in edge order (deterministic).
+// GL = 0: unweighted.
+// ---------------------------------------------------------------------------
+template <int G, int K>
+__device__ __forceinline__ float group_bcast(float v) {  // lane (l & ~(G-1)) | K of each G-lane group
+  constexpr int pattern = (0x1F & ~(G - 1)) | ((K % G) << 5);
+  return __builtin_bit_cast(float, __builtin_amdgcn_ds_swizzle(__builtin_bit_cast(int, v), pattern));
+}
+
+template <int G, int U>
+__device__ __forceinline__ void bcast_all(const float* wa, float* out) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const float v = wa[u / G];
+    switch (u % G) {  // ds_swizzle needs a literal pattern
+#define GTA_BC(k) case k: out[u] = group_bcast<G, k>(v); break;
+      GTA_BC(0) GTA_BC(1) GTA_BC(2) GTA_BC(3) GTA_BC(4) GTA_BC(5) GTA_BC(6) GTA_BC(7)
+      GTA_BC(8) GTA_BC(9) GTA_BC(10) GTA_BC(11) GTA_BC(12) GTA_BC(13) GTA_BC(14) GTA_BC(15)
+#undef GTA_BC
+    }
+  }
+}
+
+// Column-blocked form (SEG = true): launch b of B handles, for every row (heaviest
+// first, `perm`), only its edges whose source lies in column block b --
+// seg[r][b] .. seg[r][b+1] within the row's sorted column list -- and adds the
+// partial into y[r] (the first launch writes).  All waves of a launch gather
+// from one n_cols/B slice of X, which stays resident in each XCD's 4 MB L2.
+struct SegView {
+  const int32_t* perm;  // rows, heaviest first
+  const int32_t* seg;   // [n_rows][B+1] offsets within each row
+  int B;
+  int b;
+};
+
+template <int VW, int GL, bool SEG>
+__global__ void __launch_bounds__(kBlock)
+k_agg_lean(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows, PlanView plan,
+           int use_plan, int64_t chunk, const float* __restrict__ x, int64_t ldx, int F,
+           const float* __restrict__ w, int64_t ldw, const float* __restrict__ row_scale,
+           float* __restrict__ y, int64_t ldy, int accumulate, float* __restrict__ partial, SegView sv) {
+  constexpr int U = (GL > 8) ? GL : 8;               // edges per unrolled step
+  constexpr int NWL = (GL > 0) ? U / GL : 0;         // weight loads per step
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t item = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  const int64_t n_items = (use_plan && !SEG) ? plan.hdr[0] : n_rows;
+  if (item >= n_items) return;
+  int64_t row, eb, ee;
+  bool split = false;
+  if (SEG) {
+    row = sv.perm[item];
+    const int32_t* sg = sv.seg + row * (sv.B + 1);
+    const int64_t base = indptr[row];
+    eb = base + sg[sv.b];
+    ee = base + sg[sv.b + 1];
+    if (sv.b > 0) {
+      if (eb == ee) return;  // nothing of this row in this column block
+      accumulate = 1;
+    }
+  } else if (use_plan) {
+    row = plan.item_row[item];
+    eb = plan.item_beg[item];
+    const int64_t rb = indptr[row], re = indptr[row + 1];
+    ee = min(eb + chunk, re);
+    split = (re - rb) > chunk;
+  } else {
+    row = item;
+    eb = indptr[row];
+    ee = indptr[row + 1];
+  }
+  const int col = lane * VW;
+  const int head = (GL > 0) ? lane / GL : 0;      // this lane's head (F/H = GL * VW columns)
+  const int gsub = (GL > 0) ? lane % GL : 0;      // which edge of a GL-block this lane loads the weight of
+  float acc[VW];
+#pragma unroll
+  for (int k = 0; k < VW; ++k) acc[k] = 0.f;
+
+  int idxv = (eb < ee) ? indices[min(eb + lane, ee - 1)] : 0;
+  for (int64_t e0 = eb; e0 < ee; e0 += kWave) {
+    const int n = static_cast<int>(min<int64_t>(kWave, ee - e0));
+    const int idxn = indices[min(e0 + kWave + lane, ee - 1)];  // prefetch next block (clamped)
+    const float* wblk = (GL > 0) ? w + e0 * ldw : nullptr;
+    int s = 0;
+    for (; s + U <= n; s += U) {
+      Vec<VW> xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t xr = __builtin_amdgcn_readlane(idxv, s + u);
+        xv[u].load(x + xr * ldx + col);
+      }
+      if (GL > 0) {
+        float wa[NWL > 0 ? NWL : 1], wu[U];
+#pragma unroll
+        for (int q = 0; q < NWL; ++q) wa[q] = wblk[static_cast<int64_t>(s + q * GL + gsub) * ldw + head];
+        bcast_all<(GL > 0 ? GL : 1), U>(wa, wu);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int k = 0; k < VW; ++k) acc[k] = fmaf(wu[u], xv[u].v[k], acc[k]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int k = 0; k < VW; ++k) acc[k] += xv[u].v[k];
+      }
+    }
+    for (; s < n; ++s) {  // remainder, one edge at a time
+      const int64_t xr = __builtin_amdgcn_readlane(idxv, s);
+      Vec<VW> xv;
+      xv.load(x + xr * ldx + col);
+      const float wv = (GL > 0) ? wblk[static_cast<int64_t>(s) * ldw + head] : 1.f;
+#pragma unroll
+      for (int k = 0; k < VW; ++k) acc[k] = (GL > 0) ? fmaf(wv, xv.v[k], acc[k]) : acc[k] + xv.v[k];
+    }
+    idxv = idxn;
+  }
+  Vec<VW> o;
+  if (split) {
+#pragma unroll
+    for (int k = 0; k < VW; ++k) o.v[k] = acc[k];
+    o.store(partial + item * static_cast<int64_t>(F) + col);
+  } else {
+    const float scale = row_scale ? row_scale[row] : 1.f;
+    float* yp = y + row * ldy + col;
+    if (accumulate) {
+      Vec<VW> old;
+      old.load(yp);
+#pragma unroll
+      for (int k = 0; k < VW; ++k) o.v[k] = old.v[k] + scale * acc[k];
+    } else {
+#pragma unroll
+      for (int k = 0; k < VW; ++k) o.v[k] = scale * acc[k];
+    }
+    o.store(yp);
+  }
+}
+
+// ---- column-blocked plan: segment table + heavy-first row order -----------
+// layout: int64 hdr[8] {B, bsize, n_rows, unsorted_flag}, int32 perm[n_rows],
+//         int32 seg[n_rows*(B+1)], int32 bucket[64] (count, offset)
+struct BlockedView {
+  int64_t* hdr;
+  int32_t* perm;
+  int32_t* seg;
+  int32_t* bucket;
+};
+
+BlockedView blocked_view(void* base, int64_t n_rows, int B) {
+  char* p = static_cast<char*>(base);
+  BlockedView v;
+  v.hdr = reinterpret_cast<int64_t*>(p); p += round16(8 * 8);
+  v.perm = reinterpret_cast<int32_t*>(p); p += round16(n_rows * 4);
+  v.seg = reinterpret_cast<int32_t*>(p); p += round16(n_rows * (B + 1) * 4);
+  v.bucket = reinterpret_cast<int32_t*>(p);
+  return v;
+}
+
+int64_t blocked_bytes(int64_t n_rows, int B) {
+  return round16(64) + round16(n_rows * 4) + round16(n_rows * (B + 1) * 4) + round16(64 * 4);
+}
+
+__device__ __forceinline__ int deg_bucket(int64_t d) {  // 31 = heaviest ... 0 = empty/1
+  return d <= 1 ? 0 : min(31, 63 - __clzll(static_cast<unsigned long long>(d)));
+}
+
+// one wave per row: lane b (0..B) binary-searches the first edge with col >= b*bsize;
+// all lanes also verify the row's columns are sorted (the segments need it)
+__global__ void __launch_bounds__(kBlock)
+k_blocked_seg(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows, int B,
+              int64_t bsize, BlockedView v) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  const int64_t rb = indptr[row], re = indptr[row + 1];
+  for (int b = lane; b <= B; b += kWave) {
+    const int64_t key = static_cast<int64_t>(b) * bsize;
+    int64_t lo = rb, hi = re;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) >> 1;
+      if (static_cast<int64_t>(indices[mid]) < key) lo = mid + 1; else hi = mid;
+    }
+    v.seg[row * (B + 1) + b] = static_cast<int32_t>((b == B ? re : lo) - rb);
+  }
+  bool bad = false;
+  for (int64_t e = rb + lane; e + 1 < re; e += kWave) bad |= indices[e] > indices[e + 1];
+  if (__any(bad) && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(&v.hdr[3]), 1ull);
+  if (lane == 0) atomicAdd(&v.bucket[deg_bucket(re - rb)], 1);
+}
+
+__global__ void k_blocked_scan(BlockedView v) {  // heaviest bucket first
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int k = 31; k >= 0; --k) {
+      v.bucket[32 + k] = run;
+      run += v.bucket[k];
+    }
+  }
+}
+
+__global__ void k_blocked_perm(const int64_t* __restrict__ indptr, int64_t n_rows, BlockedView v) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (r >= n_rows) return;
+  const int k = deg_bucket(indptr[r + 1] - indptr[r]);
+  const int pos = atomicAdd(&v.bucket[32 + k], 1);  // order inside a bucket is free: results don't depend on it
+  v.perm[pos] = static_cast<int32_t>(r);
+}
+
 // sum the chunk partials of split rows, in chunk order
 __global__ void __launch_bounds__(kBlock)
 k_aggregate_combine(PlanView plan, int F, const float* __restrict__ row_scale, float* __restrict__ y, int64_t ldy,
@@ -661,6 +878,7 @@ bool dispatch_lpe(int lpe, int nv, int xm, int wm, bool nt, const AggArgs& a, in
 int g_force_lpe = 0;  // tuning hooks (gta_debug_set); 0 = automatic
 int g_force_vw = 0;
 int g_agg_nt = 0;     // non-temporal index/weight loads in the SpMM form
+int g_agg_lean = 1;   // k_agg_lean for F = 64*VW SpMM shapes
 
 }  // namespace
 
@@ -678,6 +896,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "agg_lpe") { g_force_lpe = static_cast<int>(value); return 0; }
   if (k == "agg_vw") { g_force_vw = static_cast<int>(value); return 0; }
   if (k == "agg_nt") { g_agg_nt = static_cast<int>(value); return 0; }
+  if (k == "agg_lean") { g_agg_lean = static_cast<int>(value); return 0; }
   return fail(GTA_ERR_ARG, "gta_debug_set: unknown key " + k);
 }
 
@@ -763,7 +982,28 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
   }
   hipStream_t s = S(stream);
   bool ok = false;
-  switch (vw) {
+  // lean path: one edge per instruction exactly filling the wave, SpMM form
+  int gl = (wm == WM_HEAD) ? gsz / vw : 0;
+  const bool lean_shape = g_agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
+                          !a.x_is_row && wm != WM_FULL && (wm == WM_NONE || gl == 4 || gl == 8 || gl == 16);
+  if (lean_shape) {
+    const int64_t blocks = (bound + kWavesPerBlock - 1) / kWavesPerBlock;
+    const dim3 grid(static_cast<unsigned>(blocks)), blk(kBlock);
+#define GTA_LEAN(VW_, GL_)                                                                                   \
+  k_agg_lean<VW_, GL_, false><<<grid, blk, 0, s>>>(a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, \
+                                                   a.x, a.ldx, a.F, a.w, a.ldw, a.row_scale, a.y, a.ldy,        \
+                                                   a.accumulate, a.partial, SegView{})
+    if (vw == 2) {
+      if (gl == 0) GTA_LEAN(2, 0); else if (gl == 4) GTA_LEAN(2, 4); else if (gl == 8) GTA_LEAN(2, 8); else GTA_LEAN(2, 16);
+    } else if (vw == 4) {
+      if (gl == 0) GTA_LEAN(4, 0); else if (gl == 4) GTA_LEAN(4, 4); else if (gl == 8) GTA_LEAN(4, 8); else GTA_LEAN(4, 16);
+    } else {
+      if (gl == 0) GTA_LEAN(1, 0); else if (gl == 4) GTA_LEAN(1, 4); else if (gl == 8) GTA_LEAN(1, 8); else GTA_LEAN(1, 16);
+    }
+#undef GTA_LEAN
+    ok = true;
+  }
+  if (!ok) switch (vw) {
     case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, g_agg_nt != 0, a, bound, s); break;
     case 2: ok = dispatch_lpe<2>(lpe, nv, xm, wm, g_agg_nt != 0, a, bound, s); break;
     default: ok = dispatch_lpe<1>(lpe, nv, xm, wm, g_agg_nt != 0, a, bound, s); break;
@@ -778,6 +1018,76 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
           a.plan, a.F, row_scale, y, ldy, accumulate, a.partial);
       GTA_LAUNCHED("k_aggregate_combine");
     }
+  }
+  return GTA_OK;
+}
+
+int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t blocks) {
+  if (n_rows < 0 || blocks < 1 || blocks > 63) return fail(GTA_ERR_ARG, "blocked_plan_bytes: need 1 <= blocks <= 63");
+  return blocked_bytes(n_rows, static_cast<int>(blocks));
+}
+
+int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
+                                     int64_t blocks, void* plan, int64_t plan_bytes, void* stream) {
+  if (!indptr || !indices || !plan || n_rows <= 0 || n_cols <= 0 || blocks < 1 || blocks > 63)
+    return fail(GTA_ERR_ARG, "blocked_plan_build: bad arguments");
+  if (n_rows > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "blocked_plan_build: > 2^31 rows");
+  const int B = static_cast<int>(blocks);
+  if (plan_bytes < blocked_bytes(n_rows, B)) return fail(GTA_ERR_ARG, "blocked_plan_build: plan buffer too small");
+  BlockedView v = blocked_view(plan, n_rows, B);
+  hipStream_t s = S(stream);
+  const int64_t bsize = (n_cols + B - 1) / B;
+  GTA_HIP(hipMemsetAsync(v.hdr, 0, 64, s));
+  GTA_HIP(hipMemsetAsync(v.bucket, 0, 64 * 4, s));
+  k_blocked_seg<<<dim3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0, s>>>(
+      indptr, indices, n_rows, B, bsize, v);
+  GTA_LAUNCHED("k_blocked_seg");
+  k_blocked_scan<<<1, 64, 0, s>>>(v);
+  GTA_LAUNCHED("k_blocked_scan");
+  k_blocked_perm<<<dim3(static_cast<unsigned>((n_rows + 255) / 256)), dim3(256), 0, s>>>(indptr, n_rows, v);
+  GTA_LAUNCHED("k_blocked_perm");
+  return GTA_OK;
+}
+
+int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
+                          const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
+                          const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
+                          int64_t blocks, void* stream) {
+  if (!indptr || !indices || !x || !y || !plan || n_rows < 0 || F <= 0 || blocks < 1 || blocks > 63)
+    return fail(GTA_ERR_ARG, "aggregate_blocked: bad arguments");
+  if (n_rows == 0) return GTA_OK;
+  int gl = 0, vw = 0;
+  for (int c : {4, 2, 1}) {
+    if (F == static_cast<int64_t>(kWave) * c && ldx % c == 0 && ldy % c == 0 && aligned(x, 4 * c) && aligned(y, 4 * c)) {
+      vw = c;
+      break;
+    }
+  }
+  if (!vw) return fail(GTA_ERR_UNSUPPORTED, "aggregate_blocked: F must be 64, 128 or 256 (one edge per wave row)");
+  if (w) {
+    if (heads <= 0 || F % heads) return fail(GTA_ERR_ARG, "aggregate_blocked: heads must divide F");
+    gl = static_cast<int>(F / heads) / vw;
+    if ((F / heads) % vw || (gl != 4 && gl != 8 && gl != 16))
+      return fail(GTA_ERR_UNSUPPORTED, "aggregate_blocked: (F/heads)/VW must be 4, 8 or 16");
+  }
+  const int B = static_cast<int>(blocks);
+  BlockedView v = blocked_view(const_cast<void*>(plan), n_rows, B);
+  hipStream_t s = S(stream);
+  const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock)), blk(kBlock);
+  for (int b = 0; b < B; ++b) {
+    SegView sv{v.perm, v.seg, B, b};
+#define GTA_LEANSEG(VW_, GL_)                                                                                      \
+  k_agg_lean<VW_, GL_, true><<<grid, blk, 0, s>>>(indptr, indices, n_rows, PlanView{}, 0, 0, x, ldx,              \
+                                                  static_cast<int>(F), w, ldw, row_scale, y, ldy, accumulate, nullptr, sv)
+    if (vw == 2) {
+      if (gl == 0) GTA_LEANSEG(2, 0); else if (gl == 4) GTA_LEANSEG(2, 4); else if (gl == 8) GTA_LEANSEG(2, 8); else GTA_LEANSEG(2, 16);
+    } else if (vw == 4) {
+      if (gl == 0) GTA_LEANSEG(4, 0); else if (gl == 4) GTA_LEANSEG(4, 4); else if (gl == 8) GTA_LEANSEG(4, 8); else GTA_LEANSEG(4, 16);
+    } else {
+      if (gl == 0) GTA_LEANSEG(1, 0); else if (gl == 4) GTA_LEANSEG(1, 4); else if (gl == 8) GTA_LEANSEG(1, 8); else GTA_LEANSEG(1, 16);
+    }
+#undef GTA_LEANSEG
+    GTA_LAUNCHED("k_agg_lean<seg>");
   }
   return GTA_OK;
 }

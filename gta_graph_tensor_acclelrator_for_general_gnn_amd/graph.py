@@ -67,6 +67,14 @@ class Graph:
             self._plans[chunk] = ops.AggregatePlan(self, chunk)
         return self._plans[chunk]
 
+    def blocked_plan(self, blocks=32):
+        """Cached column-blocked plan (segment table over `blocks` source-column blocks)."""
+        key = ("blocked", blocks)
+        if key not in self._plans:
+            from . import ops
+            self._plans[key] = ops.BlockedPlan(self, blocks)
+        return self._plans[key]
+
     def numpy(self):
         return self.indptr.cpu().numpy(), self.indices.cpu().numpy()
 

@@ -132,6 +132,62 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
     return out
 
 
+class BlockedPlan:
+    """Column-blocked aggregate plan: per-row segment table over B source-column blocks
+    + heaviest-first row order (gta_aggregate_blocked_plan_build)."""
+
+    def __init__(self, graph, blocks=32):
+        _need_gpu(graph.indptr)
+        L = _L()
+        self.graph, self.blocks = graph, int(blocks)
+        nb = check(L.gta_aggregate_blocked_plan_bytes(graph.n_rows, self.blocks), "blocked_plan_bytes")
+        self.buf = torch.empty(int(nb), dtype=torch.uint8, device=graph.device)
+        check(L.gta_aggregate_blocked_plan_build(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols,
+                                                 self.blocks, _ptr(self.buf), int(nb), _stream(graph.device)),
+              "blocked_plan_build")
+        self.sorted = int(self.buf[24:32].view(torch.int64).item()) == 0
+
+    @staticmethod
+    def supports(F, heads, x=None):
+        vw = F // 64 if F in (64, 128, 256) else 0
+        if not vw:
+            return False
+        if heads:
+            if F % heads or (F // heads) % vw:
+                return False
+            if (F // heads) // vw not in (4, 8, 16):
+                return False
+        return True
+
+
+def aggregate_blocked(graph, x, w=None, row_scale=None, out=None, accumulate=False, plan=None, blocks=32):
+    """Same result as aggregate(graph, x, "src", w, ...) via B column-block launches (L2-resident X slices)."""
+    _need_gpu(x, w, row_scale, out, graph.indptr)
+    F = x.shape[1]
+    ldx = _rows(x, "x")
+    if x.shape[0] < graph.n_cols:
+        raise ValueError("x must have n_cols rows")
+    ldw, heads = 0, 0
+    if w is not None:
+        if w.dim() == 1:
+            w = w.view(-1, 1)
+        ldw = _rows(w, "w")
+        heads = w.shape[1]
+    if not BlockedPlan.supports(F, heads):
+        raise ValueError(f"aggregate_blocked: unsupported F={F}, heads={heads}")
+    if plan is None:
+        plan = graph.blocked_plan(blocks)
+    if not plan.sorted:
+        raise ValueError("aggregate_blocked needs every CSR row's columns sorted")
+    if out is None:
+        out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=x.device)
+    ldy = _rows(out, "out")
+    check(_L().gta_aggregate_blocked(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols, _ptr(x), ldx,
+                                     F, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy, int(bool(accumulate)),
+                                     _ptr(plan.buf), plan.blocks, _stream(x.device)), "aggregate_blocked")
+    return out
+
+
 def gather_add(graph, xe, out=None, accumulate=False):
     """y[i] (+)= sum_{e in row i} xe[e]   (gather R, ADD)."""
     _need_gpu(xe, out, graph.indptr)

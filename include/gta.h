@@ -109,6 +109,24 @@ int gta_aggregate_plan_build(const int64_t* indptr, int64_t n_rows, int64_t nnz,
                              void* plan, int64_t plan_bytes, void* stream);
 int64_t gta_aggregate_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t chunk, int64_t F);
 
+/* ---- K6 column-blocked form (L2-resident source slices) -----------------
+ * Same y as gta_aggregate (x_mode SRC, w NULL or heads), computed as B launches:
+ * launch b adds, for every row, the edges whose source column lies in
+ * [b*ceil(n_cols/B), (b+1)*ceil(n_cols/B)), so all waves of a launch gather from
+ * one X slice that stays resident in each XCD's 4 MB L2 -- the reference's own
+ * T-row x column tiling (code/preprocessing.py:26-38, interpreter TC) with the
+ * column axis outermost.  Needs each CSR row's columns sorted (the plan build
+ * flags unsorted rows in plan header word 3) and F = 64*VW (64/128/256) with
+ * (F/heads)/VW in {4, 8, 16}.  Deterministic (fixed block order, no atomics);
+ * row_scale is applied per block.  1 <= blocks <= 63. */
+int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t blocks);
+int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
+                                     int64_t blocks, void* plan, int64_t plan_bytes, void* stream);
+int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
+                          const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
+                          const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
+                          int64_t blocks, void* stream);
+
 /* ---- K2 GATHER ADD (edge -> node) ---------------------------------------
  * y[i, :] (+)= sum_{e in row i} xe[e, :]    == gta_aggregate(x_mode=EDGE, w=NULL)
  * Reference: gather ISA template/ISA_defination.yaml:46-61; LOAD_E + Virtual

@@ -26,30 +26,48 @@ def main():
                                              "lpe64:c1024:nt,lpe64:c256")
     ap.add_argument("--n", type=int, default=bench.N_REDDIT)
     ap.add_argument("--e", type=int, default=bench.E_REDDIT)
-    ap.add_argument("--locality", action="store_true")
+    ap.add_argument("--slices", type=int, default=1, help="confine sources to n/slices nodes (L2 probe)")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     g, x, alpha = bench.make_inputs(args.n, args.e, dev)
+    if args.slices > 1:
+        from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G
+        g = G.Graph(g.indptr, torch.remainder(g.indices, args.n // args.slices).to(torch.int32).contiguous())
     y = torch.empty(g.n_rows, bench.F, device=dev)
     variants = []
     for v in args.variants.split(","):
         parts = v.split(":")
+        if parts[0].startswith("blk"):  # column-blocked path, B = blk<B>
+            variants.append((v, -int(parts[0][3:]), None, 0, 1))
+            continue
         lpe = int(parts[0].replace("lpe", ""))
         chunk = None if parts[1] == "none" else int(parts[1].replace("c", ""))
         nt = int("nt" in parts[2:])
-        variants.append((v, lpe, chunk, nt))
-    plans = {c: (g.plan(c) if c else None) for _, _, c, _ in variants}
+        lean = 0 if "lean0" in parts[2:] else 1
+        variants.append((v, lpe, chunk, nt, lean))
+    plans = {v[2]: (g.plan(v[2]) if v[2] else None) for v in variants}
+    for v in variants:
+        if v[1] < 0:
+            g.blocked_plan(-v[1])
     times = {v[0]: [] for v in variants}
     ref = None
     for r in range(args.rounds):
-        for name, lpe, chunk, nt in variants:
-            ops.set_debug("agg_lpe", lpe)
-            ops.set_debug("agg_nt", nt)
-            ops.aggregate(g, x, "src", alpha, out=y, plan=plans[chunk])  # warm
+        for name, lpe, chunk, nt, lean in variants:
+            if lpe < 0:
+                def run():
+                    ops.aggregate_blocked(g, x, alpha, out=y, blocks=-lpe)
+            else:
+                ops.set_debug("agg_lpe", lpe)
+                ops.set_debug("agg_nt", nt)
+                ops.set_debug("agg_lean", lean)
+
+                def run():
+                    ops.aggregate(g, x, "src", alpha, out=y, plan=plans[chunk])
+            run()  # warm
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             s.record()
             for _ in range(args.reps):
-                ops.aggregate(g, x, "src", alpha, out=y, plan=plans[chunk])
+                run()
             e.record()
             torch.cuda.synchronize()
             times[name].append(s.elapsed_time(e) / args.reps)
@@ -68,7 +86,7 @@ def main():
         print(f"{name:16s} median {med:7.3f} ms  min {out[name]['min_ms']:7.3f}  "
               f"{out[name]['alg_GBps']:7.0f} GB/s alg  {out[name]['edges_per_s']/1e9:6.2f} Gedges/s", flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "agg_sweep.json"), "w") as f:
+    with open(os.path.join(ROOT, "gpurun_out", f"agg_sweep_s{args.slices}.json"), "w") as f:
         json.dump(out, f, indent=1)
 
 

@@ -222,3 +222,53 @@ def test_update_mm_f32_x_bf16_w(dev, M, K, N):
     wf = w.float().numpy()
     ref = isa_ref.mm(xr, wf, sf_kind="RELU")
     _check(out, ref, np.abs(xr).astype(np.float64) @ np.abs(wf).astype(np.float64), "update_mm f32xbf16")
+
+
+@pytest.mark.parametrize("F,heads", [(128, 8), (128, 16), (128, 4), (64, 4), (256, 16), (128, 0), (64, 0)])
+@pytest.mark.parametrize("blocks", [1, 7, 32, 63])
+def test_aggregate_blocked_matches_oracle(dev, F, heads, blocks):
+    """Column-blocked K6 (B launches over source-column slices) == fp64 oracle; rows must be column-sorted."""
+    n, e = 700, 20000
+    g0 = G.synthetic(n, e, seed=blocks + F, device="cpu")          # sorted columns
+    ip, ix = g0.numpy()
+    deg = np.diff(ip).copy()
+    deg[5] = 3000                                                   # heavy row, more edges than a block slice
+    deg[[7, 8, 9]] = 0                                              # empty rows
+    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    rng = np.random.default_rng(blocks)
+    ix = np.concatenate([np.sort(rng.integers(0, n, d)) for d in deg]).astype(np.int32)
+    g = G.from_numpy(ip, ix, device=dev)
+    x = rng.standard_normal((n, F)).astype(np.float32)
+    w = rng.random((len(ix), heads)).astype(np.float32) if heads else None
+    y = ops.aggregate_blocked(g, torch.from_numpy(x).to(dev), None if w is None else torch.from_numpy(w).to(dev),
+                              blocks=blocks)
+    ref = isa_ref.aggregate(ip, ix, x, "src", w)
+    _check(y, ref, isa_ref.aggregate_abs(ip, ix, x, "src", w), f"blocked F={F} H={heads} B={blocks}")
+    y2 = ops.aggregate_blocked(g, torch.from_numpy(x).to(dev), None if w is None else torch.from_numpy(w).to(dev),
+                               blocks=blocks)
+    assert torch.equal(y, y2)
+
+
+def test_aggregate_blocked_accumulate_rowscale(dev):
+    n, e, F = 500, 9000, 128
+    g = G.synthetic(n, e, seed=3, device=dev)
+    ip, ix = g.numpy()
+    rng = np.random.default_rng(0)
+    x = rng.standard_normal((n, F)).astype(np.float32)
+    w = rng.random((g.nnz, 8)).astype(np.float32)
+    y0 = rng.standard_normal((n, F)).astype(np.float32)
+    sc = (rng.random(n) + 0.5).astype(np.float32)
+    yd = torch.from_numpy(y0).to(dev)
+    ops.aggregate_blocked(g, torch.from_numpy(x).to(dev), torch.from_numpy(w).to(dev),
+                          row_scale=torch.from_numpy(sc).to(dev), out=yd, accumulate=True, blocks=16)
+    ref = y0 + isa_ref.aggregate(ip, ix, x, "src", w, sc)
+    _check(yd, ref, isa_ref.aggregate_abs(ip, ix, x, "src", w, sc) + np.abs(y0), "blocked acc+scale")
+
+
+def test_aggregate_blocked_rejects_unsorted_rows(dev):
+    ip = np.array([0, 3, 5], dtype=np.int64)
+    ix = np.array([2, 0, 1, 1, 0], dtype=np.int32)
+    g = G.from_numpy(ip, ix, device=dev, n_cols=4)
+    x = torch.zeros(4, 128, device=dev)
+    with pytest.raises(ValueError):
+        ops.aggregate_blocked(g, x, None, blocks=2)
