@@ -503,6 +503,104 @@ k_agg_lean(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indic
   }
 }
 
+// Persistent column-blocked launch b: each wave walks rows it, it+W, it+2W, ...
+// (heaviest first), prefetching the next row's metadata (perm -> indptr, segment
+// bounds) one and two rows ahead so the dependent-load chain overlaps the current
+// row's gathers; y[row] old value is loaded at row start and added at the end.
+template <int VW, int GL>
+__global__ void __launch_bounds__(kBlock)
+k_agg_seg(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
+          const float* __restrict__ x, int64_t ldx, const float* __restrict__ w, int64_t ldw,
+          const float* __restrict__ row_scale, float* __restrict__ y, int64_t ldy, int accumulate, SegView sv) {
+  constexpr int U = (GL > 8) ? GL : 8;
+  constexpr int NWL = (GL > 0) ? U / GL : 0;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t W = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  const int64_t first = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  const int col = lane * VW;
+  const int head = (GL > 0) ? lane / GL : 0;
+  const int gsub = (GL > 0) ? lane % GL : 0;
+  const int S1 = sv.B + 1;
+  const bool acc_in = accumulate || sv.b > 0;
+  // pipeline: r1 = row of item it (meta loaded), r2 = row of item it+W (perm loaded)
+  int64_t it = first;
+  if (it >= n_rows) return;
+  int r1 = sv.perm[it];
+  int64_t b1 = indptr[r1];
+  int s1a = sv.seg[static_cast<int64_t>(r1) * S1 + sv.b], s1b = sv.seg[static_cast<int64_t>(r1) * S1 + sv.b + 1];
+  int r2 = (it + W < n_rows) ? sv.perm[it + W] : 0;
+  for (; it < n_rows; it += W) {
+    const int row = r1;
+    const int64_t eb = b1 + s1a, ee = b1 + s1b;
+    // prefetch: metadata of item it+W (row r2), perm of item it+2W
+    int64_t nb1 = 0;
+    int ns1a = 0, ns1b = 0, nr2 = 0;
+    if (it + W < n_rows) {
+      nb1 = indptr[r2];
+      ns1a = sv.seg[static_cast<int64_t>(r2) * S1 + sv.b];
+      ns1b = sv.seg[static_cast<int64_t>(r2) * S1 + sv.b + 1];
+      if (it + 2 * W < n_rows) nr2 = sv.perm[it + 2 * W];
+    }
+    if (eb < ee || !acc_in) {
+      float* yp = y + static_cast<int64_t>(row) * ldy + col;
+      Vec<VW> old;
+      if (acc_in) old.load(yp);
+      float acc[VW];
+#pragma unroll
+      for (int k = 0; k < VW; ++k) acc[k] = 0.f;
+      int idxv = (eb < ee) ? indices[min(eb + lane, ee - 1)] : 0;
+      for (int64_t e0 = eb; e0 < ee; e0 += kWave) {
+        const int n = static_cast<int>(min<int64_t>(kWave, ee - e0));
+        const int idxn = indices[min(e0 + kWave + lane, ee - 1)];
+        const float* wblk = (GL > 0) ? w + e0 * ldw : nullptr;
+        int s = 0;
+        for (; s + U <= n; s += U) {
+          Vec<VW> xv[U];
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const int64_t xr = __builtin_amdgcn_readlane(idxv, s + u);
+            xv[u].load(x + xr * ldx + col);
+          }
+          if (GL > 0) {
+            float wa[NWL > 0 ? NWL : 1], wu[U];
+#pragma unroll
+            for (int q = 0; q < NWL; ++q) wa[q] = wblk[static_cast<int64_t>(s + q * GL + gsub) * ldw + head];
+            bcast_all<(GL > 0 ? GL : 1), U>(wa, wu);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+              for (int k = 0; k < VW; ++k) acc[k] = fmaf(wu[u], xv[u].v[k], acc[k]);
+          } else {
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+              for (int k = 0; k < VW; ++k) acc[k] += xv[u].v[k];
+          }
+        }
+        for (; s < n; ++s) {
+          const int64_t xr = __builtin_amdgcn_readlane(idxv, s);
+          Vec<VW> xv;
+          xv.load(x + xr * ldx + col);
+          const float wv = (GL > 0) ? wblk[static_cast<int64_t>(s) * ldw + head] : 1.f;
+#pragma unroll
+          for (int k = 0; k < VW; ++k) acc[k] = (GL > 0) ? fmaf(wv, xv.v[k], acc[k]) : acc[k] + xv.v[k];
+        }
+        idxv = idxn;
+      }
+      const float scale = row_scale ? row_scale[row] : 1.f;
+      Vec<VW> o;
+#pragma unroll
+      for (int k = 0; k < VW; ++k) o.v[k] = (acc_in ? old.v[k] : 0.f) + scale * acc[k];
+      o.store(yp);
+    }
+    r1 = r2;
+    b1 = nb1;
+    s1a = ns1a;
+    s1b = ns1b;
+    r2 = nr2;
+  }
+}
+
 // ---- column-blocked plan: segment table + heavy-first row order -----------
 // layout: int64 hdr[8] {B, bsize, n_rows, unsorted_flag}, int32 perm[n_rows],
 //         int32 seg[n_rows*(B+1)], int32 bucket[64] (count, offset)
@@ -879,6 +977,7 @@ int g_force_lpe = 0;  // tuning hooks (gta_debug_set); 0 = automatic
 int g_force_vw = 0;
 int g_agg_nt = 0;     // non-temporal index/weight loads in the SpMM form
 int g_agg_lean = 1;   // k_agg_lean for F = 64*VW SpMM shapes
+int64_t g_seg_waves = 0;  // persistent waves of the column-blocked kernel (0 = 8 per SIMD)
 
 }  // namespace
 
@@ -897,6 +996,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "agg_vw") { g_force_vw = static_cast<int>(value); return 0; }
   if (k == "agg_nt") { g_agg_nt = static_cast<int>(value); return 0; }
   if (k == "agg_lean") { g_agg_lean = static_cast<int>(value); return 0; }
+  if (k == "seg_waves") { g_seg_waves = value; return 0; }
   return fail(GTA_ERR_ARG, "gta_debug_set: unknown key " + k);
 }
 
@@ -1073,12 +1173,14 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
   const int B = static_cast<int>(blocks);
   BlockedView v = blocked_view(const_cast<void*>(plan), n_rows, B);
   hipStream_t s = S(stream);
-  const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock)), blk(kBlock);
+  // persistent waves: enough for 8 per SIMD on every CU, never more than one per row
+  const int64_t waves = std::min<int64_t>(n_rows, g_seg_waves > 0 ? g_seg_waves : 256 * 32);
+  const dim3 grid(static_cast<unsigned>((waves + kWavesPerBlock - 1) / kWavesPerBlock)), blk(kBlock);
   for (int b = 0; b < B; ++b) {
     SegView sv{v.perm, v.seg, B, b};
-#define GTA_LEANSEG(VW_, GL_)                                                                                      \
-  k_agg_lean<VW_, GL_, true><<<grid, blk, 0, s>>>(indptr, indices, n_rows, PlanView{}, 0, 0, x, ldx,              \
-                                                  static_cast<int>(F), w, ldw, row_scale, y, ldy, accumulate, nullptr, sv)
+#define GTA_LEANSEG(VW_, GL_)                                                                        \
+  k_agg_seg<VW_, GL_><<<grid, blk, 0, s>>>(indptr, indices, n_rows, x, ldx, w, ldw, row_scale, y, ldy, \
+                                           accumulate, sv)
     if (vw == 2) {
       if (gl == 0) GTA_LEANSEG(2, 0); else if (gl == 4) GTA_LEANSEG(2, 4); else if (gl == 8) GTA_LEANSEG(2, 8); else GTA_LEANSEG(2, 16);
     } else if (vw == 4) {
@@ -1087,7 +1189,7 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
       if (gl == 0) GTA_LEANSEG(1, 0); else if (gl == 4) GTA_LEANSEG(1, 4); else if (gl == 8) GTA_LEANSEG(1, 8); else GTA_LEANSEG(1, 16);
     }
 #undef GTA_LEANSEG
-    GTA_LAUNCHED("k_agg_lean<seg>");
+    GTA_LAUNCHED("k_agg_seg");
   }
   return GTA_OK;
 }

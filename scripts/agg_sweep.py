@@ -37,8 +37,9 @@ def main():
     variants = []
     for v in args.variants.split(","):
         parts = v.split(":")
-        if parts[0].startswith("blk"):  # column-blocked path, B = blk<B>
-            variants.append((v, -int(parts[0][3:]), None, 0, 1))
+        if parts[0].startswith("blk"):  # column-blocked path, B = blk<B>[:w<persistent waves>]
+            wv = int(parts[1][1:]) if len(parts) > 1 and parts[1].startswith("w") else 0
+            variants.append((v, -int(parts[0][3:]), None, wv, 1))
             continue
         lpe = int(parts[0].replace("lpe", ""))
         chunk = None if parts[1] == "none" else int(parts[1].replace("c", ""))
@@ -54,6 +55,8 @@ def main():
     for r in range(args.rounds):
         for name, lpe, chunk, nt, lean in variants:
             if lpe < 0:
+                ops.set_debug("seg_waves", nt)
+
                 def run():
                     ops.aggregate_blocked(g, x, alpha, out=y, blocks=-lpe)
             else:
