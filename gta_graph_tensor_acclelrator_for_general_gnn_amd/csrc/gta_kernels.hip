@@ -601,6 +601,111 @@ k_agg_seg(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indice
   }
 }
 
+// Single-launch column-blocked form: item k = (b = k / n_rows, row = perm[k % n_rows]),
+// b-major, so the waves in flight at any moment gather from one or two X slices.
+// Each non-empty (b, row) segment writes its partial to slab b; k_seg_reduce sums
+// the non-empty slabs of each row in block order (deterministic, no atomics).
+template <int VW, int GL>
+__global__ void __launch_bounds__(kBlock)
+k_agg_seg2d(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
+            const float* __restrict__ x, int64_t ldx, const float* __restrict__ w, int64_t ldw,
+            float* __restrict__ slabs, SegView sv) {
+  constexpr int U = (GL > 8) ? GL : 8;
+  constexpr int NWL = (GL > 0) ? U / GL : 0;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (k >= n_rows * sv.B) return;
+  const int b = static_cast<int>(k / n_rows);
+  const int64_t row = sv.perm[k - static_cast<int64_t>(b) * n_rows];
+  const int32_t* sg = sv.seg + row * (sv.B + 1);
+  const int64_t base = indptr[row];
+  const int64_t eb = base + sg[b], ee = base + sg[b + 1];
+  if (eb == ee) return;
+  const int col = lane * VW;
+  const int head = (GL > 0) ? lane / GL : 0;
+  const int gsub = (GL > 0) ? lane % GL : 0;
+  float acc[VW];
+#pragma unroll
+  for (int q = 0; q < VW; ++q) acc[q] = 0.f;
+  int idxv = indices[min(eb + lane, ee - 1)];
+  for (int64_t e0 = eb; e0 < ee; e0 += kWave) {
+    const int n = static_cast<int>(min<int64_t>(kWave, ee - e0));
+    const int idxn = indices[min(e0 + kWave + lane, ee - 1)];
+    const float* wblk = (GL > 0) ? w + e0 * ldw : nullptr;
+    int s = 0;
+    for (; s + U <= n; s += U) {
+      Vec<VW> xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t xr = __builtin_amdgcn_readlane(idxv, s + u);
+        xv[u].load(x + xr * ldx + col);
+      }
+      if (GL > 0) {
+        float wa[NWL > 0 ? NWL : 1], wu[U];
+#pragma unroll
+        for (int q = 0; q < NWL; ++q) wa[q] = wblk[static_cast<int64_t>(s + q * GL + gsub) * ldw + head];
+        bcast_all<(GL > 0 ? GL : 1), U>(wa, wu);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int q = 0; q < VW; ++q) acc[q] = fmaf(wu[u], xv[u].v[q], acc[q]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int q = 0; q < VW; ++q) acc[q] += xv[u].v[q];
+      }
+    }
+    for (; s < n; ++s) {
+      const int64_t xr = __builtin_amdgcn_readlane(idxv, s);
+      Vec<VW> xv;
+      xv.load(x + xr * ldx + col);
+      const float wv = (GL > 0) ? wblk[static_cast<int64_t>(s) * ldw + head] : 1.f;
+#pragma unroll
+      for (int q = 0; q < VW; ++q) acc[q] = (GL > 0) ? fmaf(wv, xv.v[q], acc[q]) : acc[q] + xv.v[q];
+    }
+    idxv = idxn;
+  }
+  Vec<VW> o;
+#pragma unroll
+  for (int q = 0; q < VW; ++q) o.v[q] = acc[q];
+  o.store(slabs + (static_cast<int64_t>(b) * n_rows + row) * (kWave * VW) + col);
+}
+
+template <int VW>
+__global__ void __launch_bounds__(kBlock)
+k_seg_reduce(int64_t n_rows, const float* __restrict__ slabs, const float* __restrict__ row_scale,
+             float* __restrict__ y, int64_t ldy, int accumulate, SegView sv) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  const int32_t* sg = sv.seg + row * (sv.B + 1);
+  const int col = lane * VW;
+  constexpr int F = kWave * VW;
+  float acc[VW];
+#pragma unroll
+  for (int q = 0; q < VW; ++q) acc[q] = 0.f;
+  for (int b = 0; b < sv.B; ++b) {
+    if (sg[b] == sg[b + 1]) continue;
+    Vec<VW> p;
+    p.load(slabs + (static_cast<int64_t>(b) * n_rows + row) * F + col);
+#pragma unroll
+    for (int q = 0; q < VW; ++q) acc[q] += p.v[q];
+  }
+  const float scale = row_scale ? row_scale[row] : 1.f;
+  float* yp = y + row * ldy + col;
+  Vec<VW> o;
+  if (accumulate) {
+    o.load(yp);
+#pragma unroll
+    for (int q = 0; q < VW; ++q) o.v[q] += scale * acc[q];
+  } else {
+#pragma unroll
+    for (int q = 0; q < VW; ++q) o.v[q] = scale * acc[q];
+  }
+  o.store(yp);
+}
+
 // ---- column-blocked plan: segment table + heavy-first row order -----------
 // layout: int64 hdr[8] {B, bsize, n_rows, unsorted_flag}, int32 perm[n_rows],
 //         int32 seg[n_rows*(B+1)], int32 bucket[64] (count, offset)
@@ -1149,10 +1254,15 @@ int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indic
   return GTA_OK;
 }
 
+int64_t gta_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t blocks, int64_t F) {
+  if (n_rows < 0 || blocks < 1 || F <= 0) return fail(GTA_ERR_ARG, "blocked_workspace_bytes: bad sizes");
+  return n_rows * blocks * F * static_cast<int64_t>(sizeof(float));
+}
+
 int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
                           const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
                           const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
-                          int64_t blocks, void* stream) {
+                          int64_t blocks, void* workspace, void* stream) {
   if (!indptr || !indices || !x || !y || !plan || n_rows < 0 || F <= 0 || blocks < 1 || blocks > 63)
     return fail(GTA_ERR_ARG, "aggregate_blocked: bad arguments");
   if (n_rows == 0) return GTA_OK;
@@ -1173,6 +1283,29 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
   const int B = static_cast<int>(blocks);
   BlockedView v = blocked_view(const_cast<void*>(plan), n_rows, B);
   hipStream_t s = S(stream);
+  if (workspace) {  // single launch into per-block slabs + ordered reduce
+    SegView sv{v.perm, v.seg, B, 0};
+    float* slabs = static_cast<float*>(workspace);
+    const int64_t items = n_rows * B;
+    const dim3 g2(static_cast<unsigned>((items + kWavesPerBlock - 1) / kWavesPerBlock)), blk2(kBlock);
+#define GTA_SEG2D(VW_, GL_) \
+  k_agg_seg2d<VW_, GL_><<<g2, blk2, 0, s>>>(indptr, indices, n_rows, x, ldx, w, ldw, slabs, sv)
+    if (vw == 2) {
+      if (gl == 0) GTA_SEG2D(2, 0); else if (gl == 4) GTA_SEG2D(2, 4); else if (gl == 8) GTA_SEG2D(2, 8); else GTA_SEG2D(2, 16);
+    } else if (vw == 4) {
+      if (gl == 0) GTA_SEG2D(4, 0); else if (gl == 4) GTA_SEG2D(4, 4); else if (gl == 8) GTA_SEG2D(4, 8); else GTA_SEG2D(4, 16);
+    } else {
+      if (gl == 0) GTA_SEG2D(1, 0); else if (gl == 4) GTA_SEG2D(1, 4); else if (gl == 8) GTA_SEG2D(1, 8); else GTA_SEG2D(1, 16);
+    }
+#undef GTA_SEG2D
+    GTA_LAUNCHED("k_agg_seg2d");
+    const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+    if (vw == 2) k_seg_reduce<2><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, sv);
+    else if (vw == 4) k_seg_reduce<4><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, sv);
+    else k_seg_reduce<1><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, sv);
+    GTA_LAUNCHED("k_seg_reduce");
+    return GTA_OK;
+  }
   // persistent waves: enough for 8 per SIMD on every CU, never more than one per row
   const int64_t waves = std::min<int64_t>(n_rows, g_seg_waves > 0 ? g_seg_waves : 256 * 32);
   const dim3 grid(static_cast<unsigned>((waves + kWavesPerBlock - 1) / kWavesPerBlock)), blk(kBlock);

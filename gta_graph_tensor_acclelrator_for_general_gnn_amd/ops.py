@@ -146,6 +146,15 @@ class BlockedPlan:
                                                  self.blocks, _ptr(self.buf), int(nb), _stream(graph.device)),
               "blocked_plan_build")
         self.sorted = int(self.buf[24:32].view(torch.int64).item()) == 0
+        self._ws = {}
+
+    def workspace(self, F):
+        """Per-block partial slabs for the single-launch form ([B, N, F] fp32)."""
+        if F not in self._ws:
+            nb = check(_L().gta_aggregate_blocked_workspace_bytes(self.graph.n_rows, self.blocks, F),
+                       "blocked_workspace_bytes")
+            self._ws[F] = torch.empty(int(nb), dtype=torch.uint8, device=self.graph.device)
+        return self._ws[F]
 
     @staticmethod
     def supports(F, heads, x=None):
@@ -160,8 +169,11 @@ class BlockedPlan:
         return True
 
 
-def aggregate_blocked(graph, x, w=None, row_scale=None, out=None, accumulate=False, plan=None, blocks=32):
-    """Same result as aggregate(graph, x, "src", w, ...) via B column-block launches (L2-resident X slices)."""
+def aggregate_blocked(graph, x, w=None, row_scale=None, out=None, accumulate=False, plan=None, blocks=32,
+                      single_launch=True):
+    """Same result as aggregate(graph, x, "src", w, ...) computed column block by column block so the
+    gathered X slice stays L2-resident.  single_launch: one launch over (block, row) items into per-block
+    slabs + an ordered reduce; otherwise B dependent launches accumulating into out."""
     _need_gpu(x, w, row_scale, out, graph.indptr)
     F = x.shape[1]
     ldx = _rows(x, "x")
@@ -182,9 +194,10 @@ def aggregate_blocked(graph, x, w=None, row_scale=None, out=None, accumulate=Fal
     if out is None:
         out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=x.device)
     ldy = _rows(out, "out")
+    ws = plan.workspace(F) if single_launch else None
     check(_L().gta_aggregate_blocked(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols, _ptr(x), ldx,
                                      F, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy, int(bool(accumulate)),
-                                     _ptr(plan.buf), plan.blocks, _stream(x.device)), "aggregate_blocked")
+                                     _ptr(plan.buf), plan.blocks, _ptr(ws), _stream(x.device)), "aggregate_blocked")
     return out
 
 

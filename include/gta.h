@@ -122,10 +122,14 @@ int64_t gta_aggregate_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t chunk
 int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t blocks);
 int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
                                      int64_t blocks, void* plan, int64_t plan_bytes, void* stream);
+/* workspace: NULL = B dependent launches accumulating into y; otherwise >=
+ * gta_aggregate_blocked_workspace_bytes: one launch over (block, row) items in
+ * block-major order writing per-block partial slabs, then an ordered reduce. */
+int64_t gta_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t blocks, int64_t F);
 int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
                           const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
                           const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
-                          int64_t blocks, void* stream);
+                          int64_t blocks, void* workspace, void* stream);
 
 /* ---- K2 GATHER ADD (edge -> node) ---------------------------------------
  * y[i, :] (+)= sum_{e in row i} xe[e, :]    == gta_aggregate(x_mode=EDGE, w=NULL)

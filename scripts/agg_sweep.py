@@ -39,7 +39,8 @@ def main():
         parts = v.split(":")
         if parts[0].startswith("blk"):  # column-blocked path, B = blk<B>[:w<persistent waves>]
             wv = int(parts[1][1:]) if len(parts) > 1 and parts[1].startswith("w") else 0
-            variants.append((v, -int(parts[0][3:]), None, wv, 1))
+            single = 0 if "multi" in parts[1:] else 1
+            variants.append((v, -int(parts[0][3:]), None, wv, single))
             continue
         lpe = int(parts[0].replace("lpe", ""))
         chunk = None if parts[1] == "none" else int(parts[1].replace("c", ""))
@@ -57,14 +58,14 @@ def main():
             if lpe < 0:
                 ops.set_debug("seg_waves", nt)
 
-                def run():
-                    ops.aggregate_blocked(g, x, alpha, out=y, blocks=-lpe)
+                def run(lpe=lpe, lean=lean):
+                    ops.aggregate_blocked(g, x, alpha, out=y, blocks=-lpe, single_launch=bool(lean))
             else:
                 ops.set_debug("agg_lpe", lpe)
                 ops.set_debug("agg_nt", nt)
                 ops.set_debug("agg_lean", lean)
 
-                def run():
+                def run(chunk=chunk):
                     ops.aggregate(g, x, "src", alpha, out=y, plan=plans[chunk])
             run()  # warm
             s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -226,7 +226,8 @@ def test_update_mm_f32_x_bf16_w(dev, M, K, N):
 
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 16), (128, 4), (64, 4), (256, 16), (128, 0), (64, 0)])
 @pytest.mark.parametrize("blocks", [1, 7, 32, 63])
-def test_aggregate_blocked_matches_oracle(dev, F, heads, blocks):
+@pytest.mark.parametrize("single", [True, False])
+def test_aggregate_blocked_matches_oracle(dev, F, heads, blocks, single):
     """Column-blocked K6 (B launches over source-column slices) == fp64 oracle; rows must be column-sorted."""
     n, e = 700, 20000
     g0 = G.synthetic(n, e, seed=blocks + F, device="cpu")          # sorted columns
@@ -241,11 +242,11 @@ def test_aggregate_blocked_matches_oracle(dev, F, heads, blocks):
     x = rng.standard_normal((n, F)).astype(np.float32)
     w = rng.random((len(ix), heads)).astype(np.float32) if heads else None
     y = ops.aggregate_blocked(g, torch.from_numpy(x).to(dev), None if w is None else torch.from_numpy(w).to(dev),
-                              blocks=blocks)
+                              blocks=blocks, single_launch=single)
     ref = isa_ref.aggregate(ip, ix, x, "src", w)
     _check(y, ref, isa_ref.aggregate_abs(ip, ix, x, "src", w), f"blocked F={F} H={heads} B={blocks}")
     y2 = ops.aggregate_blocked(g, torch.from_numpy(x).to(dev), None if w is None else torch.from_numpy(w).to(dev),
-                               blocks=blocks)
+                               blocks=blocks, single_launch=single)
     assert torch.equal(y, y2)
 
 
@@ -261,6 +262,12 @@ def test_aggregate_blocked_accumulate_rowscale(dev):
     yd = torch.from_numpy(y0).to(dev)
     ops.aggregate_blocked(g, torch.from_numpy(x).to(dev), torch.from_numpy(w).to(dev),
                           row_scale=torch.from_numpy(sc).to(dev), out=yd, accumulate=True, blocks=16)
+    y2 = torch.from_numpy(y0).to(dev)
+    ops.aggregate_blocked(g, torch.from_numpy(x).to(dev), torch.from_numpy(w).to(dev),
+                          row_scale=torch.from_numpy(sc).to(dev), out=y2, accumulate=True, blocks=16,
+                          single_launch=False)
+    _check(y2, y0 + isa_ref.aggregate(ip, ix, x, "src", w, sc),
+           isa_ref.aggregate_abs(ip, ix, x, "src", w, sc) + np.abs(y0), "blocked multi acc+scale")
     ref = y0 + isa_ref.aggregate(ip, ix, x, "src", w, sc)
     _check(yd, ref, isa_ref.aggregate_abs(ip, ix, x, "src", w, sc) + np.abs(y0), "blocked acc+scale")
 
