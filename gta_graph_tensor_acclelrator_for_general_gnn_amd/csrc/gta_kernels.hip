@@ -394,6 +394,12 @@ __device__ __forceinline__ void bcast_all(const float* wa, float* out) {
 // seg[r][b] .. seg[r][b+1] within the row's sorted column list -- and adds the
 // partial into y[r] (the first launch writes).  All waves of a launch gather
 // from one n_cols/B slice of X, which stays resident in each XCD's 4 MB L2.
+struct SegItem {  // one (column block, row) work item: 16 B, loaded with one dwordx4
+  int64_t beg;
+  int32_t row;
+  int32_t len;
+};
+
 struct SegView {
   const int32_t* perm;  // rows, heaviest first
   const int32_t* seg;   // [n_rows][B+1] offsets within each row
@@ -609,18 +615,17 @@ template <int VW, int GL>
 __global__ void __launch_bounds__(kBlock)
 k_agg_seg2d(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
             const float* __restrict__ x, int64_t ldx, const float* __restrict__ w, int64_t ldw,
-            float* __restrict__ slabs, SegView sv) {
+            float* __restrict__ slabs, SegView sv, const SegItem* __restrict__ items) {
   constexpr int U = (GL > 8) ? GL : 8;
   constexpr int NWL = (GL > 0) ? U / GL : 0;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t k = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
   if (k >= n_rows * sv.B) return;
   const int b = static_cast<int>(k / n_rows);
-  const int64_t row = sv.perm[k - static_cast<int64_t>(b) * n_rows];
-  const int32_t* sg = sv.seg + row * (sv.B + 1);
-  const int64_t base = indptr[row];
-  const int64_t eb = base + sg[b], ee = base + sg[b + 1];
-  if (eb == ee) return;
+  const SegItem it = items[k];
+  if (it.len == 0) return;
+  const int64_t row = it.row;
+  const int64_t eb = it.beg, ee = it.beg + it.len;
   const int col = lane * VW;
   const int head = (GL > 0) ? lane / GL : 0;
   const int gsub = (GL > 0) ? lane % GL : 0;
@@ -714,6 +719,7 @@ struct BlockedView {
   int32_t* perm;
   int32_t* seg;
   int32_t* bucket;
+  void* items;  // SegItem[B * n_rows], block-major, heaviest row first within a block
 };
 
 BlockedView blocked_view(void* base, int64_t n_rows, int B) {
@@ -722,12 +728,14 @@ BlockedView blocked_view(void* base, int64_t n_rows, int B) {
   v.hdr = reinterpret_cast<int64_t*>(p); p += round16(8 * 8);
   v.perm = reinterpret_cast<int32_t*>(p); p += round16(n_rows * 4);
   v.seg = reinterpret_cast<int32_t*>(p); p += round16(n_rows * (B + 1) * 4);
-  v.bucket = reinterpret_cast<int32_t*>(p);
+  v.bucket = reinterpret_cast<int32_t*>(p); p += round16(64 * 4);
+  v.items = reinterpret_cast<void*>(p);
   return v;
 }
 
 int64_t blocked_bytes(int64_t n_rows, int B) {
-  return round16(64) + round16(n_rows * 4) + round16(n_rows * (B + 1) * 4) + round16(64 * 4);
+  return round16(64) + round16(n_rows * 4) + round16(n_rows * (B + 1) * 4) + round16(64 * 4) +
+         round16(n_rows * B * 16);
 }
 
 __device__ __forceinline__ int deg_bucket(int64_t d) {  // 31 = heaviest ... 0 = empty/1
@@ -766,6 +774,19 @@ __global__ void k_blocked_scan(BlockedView v) {  // heaviest bucket first
       run += v.bucket[k];
     }
   }
+}
+
+__global__ void k_blocked_items(const int64_t* __restrict__ indptr, int64_t n_rows, int B, BlockedView v) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= n_rows * B) return;
+  const int b = static_cast<int>(k / n_rows);
+  const int32_t row = v.perm[k - static_cast<int64_t>(b) * n_rows];
+  const int32_t* sg = v.seg + static_cast<int64_t>(row) * (B + 1);
+  SegItem it;
+  it.beg = indptr[row] + sg[b];
+  it.row = row;
+  it.len = sg[b + 1] - sg[b];
+  static_cast<SegItem*>(v.items)[k] = it;
 }
 
 __global__ void k_blocked_perm(const int64_t* __restrict__ indptr, int64_t n_rows, BlockedView v) {
@@ -1251,6 +1272,8 @@ int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indic
   GTA_LAUNCHED("k_blocked_scan");
   k_blocked_perm<<<dim3(static_cast<unsigned>((n_rows + 255) / 256)), dim3(256), 0, s>>>(indptr, n_rows, v);
   GTA_LAUNCHED("k_blocked_perm");
+  k_blocked_items<<<dim3(static_cast<unsigned>((n_rows * B + 255) / 256)), dim3(256), 0, s>>>(indptr, n_rows, B, v);
+  GTA_LAUNCHED("k_blocked_items");
   return GTA_OK;
 }
 
@@ -1289,7 +1312,8 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     const int64_t items = n_rows * B;
     const dim3 g2(static_cast<unsigned>((items + kWavesPerBlock - 1) / kWavesPerBlock)), blk2(kBlock);
 #define GTA_SEG2D(VW_, GL_) \
-  k_agg_seg2d<VW_, GL_><<<g2, blk2, 0, s>>>(indptr, indices, n_rows, x, ldx, w, ldw, slabs, sv)
+  k_agg_seg2d<VW_, GL_><<<g2, blk2, 0, s>>>(indptr, indices, n_rows, x, ldx, w, ldw, slabs, sv, \
+                                            static_cast<const SegItem*>(v.items))
     if (vw == 2) {
       if (gl == 0) GTA_SEG2D(2, 0); else if (gl == 4) GTA_SEG2D(2, 4); else if (gl == 8) GTA_SEG2D(2, 8); else GTA_SEG2D(2, 16);
     } else if (vw == 4) {
