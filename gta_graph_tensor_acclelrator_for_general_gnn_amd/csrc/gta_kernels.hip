@@ -607,110 +607,6 @@ k_agg_seg(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indice
   }
 }
 
-// Software-pipelined gather-accumulate over edges [eb, ee) of one row segment:
-//   acc[k] += w(e, head) * x[indices[e], col + k]      (GL == 0: unweighted)
-// Steps of U edges are double-buffered (the next step's row loads and weight load
-// are issued before the current step is consumed; the loop is unrolled by two so
-// both buffers stay in registers), indices arrive 64 at a time and are rotated as
-// the steps cross 64-edge blocks, and the < U remainder is ONE masked step
-// (clamped in-row indices, results selected away) instead of U serial round trips.
-template <int VW, int GL>
-__device__ __forceinline__ void gather_accumulate(const int32_t* __restrict__ indices, int64_t eb, int64_t ee,
-                                                  const float* __restrict__ x, int64_t ldx,
-                                                  const float* __restrict__ w, int64_t ldw, int lane, float* acc) {
-  constexpr int U = (GL > 8) ? GL : 8;
-  constexpr int NWL = (GL > 0) ? U / GL : 1;
-  const int col = lane * VW;
-  const int head = (GL > 0) ? lane / GL : 0;
-  const int gsub = (GL > 0) ? lane % GL : 0;
-  const int64_t len = ee - eb;
-  if (len <= 0) return;
-  const int64_t nfull = len / U;
-  const int rem = static_cast<int>(len - nfull * U);
-  int idxv = indices[min(eb + lane, ee - 1)];
-  int idxn = indices[min(eb + kWave + lane, ee - 1)];
-  int64_t blk0 = eb;  // first edge covered by idxv
-
-  Vec<VW> xa[U], xb[U];
-  float wa[NWL], wb[NWL];
-  auto issue = [&](Vec<VW>* xv, float* wv, int64_t j) {
-    const int64_t e = eb + j * U;
-    if (e >= blk0 + kWave) {  // crossed into the next 64-edge index block (steps never straddle one)
-      idxv = idxn;
-      blk0 += kWave;
-      idxn = indices[min(blk0 + kWave + lane, ee - 1)];
-    }
-    const int off = static_cast<int>(e - blk0);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t xr = __builtin_amdgcn_readlane(idxv, off + u);
-      xv[u].load(x + xr * ldx + col);
-    }
-    if (GL > 0) {
-#pragma unroll
-      for (int q = 0; q < NWL; ++q) wv[q] = w[(e + q * GL + gsub) * ldw + head];
-    }
-  };
-  auto consume = [&](const Vec<VW>* xv, const float* wv) {
-    if (GL > 0) {
-      float wu[U];
-      bcast_all<(GL > 0 ? GL : 1), U>(wv, wu);
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int k = 0; k < VW; ++k) acc[k] = fmaf(wu[u], xv[u].v[k], acc[k]);
-    } else {
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int k = 0; k < VW; ++k) acc[k] += xv[u].v[k];
-    }
-  };
-  if (nfull > 0) {
-    issue(xa, wa, 0);
-    int64_t j = 0;
-    while (true) {
-      const bool more_b = j + 1 < nfull;
-      if (more_b) issue(xb, wb, j + 1);
-      consume(xa, wa);
-      ++j;
-      if (!more_b) break;
-      const bool more_a = j + 1 < nfull;
-      if (more_a) issue(xa, wa, j + 1);
-      consume(xb, wb);
-      ++j;
-      if (!more_a) break;
-    }
-  }
-  if (rem > 0) {  // one masked step
-    const int64_t e = eb + nfull * U;
-    if (e >= blk0 + kWave) {
-      idxv = idxn;
-      blk0 += kWave;
-    }
-    const int off = static_cast<int>(e - blk0);
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int uu = u < rem ? u : rem - 1;
-      const int64_t xr = __builtin_amdgcn_readlane(idxv, off + uu);
-      xa[u].load(x + xr * ldx + col);
-    }
-    float wt[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int uu = u < rem ? u : rem - 1;
-      wt[u] = (GL > 0) ? w[(e + uu) * ldw + head] : 1.f;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u)
-#pragma unroll
-      for (int k = 0; k < VW; ++k) {
-        const float t = (GL > 0) ? wt[u] * xa[u].v[k] : xa[u].v[k];
-        acc[k] += (u < rem) ? t : 0.f;
-      }
-  }
-}
-
 // Single-launch column-blocked form: item k = (b = k / n_rows, row = perm[k % n_rows]),
 // b-major, so the waves in flight at any moment gather from one or two X slices.
 // Each non-empty (b, row) segment writes its partial to slab b; k_seg_reduce sums
@@ -731,10 +627,50 @@ k_agg_seg2d(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
   const int64_t row = it.row;
   const int64_t eb = it.beg, ee = it.beg + it.len;
   const int col = lane * VW;
+  const int head = (GL > 0) ? lane / GL : 0;
+  const int gsub = (GL > 0) ? lane % GL : 0;
   float acc[VW];
 #pragma unroll
   for (int q = 0; q < VW; ++q) acc[q] = 0.f;
-  gather_accumulate<VW, GL>(indices, eb, ee, x, ldx, w, ldw, lane, acc);
+  int idxv = indices[min(eb + lane, ee - 1)];
+  for (int64_t e0 = eb; e0 < ee; e0 += kWave) {
+    const int n = static_cast<int>(min<int64_t>(kWave, ee - e0));
+    const int idxn = indices[min(e0 + kWave + lane, ee - 1)];
+    const float* wblk = (GL > 0) ? w + e0 * ldw : nullptr;
+    int s = 0;
+    for (; s + U <= n; s += U) {
+      Vec<VW> xv[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int64_t xr = __builtin_amdgcn_readlane(idxv, s + u);
+        xv[u].load(x + xr * ldx + col);
+      }
+      if (GL > 0) {
+        float wa[NWL > 0 ? NWL : 1], wu[U];
+#pragma unroll
+        for (int q = 0; q < NWL; ++q) wa[q] = wblk[static_cast<int64_t>(s + q * GL + gsub) * ldw + head];
+        bcast_all<(GL > 0 ? GL : 1), U>(wa, wu);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int q = 0; q < VW; ++q) acc[q] = fmaf(wu[u], xv[u].v[q], acc[q]);
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+          for (int q = 0; q < VW; ++q) acc[q] += xv[u].v[q];
+      }
+    }
+    for (; s < n; ++s) {
+      const int64_t xr = __builtin_amdgcn_readlane(idxv, s);
+      Vec<VW> xv;
+      xv.load(x + xr * ldx + col);
+      const float wv = (GL > 0) ? wblk[static_cast<int64_t>(s) * ldw + head] : 1.f;
+#pragma unroll
+      for (int q = 0; q < VW; ++q) acc[q] = (GL > 0) ? fmaf(wv, xv.v[q], acc[q]) : acc[q] + xv.v[q];
+    }
+    idxv = idxn;
+  }
   Vec<VW> o;
 #pragma unroll
   for (int q = 0; q < VW; ++q) o.v[q] = acc[q];
