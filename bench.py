@@ -99,6 +99,9 @@ def main():
     ap.add_argument("--chunk", type=int, default=512, help="aggregate plan row-chunk (edges)")
     ap.add_argument("--row-chunks", type=int, default=0, help="row chunks for comm overlap (0 = auto)")
     ap.add_argument("--lpe", type=int, default=0, help="force lanes-per-edge variant (32 or 64)")
+    ap.add_argument("--impl", choices=["blocked", "plan"], default="blocked",
+                    help="blocked: column-blocked aggregate (L2-resident X slices); plan: row-chunked single pass")
+    ap.add_argument("--blocks", type=int, default=16, help="column blocks of the blocked aggregate")
     ap.add_argument("--n", type=int, default=N_REDDIT)
     ap.add_argument("--e", type=int, default=E_REDDIT)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -132,12 +135,24 @@ def main():
     else:
         shard, gl, xl, wl = None, g, x, alpha
         n_chunks = args.row_chunks or 1
-    chunked = partition.ChunkedRows(gl, n_chunks=n_chunks, chunk=args.chunk)
+    chunked = partition.ChunkedRows(gl, n_chunks=n_chunks, chunk=args.chunk if args.impl == "plan" else 0)
+    impl = args.impl
+    if impl == "blocked":
+        for _, _, gg, _ in chunked.parts:
+            if not (ops.BlockedPlan.supports(F, HEADS) and gg.blocked_plan(args.blocks).sorted):
+                impl = "plan"
+        if impl == "plan":
+            chunked = partition.ChunkedRows(gl, n_chunks=n_chunks, chunk=args.chunk)
     y = torch.empty(g.n_rows, F, device=dev)
     stream = torch.cuda.current_stream(dev)
 
+    def agg_chunk(gg, xx, ww, out, plan):
+        if impl == "blocked":
+            return ops.aggregate_blocked(gg, xx, ww, out=out, blocks=args.blocks)
+        return ops.aggregate(gg, xx, "src", ww, out=out, plan=plan)
+
     def step():
-        partition.distributed_aggregate(chunked, xl, wl, y)
+        partition.distributed_aggregate(chunked, xl, wl, y, aggregate_fn=agg_chunk)
 
     for _ in range(args.warmup):
         step()
@@ -149,7 +164,7 @@ def main():
     for a, b in evs:
         a.record(stream)
         for r0, r1, gg, plan in chunked.parts:
-            ops.aggregate(gg, xl, "src", wl, out=y[r0:r1], plan=plan)
+            agg_chunk(gg, xl, wl, y[r0:r1], plan)
         b.record(stream)
     torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
@@ -193,7 +208,7 @@ def main():
     if os.path.exists(pmc_path) and world == 1:
         try:
             pm = json.load(open(pmc_path))
-            if pm.get("n") == args.n and pm.get("e") == args.e:
+            if pm.get("n") == args.n and pm.get("e") == args.e and pm.get("impl", "plan") == impl:
                 traffic = pm.get("hbm_bytes_per_launch")
         except Exception:
             traffic = None
@@ -215,12 +230,14 @@ def main():
         "config": {"workload": "GAT layer-1 aggregate block [3,11,12] (scatter C -> applyedge MUL -> gather ADD)",
                    "graph": "reddit-shaped", "N": args.n, "E": nnz_total, "F": F, "heads": HEADS,
                    "parallelism": f"edge-partition by source column x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
-                   "plan_chunk": args.chunk, "row_chunks": n_chunks},
+                   "impl": impl, "blocks": args.blocks if impl == "blocked" else None,
+                   "plan_chunk": args.chunk if impl == "plan" else None, "row_chunks": n_chunks},
         "achieved_GBps": nnz_total and alg_bytes(g.n_rows, nnz_total) / (ms_per_step / 1e3) / 1e9,
         "parity": parity,
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
-                     "kernel_ms": kern_ms, "alg_bytes_per_launch": ab},
+                     "kernel_ms": kern_ms, "alg_bytes_per_launch": ab,
+                     "kernels": ("k_agg_seg2d + k_seg_reduce" if impl == "blocked" else "k_aggregate + combine")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(g, x, alpha)

@@ -110,6 +110,10 @@ class Executor:
         #   fuse_sf: an SF whose producer feeds only it runs as the producer's post-op
         self.elide_scatter_stores = True
         self.fuse_sf = True
+        # weighted/unweighted SpMM aggregates whose gathered table exceeds the chip's L2
+        # run column-blocked (L2-resident slices) when the shape allows it
+        self.blocked_min_table_bytes = 32 << 20
+        self.blocked_blocks = 16
         self.consumers = {i: [] for i in range(len(opgraph))}
         for i in range(len(opgraph)):
             for src in opgraph.inputs[i]:
@@ -272,7 +276,7 @@ class Executor:
             else:  # a non-MUL fused pair: evaluate the producer, then gather
                 v = self._materialize_deferred(v)
         if isinstance(v, Scat):
-            y = ops.aggregate(self.graph, v.t, v.mode, None, plan=self._plan())
+            y = self._spmm(v.t, v.mode, None)
             self._count(E * (4 + v.t.shape[1] * 4) + n * (8 + v.t.shape[1] * 4))
             return NodeT(y)
         xe = self._to_edge_tensor(v)
@@ -303,9 +307,18 @@ class Executor:
             xt, mode = self._to_edge_tensor(x), "edge"
         if xt.shape[1] % wt.shape[1]:
             raise ValueError(f"weighted aggregate: weight width {wt.shape[1]} does not divide {xt.shape[1]}")
-        y = ops.aggregate(self.graph, xt, mode, wt, plan=self._plan())
+        y = self._spmm(xt, mode, wt)
         self._count(E * (4 + 4 * wt.shape[1] + 4 * xt.shape[1]) + n * (8 + 4 * xt.shape[1]))
         return y
+
+    def _spmm(self, xt, mode, wt):
+        """SpMM-form aggregate: column-blocked when the gathered table outgrows L2, else row-chunked."""
+        heads = 0 if wt is None else wt.shape[1]
+        if (mode == "src" and self.blocked_blocks and xt.numel() * 4 >= self.blocked_min_table_bytes
+                and ops.BlockedPlan.supports(xt.shape[1], heads)
+                and self.graph.blocked_plan(self.blocked_blocks).sorted):
+            return ops.aggregate_blocked(self.graph, xt, wt, blocks=self.blocked_blocks)
+        return ops.aggregate(self.graph, xt, mode, wt, plan=self._plan())
 
     def _unweighted(self, x):
         if isinstance(x, Scat):

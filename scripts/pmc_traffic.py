@@ -19,16 +19,28 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-METRIC_KERNEL = re.compile(r"k_aggregate<\d+, \d+, \d+, 0, 1>")  # XM_IDX + WM_HEAD: the metric variant
+# the metric's aggregate kernels: plan path k_aggregate<..., 0, 1> / k_agg_lean, blocked path k_agg_seg2d + k_seg_reduce
+METRIC_KERNELS = {"plan": re.compile(r"k_aggregate<\d+, \d+, \d+, 0, 1>|k_agg_lean<"),
+                  "blocked": re.compile(r"k_agg_seg2d<|k_seg_reduce<")}
+METRIC_KERNEL = METRIC_KERNELS["blocked"]
 
 
 def read_counter(d, counter):
+    """Per-launch value: sum over the dispatches of one aggregate launch (seg2d + reduce are one launch
+    pair; consecutive matching dispatches are grouped by Dispatch_Id order)."""
     files = glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True)
-    vals = []
+    rows = []
     for f in files:
         for row in csv.DictReader(open(f)):
             if METRIC_KERNEL.search(row.get("Kernel_Name", "")) and row.get("Counter_Name") == counter:
-                vals.append(float(row["Counter_Value"]))
+                rows.append((int(row.get("Dispatch_Id", 0)), row["Kernel_Name"], float(row["Counter_Value"])))
+    rows.sort()
+    vals, cur = [], 0.0
+    for _, name, v in rows:
+        cur += v
+        if "k_seg_reduce" in name or "k_agg_seg2d" not in name:
+            vals.append(cur)
+            cur = 0.0
     return vals
 
 
@@ -44,7 +56,7 @@ def main(fetch_dir="gpurun_out/pmc_fetch", write_dir="gpurun_out/pmc_write", n=2
     fetch_kb = sum(fs) / len(fs)
     write_kb = sum(ws) / len(ws)
     hbm = 2 * fetch_kb * 1024 + write_kb * 1024
-    out = {"n": n, "e": e, "kernel": "k_aggregate", "dispatches": [len(f), len(w)],
+    out = {"n": n, "e": e, "impl": "blocked", "kernel": "k_agg_seg2d + k_seg_reduce", "dispatches": [len(f), len(w)],
            "FETCH_SIZE_KB_avg": fetch_kb, "WRITE_SIZE_KB_avg": write_kb,
            "hbm_bytes_per_launch": hbm,
            "method": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction), "
