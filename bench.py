@@ -57,6 +57,16 @@ def make_inputs(n, e, device, seed=0):
     return g, x, alpha
 
 
+def auto_blocks(graph, f):
+    """Column blocks for the blocked aggregate: X slices of ~7.5 MB (half an XCD L2 x 4 -- the
+    measured optimum on the 1-GPU Reddit shape was B = 16 for a 119 MB table, profiles/
+    r01_agg_sweep_*), capped so a row still has >= 24 edges per block on average (each
+    (block, row) item pays a fixed start-up; at 8 GPUs a shard's rows hold ~61 edges)."""
+    table_mb = graph.n_cols * f * 4 / 1e6
+    avg_deg = graph.nnz / max(1, graph.n_rows)
+    return int(max(1, min(16, round(table_mb / 7.5), avg_deg // 24)))
+
+
 def cpu_baseline(g, x, alpha, target_s=12.0):
     """Oracle C aggregate (OpenMP) on the first rows of the same workload, ~target_s of CPU work."""
     from oracle import cbase
@@ -101,7 +111,8 @@ def main():
     ap.add_argument("--lpe", type=int, default=0, help="force lanes-per-edge variant (32 or 64)")
     ap.add_argument("--impl", choices=["blocked", "plan"], default="blocked",
                     help="blocked: column-blocked aggregate (L2-resident X slices); plan: row-chunked single pass")
-    ap.add_argument("--blocks", type=int, default=16, help="column blocks of the blocked aggregate")
+    ap.add_argument("--blocks", type=int, default=0,
+                    help="column blocks of the blocked aggregate (0 = auto: ~7.5 MB X slices, >= 24 edges/row/block)")
     ap.add_argument("--n", type=int, default=N_REDDIT)
     ap.add_argument("--e", type=int, default=E_REDDIT)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -137,6 +148,10 @@ def main():
         n_chunks = args.row_chunks or 1
     chunked = partition.ChunkedRows(gl, n_chunks=n_chunks, chunk=args.chunk if args.impl == "plan" else 0)
     impl = args.impl
+    if impl == "blocked" and not args.blocks:
+        args.blocks = auto_blocks(gl, F)
+        if args.blocks < 4:  # slices already L2/MALL-friendly and segments short: single pass wins
+            impl = "plan"
     if impl == "blocked":
         for _, _, gg, _ in chunked.parts:
             if not (ops.BlockedPlan.supports(F, HEADS) and gg.blocked_plan(args.blocks).sorted):
