@@ -5,6 +5,8 @@
   sage-reddit  GraphSAGE-mean layer 1 on Reddit (232,965 / 114,615,892), F=602
   gin-products GIN layer 1 on an ogbn-products-shaped CSR (2,449,029 / 123,718,280), F=100,
                both MLP GEMMs in bf16 on MFMA (fp32 accumulation)
+  gat8-reddit  GAT layer 1 on Reddit, 8 heads, F=602: not a BASELINE config; the full layer
+               around the metric's aggregate (edge-softmax, GEMMs, aggregate, ELU)
 (config 0 -- V2/GAT_Cora.yaml through compile/interpret on the CPU -- is the golden-stream
 suite: tests/test_lowering.py, test_compiler.py.)
 """
@@ -15,6 +17,7 @@ from . import graph as G, pipeline, workloads
 CONFIGS = {
     "gcn-cora": dict(network="GCN", dataset="cora", feature=1433, layers=(1, 2)),
     "gat8-flickr": dict(network="GAT", dataset="flickr", feature=500, layers=(1,), heads=8),
+    "gat8-reddit": dict(network="GAT", dataset="reddit", feature=602, layers=(1,), heads=8),
     "sage-reddit": dict(network="GraphSAGE", dataset="reddit", feature=602, layers=(1,)),
     "gin-products": dict(network="GIN", dataset="products", feature=100, layers=(1,), bf16=True),
 }

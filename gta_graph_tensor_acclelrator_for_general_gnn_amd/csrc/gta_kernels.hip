@@ -883,6 +883,81 @@ k_apply_node(int bin, int sf, int64_t n, const float* __restrict__ a, int64_t ld
 }
 
 // ---------------------------------------------------------------------------
+// K3' fused GAT edge-softmax: one wave per destination row; lane = k*H + h
+// handles edge slot k (64/H edges per step) and head h.  Indices arrive 64 at
+// a time (one coalesced load) and are handed to the lanes with ds_bpermute;
+// each step gathers H consecutive floats of b_src per edge.  Pass 1 sums v per
+// lane, a butterfly over the k bits gives the row sum per head; pass 2
+// recomputes v (same bits) and writes v / sum -- one contiguous 256-B store per
+// step.  normalize = 0 writes v in pass 1 and skips pass 2.
+// ---------------------------------------------------------------------------
+template <int H>
+__global__ void __launch_bounds__(kBlock)
+k_edge_softmax(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
+               const float* __restrict__ a, int64_t lda, const float* __restrict__ b, int64_t ldb, int sf,
+               int normalize, float* __restrict__ out, float* __restrict__ sums) {
+  constexpr int EPS = kWave / H;  // edges per step
+  constexpr int NB = H < 8 ? H : 8;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  const int h = lane % H, k = lane / H;
+  const int64_t beg = indptr[row], end = indptr[row + 1];
+  const float ar = a[row * lda + h];
+  float s = 0.f;
+  for (int pass = 0; pass < 2; ++pass) {
+    const float inv = s;  // pass 1: row sum (division below, not a reciprocal)
+    for (int64_t e0 = beg; e0 < end; e0 += kWave) {
+      const int cnt = (end - e0 < kWave) ? static_cast<int>(end - e0) : kWave;
+      const int mine = (lane < cnt) ? indices[e0 + lane] : 0;
+      if (cnt == kWave) {  // H steps of EPS edges, gathers issued NB at a time
+#pragma unroll
+        for (int j0 = 0; j0 < H; j0 += NB) {
+          float v[NB];
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            const int src = __shfl(mine, (j0 + j) * EPS + k);
+            v[j] = b[static_cast<int64_t>(src) * ldb + h];
+          }
+#pragma unroll
+          for (int j = 0; j < NB; ++j) {
+            const float x = sf_apply(sf, ar + v[j]);
+            float* o = out + (e0 + (j0 + j) * EPS + k) * H + h;
+            if (pass == 0) {
+              s += x;
+              if (!normalize) *o = x;
+            } else {
+              *o = x / inv;
+            }
+          }
+        }
+      } else {
+        for (int j = 0; j * EPS < cnt; ++j) {
+          const int slot = j * EPS + k;
+          const int src = __shfl(mine, slot < cnt ? slot : 0);
+          if (slot < cnt) {
+            const float x = sf_apply(sf, ar + b[static_cast<int64_t>(src) * ldb + h]);
+            float* o = out + (e0 + slot) * H + h;
+            if (pass == 0) {
+              s += x;
+              if (!normalize) *o = x;
+            } else {
+              *o = x / inv;
+            }
+          }
+        }
+      }
+    }
+    if (pass == 0) {
+#pragma unroll
+      for (int off = H; off < kWave; off <<= 1) s += __shfl_xor(s, off);
+      if (sums != nullptr && k == 0) sums[row * H + h] = s;
+      if (!normalize) break;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
 // K4 UPDATE: out = sf(X[r(m)] . W), fp32 via v_mfma_f32_16x16x4_f32.
 // Block tile 64x64, BK = 16, 4 waves as 2x2, each wave 32x32 = 2x2 MFMA tiles.
 // MFMA 16x16x4 f32 maps (cdna_hip_programming.md §3): lane l holds
@@ -1427,6 +1502,29 @@ int gta_apply_node(int bin, int sf, int64_t n, const float* a, int64_t lda, int6
   k_apply_node<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, S(stream)>>>(
       bin, sf, n, a, lda, static_cast<int>(Fa), b, ldb, static_cast<int>(Fb), out, ldo, static_cast<int>(Fo));
   GTA_LAUNCHED("k_apply_node");
+  return GTA_OK;
+}
+
+int gta_edge_softmax(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
+                     const float* a_dst, int64_t lda, const float* b_src, int64_t ldb, int64_t heads, int sf,
+                     int normalize, float* out, float* sums, void* stream) {
+  if (!indptr || !a_dst || !b_src || n_rows < 0 || nnz < 0 || (nnz > 0 && (!indices || !out)))
+    return fail(GTA_ERR_ARG, "edge_softmax: bad arguments");
+  if (heads <= 0 || heads > kWave || (heads & (heads - 1)))
+    return fail(GTA_ERR_UNSUPPORTED, "edge_softmax: heads must be a power of two <= 64");
+  if (lda < heads || ldb < heads) return fail(GTA_ERR_ARG, "edge_softmax: leading dimension < heads");
+  if (n_rows == 0) return GTA_OK;
+  const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+  switch (heads) {
+#define GTA_ESM(H_)                                                                                         \
+  case H_:                                                                                                  \
+    k_edge_softmax<H_><<<grid, dim3(kBlock), 0, S(stream)>>>(indptr, indices, n_rows, a_dst, lda, b_src, ldb, \
+                                                             sf, normalize, out, sums);                       \
+    break;
+    GTA_ESM(1) GTA_ESM(2) GTA_ESM(4) GTA_ESM(8) GTA_ESM(16) GTA_ESM(32) GTA_ESM(64)
+#undef GTA_ESM
+  }
+  GTA_LAUNCHED("k_edge_softmax");
   return GTA_OK;
 }
 

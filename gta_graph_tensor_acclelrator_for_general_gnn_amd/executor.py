@@ -119,6 +119,10 @@ class Executor:
             for src in opgraph.inputs[i]:
                 if src.kind == "op":
                     self.consumers[src.op].append(i)
+        #   fuse_softmax: GAT's score -> SF -> per-row sum (-> divide) chain runs as one
+        #   gta_edge_softmax launch (results equal to fp32 rounding, not bitwise)
+        self.fuse_softmax = True
+        self.softmax = self._match_softmax()
 
     # ---------------------------------------------------------------- inputs
     def _ext(self, op, slot):
@@ -195,6 +199,72 @@ class Executor:
     def _count(self, nbytes):
         self.alg_bytes += int(nbytes)
         self.launches += 1
+
+    # ------------------------------------------------------- edge softmax
+    def _match_softmax(self):
+        """GAT edge-softmax chains keyed by their score op A (vTCAD/GraphOP/genGraphOP.py:51-60):
+            A = applyedge ADD(scatter R(a), scatter C(b));  V = applyedge SF(A);  G = gather R(V)
+          original (ops 6,7,8,10,9): D = applyedge V / scatter R(G)  -> alpha, one launch
+          trans    (ops 6,8,9):      V and G from one launch (V's other consumer aggregates it)"""
+        ops_, ins, cons = self.g.ops, self.g.inputs, self.consumers
+
+        def only(i):
+            return len(cons[i]) == 1 and cons[i][0]
+
+        found = {}
+        for A in ops_:
+            if A.type != "applyedge" or A.comp != "ADD" or len(ins[A.idx]) != 2:
+                continue
+            srcs = [x.op for x in ins[A.idx] if x.kind == "op"]
+            if len(srcs) != 2:
+                continue
+            orders = sorted(ops_[i].order for i in srcs if ops_[i].type == "scatter")
+            if orders != ["C", "R"] or self.sem.bin_of(A) != "ADD":
+                continue
+            v = only(A.idx)
+            if v is False or ops_[v].type != "applyedge" or ops_[v].comp != "SF":
+                continue
+            gs = [c for c in cons[v] if ops_[c].type == "gather" and ops_[c].order == "R"]
+            if len(gs) != 1:
+                continue
+            G = gs[0]
+            pat = {"A": A.idx, "V": v, "G": G, "D": None}
+            S = only(G)
+            if S is not False and ops_[S].type == "scatter" and ops_[S].order == "R":
+                D = only(S)
+                if D is not False and set(cons[v]) == {G, D} and ops_[D].type == "applyedge":
+                    dins = [x.op if x.kind == "op" else None for x in ins[D]]
+                    b = self.sem.bin_of(ops_[D])
+                    if (b == "DIV" and dins == [v, S]) or (b == "RDIV" and dins == [S, v]):
+                        pat["D"], pat["S"] = D, S
+            found[A.idx] = pat
+        return found
+
+    def _eval_softmax(self, A, pat):
+        """Registers V, G (and D) as views of one gta_edge_softmax launch; returns A's own value."""
+        ins = self._inputs(A)
+        if not all(isinstance(x, Scat) for x in ins) or {x.mode for x in ins} != {"dst", "src"}:
+            return None
+        a = next(x.t for x in ins if x.mode == "dst")
+        b = next(x.t for x in ins if x.mode == "src")
+        H = a.shape[1]
+        if b.shape[1] != H or H > 64 or H & (H - 1):
+            return None
+        V, sf, norm = self.g.ops[pat["V"]], self.sem.sf_of(self.g.ops[pat["V"]]), pat["D"] is not None
+        E, n = self.graph.nnz, self.graph.n_rows
+
+        def launch():
+            out, sums = ops.edge_softmax(self.graph, a, b, sf, normalize=norm, want_sums=True)
+            self._count(E * (4 + 8 * H) + n * (8 + 8 * H))
+            return out, sums
+        shared = Lazy(launch)
+        self.values[pat["G"]] = Lazy(lambda: NodeT(shared.force()[1]))
+        if norm:
+            self.values[pat["D"]] = Lazy(lambda: EdgeT(shared.force()[0]))
+            self.values[V.idx] = Lazy(lambda: self._eval_applyedge(A, post_sf=sf))
+        else:
+            self.values[V.idx] = Lazy(lambda: EdgeT(shared.force()[0]))
+        return Lazy(lambda: self._eval_applyedge(A))
 
     # ---------------------------------------------------------------- eval
     def _binary(self, op):
@@ -379,6 +449,10 @@ class Executor:
             if op.idx in block.stored and not (self.elide_scatter_stores and self.consumers[op.idx]):
                 return EdgeT(self._to_edge_tensor(s))
             return s
+        if self.fuse_softmax and op.idx in self.softmax:
+            v = self._eval_softmax(op, self.softmax[op.idx])
+            if v is not None:
+                return v
         if op.type == "applyedge":
             c = fused_into.get(op.idx)
             if c is not None and self.g.ops[c].type == "gather" and op.comp in ("MUL", "MM"):

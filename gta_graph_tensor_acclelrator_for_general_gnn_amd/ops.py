@@ -270,6 +270,32 @@ def apply_edge(graph, bin, sf, a, a_mode="edge", b=None, b_mode="edge", out=None
     return out
 
 
+def edge_softmax(graph, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize=True, out=None, sums=None,
+                 want_sums=False):
+    """Fused GAT edge-softmax (GAT ops 6-10, vTCAD/GraphOP/genGraphOP.py:51-60):
+    v[e] = sf(a_dst[dst(e)] + b_src[src(e)]); sums[i] = sum_{e in row i} v[e];
+    out[e] = v[e] / sums[dst(e)] (normalize) or v[e].  Returns (out [E, H], sums [N, H] or None)."""
+    _need_gpu(a_dst, b_src, out, sums, graph.indptr)
+    H = a_dst.shape[1]
+    if b_src.shape[1] != H:
+        raise ValueError("edge_softmax: a_dst and b_src need the same head count")
+    if a_dst.shape[0] < graph.n_rows or b_src.shape[0] < graph.n_cols:
+        raise ValueError("edge_softmax: score tensors have too few rows")
+    if out is None:
+        out = torch.empty(graph.nnz, H, dtype=torch.float32, device=a_dst.device)
+    if not out.is_contiguous() or tuple(out.shape) != (graph.nnz, H):
+        raise ValueError("edge_softmax: out must be a contiguous [E, H] tensor")
+    if sums is None and want_sums:
+        sums = torch.empty(graph.n_rows, H, dtype=torch.float32, device=a_dst.device)
+    if sums is not None and (not sums.is_contiguous() or tuple(sums.shape) != (graph.n_rows, H)):
+        raise ValueError("edge_softmax: sums must be a contiguous [N, H] tensor")
+    check(_L().gta_edge_softmax(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz, _ptr(a_dst),
+                                _rows(a_dst, "a_dst"), _ptr(b_src), _rows(b_src, "b_src"), H, _sf(sf),
+                                1 if normalize else 0, _ptr(out), _ptr(sums), _stream(a_dst.device)),
+          "edge_softmax")
+    return out, sums
+
+
 def apply_node(bin, sf, a, b=None, out=None, b_broadcast_row=False):
     """out[i] = sf(a[i] bin b[i]); b_broadcast_row: b is a single row for all i (e.g. (1+eps))."""
     _need_gpu(a, b, out)

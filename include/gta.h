@@ -138,6 +138,19 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
 int gta_gather_add(const int64_t* indptr, int64_t n_rows, int64_t nnz, const float* xe, int64_t ldxe,
                    int64_t F, float* y, int64_t ldy, int accumulate, void* stream);
 
+/* ---- K3' fused GAT edge-softmax (ops 6-10 of the GAT op graph) ------------
+ * v(e, h)     = sf( a_dst[dst(e), h] + b_src[src(e), h] )       (ops 6 ADD, 7 SF)
+ * sums[i, h]  = sum_{e in row i} v(e, h)                        (op 8 gather ADD)
+ * out[e, h]   = v(e, h) / sums[dst(e), h]   if normalize        (ops 10 scatter R, 9 "/")
+ *             = v(e, h)                      otherwise (GAT-trans: ops 6, 8, 9)
+ * heads in {1,2,4,...,64}; out [E, heads] and sums [N, heads] contiguous; sums
+ * may be NULL.  Zero in-degree rows get sums 0 and no edges.
+ * Reference: GAT op graph vTCAD/GraphOP/genGraphOP.py:51-60 (ops 4-10),
+ * template/GAT_op.png (alpha = exp / sum exp); SF unit code/interpreter.py:7. */
+int gta_edge_softmax(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
+                     const float* a_dst, int64_t lda, const float* b_src, int64_t ldb, int64_t heads, int sf,
+                     int normalize, float* out, float* sums, void* stream);
+
 /* ---- K3 APPLYEDGE element-wise -----------------------------------------
  * out[e, c] = sf( a[ia(e), c_a] (bin) b[ib(e), c_b] )   for c < max(Fa, Fb)
  * ia/ib per GTA_IDX_*; the narrower operand is broadcast in contiguous

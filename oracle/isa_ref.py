@@ -104,6 +104,18 @@ def apply_node(bin_kind, sf_kind, a, b=None, b_broadcast_row=False):
     return sf(sf_kind, binop(bin_kind, A, B))
 
 
+def edge_softmax(indptr, indices, a_dst, b_src, sf_kind="EXP_LEAKY_RELU", normalize=True):
+    """GAT ops 6-10 composed from the ISA ops above (vTCAD/GraphOP/genGraphOP.py:51-60;
+    "/" per template/GAT_op.png): v = sf(scatter_R(a) + scatter_C(b)), sums = gather_R(v),
+    out = v / scatter_R(sums) (normalize) or v.  Returns (out, sums)."""
+    v = apply_edge(indptr, indices, "ADD", sf_kind, a_dst, "dst", b_src, "src")
+    sums = gather_add(indptr, v)
+    if not normalize:
+        return v, sums
+    with np.errstate(divide="ignore", invalid="ignore"):
+        return v / sums[row_of_edge(indptr)], sums
+
+
 def aggregate(indptr, indices, x, x_mode="src", w=None, row_scale=None):
     """Fused applyedge MUL -> gather ADD with the scatter FETCH removed
     (hardware_info.yaml Inst_fused [applyedge,gather][MUL,ADD]; code/interpreter.py:575-636, 764-802):

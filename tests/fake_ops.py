@@ -41,6 +41,12 @@ def apply_edge(graph, bin, sf, a, a_mode="edge", b=None, b_mode="edge", out=None
     return _t(isa_ref.apply_edge(ip, ix, bin, sf, _np(a), a_mode, _np(b), b_mode, b_broadcast_row))
 
 
+def edge_softmax(graph, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize=True, out=None, sums=None, want_sums=False):
+    ip, ix = graph.numpy()
+    o, su = isa_ref.edge_softmax(ip, ix, _np(a_dst), _np(b_src), sf, normalize)
+    return _t(o), (_t(su) if (want_sums or sums is not None) else None)
+
+
 def apply_node(bin, sf, a, b=None, out=None, b_broadcast_row=False):
     return _t(isa_ref.apply_node(bin, sf, _np(a), _np(b), b_broadcast_row))
 

@@ -106,3 +106,29 @@ def test_executor_deterministic(golden_dir, manifest, cora, dev):
     b, _ = executor.run_stream(og, st, gd, tensors, sem)
     for k in a.outputs:
         assert torch.equal(a.outputs[k], b.outputs[k])
+
+
+@pytest.mark.parametrize("reorder", [False, True])
+def test_gat_softmax_fusion_on_gpu(golden_dir, manifest, cora, dev, reorder):
+    """GAT ops 6-10 run as one gta_edge_softmax launch: fewer launches, same values (fp32 rounding)
+    as the unfused op-by-op path, and both match the fp64 oracle."""
+    rec = [s for s in _all_streams(manifest) if s["network"] == "GAT" and s["reorder"] == reorder][0]
+    ip, ix = cora
+    sem = Semantics.for_network("GAT", reorder)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    gd = G.from_numpy(ip, ix, device=dev)
+    tensors = {k: v.to(dev) for k, v in workloads.make_tensors(og, G.from_numpy(ip, ix), "GAT", seed=5).items()}
+    outs = {}
+    for fuse in (True, False):
+        ex = executor.Executor(og, st, gd, tensors, sem)
+        ex.fuse_softmax = fuse
+        assert bool(ex.softmax) is True
+        outs[fuse] = ({k: v.clone() for k, v in ex.run().items()}, ex.launches)
+    (fo, fl), (uo, ul) = outs[True], outs[False]
+    assert fl < ul, (fl, ul)
+    for k in uo:
+        a, b = fo[k].double().cpu(), uo[k].double().cpu()
+        fin = torch.isfinite(b)
+        assert torch.equal(torch.isfinite(a), fin)
+        assert (a[fin] - b[fin]).abs().max() <= 1e-4 * b[fin].abs().max() + 1e-6

@@ -279,3 +279,41 @@ def test_aggregate_blocked_rejects_unsorted_rows(dev):
     x = torch.zeros(4, 128, device=dev)
     with pytest.raises(ValueError):
         ops.aggregate_blocked(g, x, None, blocks=2)
+
+
+@pytest.mark.parametrize("heads", [1, 2, 4, 8, 16, 32, 64])
+@pytest.mark.parametrize("normalize", [True, False])
+def test_edge_softmax_matches_oracle(dev, heads, normalize):
+    """Fused GAT ops 6-10 vs the oracle's composition of the unfused ISA ops; the graph has
+    empty rows, a 700-edge row (full 64-edge chunks + tail) and short rows (tail only)."""
+    g, ip, ix = _graph(400, 5000, seed=3, empty_rows=20, heavy_row=700, dev=dev)
+    rng = np.random.default_rng(heads)
+    a = rng.standard_normal((g.n_rows, heads)).astype(np.float32)
+    bt = rng.standard_normal((g.n_rows, heads + 3)).astype(np.float32)
+    b = bt[:, :heads]  # leading dimension heads + 3
+    out, sums = ops.edge_softmax(g, torch.from_numpy(a).to(dev), torch.from_numpy(bt).to(dev)[:, :heads],
+                                 "EXP_LEAKY_RELU",
+                                 normalize=normalize, want_sums=True)
+    ref, rsum = isa_ref.edge_softmax(ip, ix, a.astype(np.float64), b.astype(np.float64), "EXP_LEAKY_RELU", normalize)
+    _check(sums, rsum, rsum, f"edge_softmax sums H={heads}")
+    # alpha = v / s: relative error of v (1 ulp) plus that of s (fp32 sum of deg terms)
+    deg = np.diff(ip)[isa_ref.row_of_edge(ip)][:, None]
+    _check(out, ref, np.abs(ref) * np.maximum(deg, 1), f"edge_softmax out H={heads}")
+    if normalize:  # every non-empty row's alpha sums to 1 per head
+        s = isa_ref.gather_add(ip, out.cpu().numpy().astype(np.float64))
+        nz = np.diff(ip) > 0
+        assert np.allclose(s[nz], 1.0, atol=1e-5)
+
+
+def test_edge_softmax_other_sf_and_errors(dev):
+    g, ip, ix = _graph(200, 2000, seed=4, dev=dev)
+    a = torch.randn(g.n_rows, 8, device=dev)
+    b = torch.randn(g.n_rows, 8, device=dev)
+    out, sums = ops.edge_softmax(g, a, b, "SIGMOID", normalize=True)
+    assert sums is None
+    ref, _ = isa_ref.edge_softmax(ip, ix, a.double().cpu().numpy(), b.double().cpu().numpy(), "SIGMOID", True)
+    _check(out, ref, np.abs(ref) * 64, "edge_softmax SIGMOID")
+    with pytest.raises(ops._lib.GTAError):
+        ops.edge_softmax(g, a[:, :6].contiguous(), b[:, :6].contiguous())
+    with pytest.raises(ValueError):
+        ops.edge_softmax(g, a, b[:, :4].contiguous())

@@ -94,3 +94,36 @@ def test_executor_plans_every_golden_stream(golden_dir, manifest, monkeypatch, i
     vals = {i: ex.tensor_of(i) for i in range(len(og))}
     compare(vals, ref, range(len(og)))
     assert set(outs) == {op.idx for op in og.ops if not op.out_list}
+
+
+@pytest.mark.parametrize("network,reorder,expect", [
+    ("GAT", False, {6: {"A": 6, "V": 7, "G": 8, "D": 9, "S": 10}}),
+    ("GAT", True, {6: {"A": 6, "V": 8, "G": 9, "D": None}}),
+    ("GCN", False, {}), ("GIN", False, {}), ("GraphSAGE", True, {}),
+])
+def test_softmax_chain_matching(golden_dir, network, reorder, expect):
+    """GAT ops 6-10 (genGraphOP.py:51-60) are recognised as one edge-softmax; nothing else is."""
+    sem = Semantics.for_network(network, reorder)
+    g = ir.OpGraph.load(os.path.join(golden_dir, "ops", f"{network}-cora-layer1-{'trans' if reorder else 'original'}.yaml"),
+                        sem.inputs)
+    assert executor.Executor(g, None, None, {}, sem).softmax == expect
+
+
+@pytest.mark.parametrize("reorder", [False, True])
+def test_softmax_fusion_cpu_equivalence(golden_dir, manifest, monkeypatch, reorder):
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    rec = [s for s in _streams(manifest) if s["network"] == "GAT" and s["reorder"] == reorder][1]
+    sem = Semantics.for_network("GAT", reorder)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    gc, ip, ix = _cora_graph(golden_dir)
+    tensors = workloads.make_tensors(og, gc, "GAT", seed=1)
+    runs = []
+    for fuse in (True, False):
+        ex = executor.Executor(og, st, gc, tensors, sem)
+        ex.fuse_softmax = fuse
+        runs.append((ex.run(), ex.launches))
+    assert runs[0][1] < runs[1][1]
+    ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
+    for outs, _ in runs:
+        compare(outs, ref, outs.keys())
