@@ -58,13 +58,7 @@ def make_inputs(n, e, device, seed=0):
 
 
 def auto_blocks(graph, f):
-    """Column blocks for the blocked aggregate: X slices of ~7.5 MB (half an XCD L2 x 4 -- the
-    measured optimum on the 1-GPU Reddit shape was B = 16 for a 119 MB table, profiles/
-    r01_agg_sweep_*), capped so a row still has >= 24 edges per block on average (each
-    (block, row) item pays a fixed start-up; at 8 GPUs a shard's rows hold ~61 edges)."""
-    table_mb = graph.n_cols * f * 4 / 1e6
-    avg_deg = graph.nnz / max(1, graph.n_rows)
-    return int(max(1, min(16, round(table_mb / 7.5), avg_deg // 24)))
+    return ops.BlockedPlan.auto_blocks(graph, f)
 
 
 def cpu_baseline(g, x, alpha, target_s=12.0):

@@ -957,6 +957,107 @@ k_edge_softmax(const int64_t* __restrict__ indptr, const int32_t* __restrict__ i
   }
 }
 
+// Edge-per-lane form for H in {4, 8, 16} (16-B aligned rows): lane l owns edge
+// e0 + l of a 64-edge chunk and loads its H source scores as H/4 float4 -- one
+// gather per edge per row visit.  The first K chunks of the row keep v in
+// VGPRs; later chunks park v in `out` during pass 1 and pass 2 reads it back
+// (coalesced), so every source row is gathered exactly once.  Row sums: per
+// lane, then a butterfly over all 64 lanes.
+template <int H, int K>
+__global__ void __launch_bounds__(kBlock)
+k_edge_softmax_v(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
+                 const float* __restrict__ a, int64_t lda, const float* __restrict__ b, int64_t ldb, int sf,
+                 int normalize, float* __restrict__ out, float* __restrict__ sums) {
+  constexpr int Q = H / 4;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  const int64_t beg = indptr[row], end = indptr[row + 1];
+  float ar[H], s[H];
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+    ar[h] = a[row * lda + h];
+    s[h] = 0.f;
+  }
+  float4 keep[K][Q];
+  auto visit = [&](int64_t e0, float4 (&v)[Q]) {  // gather + sf for the chunk at e0; returns v in place
+    const int64_t e = e0 + lane;
+    const bool ok = e < end;
+    const int src = ok ? indices[e] : 0;
+    const float4* bp = reinterpret_cast<const float4*>(b + static_cast<int64_t>(src) * ldb);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) v[q] = ok ? bp[q] : make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      float* c = reinterpret_cast<float*>(&v[q]);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const float x = ok ? sf_apply(sf, ar[4 * q + t] + c[t]) : 0.f;
+        c[t] = x;
+        s[4 * q + t] += x;
+      }
+    }
+    return ok;
+  };
+  // pass 1
+  int64_t e0 = beg;
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    if (e0 < end) {
+      const bool ok = visit(e0, keep[c]);
+      if (!normalize && ok) {
+        float4* o = reinterpret_cast<float4*>(out + (e0 + lane) * H);
+#pragma unroll
+        for (int q = 0; q < Q; ++q) o[q] = keep[c][q];
+      }
+    }
+    e0 += kWave;
+  }
+  for (int64_t f0 = beg + K * kWave; f0 < end; f0 += kWave) {
+    float4 v[Q];
+    if (visit(f0, v)) {
+      float4* o = reinterpret_cast<float4*>(out + (f0 + lane) * H);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) o[q] = v[q];
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < H; ++h) {
+#pragma unroll
+    for (int off = 1; off < kWave; off <<= 1) s[h] += __shfl_xor(s[h], off);
+  }
+  if (sums != nullptr && lane < H) {
+    float sv = s[0];
+#pragma unroll
+    for (int h = 1; h < H; ++h) sv = (lane == h) ? s[h] : sv;
+    sums[row * H + lane] = sv;
+  }
+  if (!normalize) return;
+  // pass 2: v / s
+  e0 = beg;
+#pragma unroll
+  for (int c = 0; c < K; ++c) {
+    if (e0 + lane < end) {
+      float4* o = reinterpret_cast<float4*>(out + (e0 + lane) * H);
+#pragma unroll
+      for (int q = 0; q < Q; ++q)
+        o[q] = make_float4(keep[c][q].x / s[4 * q], keep[c][q].y / s[4 * q + 1], keep[c][q].z / s[4 * q + 2],
+                           keep[c][q].w / s[4 * q + 3]);
+    }
+    e0 += kWave;
+  }
+  for (int64_t f0 = beg + K * kWave; f0 < end; f0 += kWave) {
+    if (f0 + lane < end) {
+      float4* o = reinterpret_cast<float4*>(out + (f0 + lane) * H);
+#pragma unroll
+      for (int q = 0; q < Q; ++q) {
+        const float4 v = o[q];
+        o[q] = make_float4(v.x / s[4 * q], v.y / s[4 * q + 1], v.z / s[4 * q + 2], v.w / s[4 * q + 3]);
+      }
+    }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K4 UPDATE: out = sf(X[r(m)] . W), fp32 via v_mfma_f32_16x16x4_f32.
 // Block tile 64x64, BK = 16, 4 waves as 2x2, each wave 32x32 = 2x2 MFMA tiles.
@@ -1179,6 +1280,8 @@ int g_force_vw = 0;
 int g_agg_nt = 0;     // non-temporal index/weight loads in the SpMM form
 int g_agg_lean = 1;   // k_agg_lean for F = 64*VW SpMM shapes
 int64_t g_seg_waves = 0;  // persistent waves of the column-blocked kernel (0 = 8 per SIMD)
+int g_esm_lane = 1;        // edge-per-lane edge-softmax when H in {4,8,16} and rows are 16-B aligned
+int g_esm_keep = 4;        // chunks of 64 edges held in VGPRs by the edge-per-lane form (2 or 4)
 
 }  // namespace
 
@@ -1198,6 +1301,8 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "agg_nt") { g_agg_nt = static_cast<int>(value); return 0; }
   if (k == "agg_lean") { g_agg_lean = static_cast<int>(value); return 0; }
   if (k == "seg_waves") { g_seg_waves = value; return 0; }
+  if (k == "esm_lane") { g_esm_lane = static_cast<int>(value); return 0; }
+  if (k == "esm_keep") { g_esm_keep = static_cast<int>(value); return 0; }
   return fail(GTA_ERR_ARG, "gta_debug_set: unknown key " + k);
 }
 
@@ -1515,6 +1620,20 @@ int gta_edge_softmax(const int64_t* indptr, const int32_t* indices, int64_t n_ro
   if (lda < heads || ldb < heads) return fail(GTA_ERR_ARG, "edge_softmax: leading dimension < heads");
   if (n_rows == 0) return GTA_OK;
   const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+  const bool vec = g_esm_lane && (heads == 4 || heads == 8 || heads == 16) && ldb % 4 == 0 && aligned(b_src, 16) &&
+                   (nnz == 0 || aligned(out, 16));
+  if (vec) {
+#define GTA_ESMV(H_, K_)                                                                                          \
+  k_edge_softmax_v<H_, K_><<<grid, dim3(kBlock), 0, S(stream)>>>(indptr, indices, n_rows, a_dst, lda, b_src, ldb, \
+                                                                 sf, normalize, out, sums)
+    const bool k4 = g_esm_keep >= 4 && heads <= 8;
+    if (heads == 4) { if (k4) GTA_ESMV(4, 4); else GTA_ESMV(4, 2); }
+    else if (heads == 8) { if (k4) GTA_ESMV(8, 4); else GTA_ESMV(8, 2); }
+    else GTA_ESMV(16, 2);
+#undef GTA_ESMV
+    GTA_LAUNCHED("k_edge_softmax_v");
+    return GTA_OK;
+  }
   switch (heads) {
 #define GTA_ESM(H_)                                                                                         \
   case H_:                                                                                                  \

@@ -1,0 +1,136 @@
+"""Multi-GPU execution of a whole layer's instruction stream (BASELINE configs 4-5).
+
+Partition (the reference's column axis j of its T-row x 1-column edge tiles,
+code/preprocessing.py:26-38): the nodes are cut into `world` contiguous ranges
+[c_p, c_{p+1}) balanced by source-column nnz (partition.column_cuts).  Rank p
+  * owns the node rows of its range: every node tensor of the layer (model
+    input, GEMM outputs, aggregates) is held as that [n_p, F] row block;
+  * owns the edges whose SOURCE lies in its range, as a CSR over all
+    destination rows with local column ids, so a scatter C / aggregate
+    gathers only from its own row block.
+The CSR's destination rows are laid out padded, block q at rows
+[q*m, q*m + n_q) with m = max_q n_q, so a gather's partial [world*m, F]
+result is exactly the input of one reduce-scatter (RCCL over xGMI under the
+"nccl" backend) that hands each rank the summed rows of its own block.  This is
+the one exchange step of GCN / GraphSAGE / GIN layers: half the bytes of an
+all-reduce, and the next layer's scatter C reads the block the rank now owns.
+A scatter R (destination side, GAT's scores) needs every row: one all-gather
+of the [n_p, F] blocks.
+"""
+import torch
+import torch.distributed as dist
+
+from . import partition
+from .graph import Graph
+
+
+class DistShard:
+    """Rank `rank`'s part of `graph` (see module docstring)."""
+
+    def __init__(self, graph, rank, world, cuts=None):
+        cuts = partition.column_cuts(graph, world) if cuts is None else torch.as_tensor(cuts)
+        self.cuts = [int(c) for c in cuts]
+        self.rank, self.world = rank, world
+        self.c0, self.c1 = self.cuts[rank], self.cuts[rank + 1]
+        self.n_local = self.c1 - self.c0
+        self.m = max(self.cuts[q + 1] - self.cuts[q] for q in range(world))
+        self.n_global, self.e_global = graph.n_rows, graph.nnz
+        dev = graph.device
+        src = graph.indices
+        keep = (src >= self.c0) & (src < self.c1)
+        rows = graph.row_of_edge().long()[keep]
+        cuts_t = torch.tensor(self.cuts, device=dev, dtype=torch.int64)
+        blk = torch.searchsorted(cuts_t, rows, right=True) - 1
+        prow = blk * self.m + (rows - cuts_t[blk])  # padded destination row (monotone in rows)
+        counts = torch.bincount(prow, minlength=world * self.m)
+        indptr = torch.zeros(world * self.m + 1, dtype=torch.int64, device=dev)
+        indptr[1:] = torch.cumsum(counts, 0)
+        self.graph = Graph(indptr, (src[keep].long() - self.c0).to(torch.int32), n_cols=self.n_local)
+        self.edge_ids = torch.nonzero(keep, as_tuple=False).flatten()
+
+    def local_tensors(self, tensors):
+        """Global layer tensors -> this rank's: node tensors [N, *] -> row block, edge tensors
+        [E, *] -> the shard's edges (CSR order kept), weights / broadcast rows unchanged."""
+        out = {}
+        for k, t in tensors.items():
+            rows = t.shape[0] if t.dim() else 0
+            if k.startswith("w:"):
+                out[k] = t
+            elif k == "x_edge" or (rows == self.e_global and rows != self.n_global):
+                out[k] = t[self.edge_ids.to(t.device)].contiguous()
+            elif rows == self.n_global:
+                out[k] = t[self.c0:self.c1].contiguous()
+            else:
+                out[k] = t
+        return out
+
+
+class Comm:
+    """The executor's exchange hooks over torch.distributed (RCCL "nccl" or gloo)."""
+
+    def __init__(self, shard, group=None):
+        self.s, self.group = shard, group
+        self.on = dist.is_available() and dist.is_initialized() and shard.world > 1
+        self.nccl = self.on and dist.get_backend(group) == "nccl"
+        self.bytes = 0
+
+    @property
+    def n_local(self):
+        return self.s.n_local
+
+    def reduce_rows(self, y):
+        """Partial aggregate over padded rows [world*m, F] -> this rank's summed block [n_p, F]."""
+        s = self.s
+        if not self.on:
+            return y[s.rank * s.m: s.rank * s.m + s.n_local]
+        self.bytes += y.numel() * y.element_size()
+        if self.nccl:
+            out = torch.empty(s.m, y.shape[1], dtype=y.dtype, device=y.device)
+            dist.reduce_scatter_tensor(out, y.contiguous(), group=self.group)
+            return out[:s.n_local]
+        dist.all_reduce(y, group=self.group)  # gloo: no reduce-scatter
+        return y[s.rank * s.m: s.rank * s.m + s.n_local]
+
+    def gather_rows(self, x):
+        """This rank's block [n_p, F] -> every block, padded: [world*m, F] (dst-side scatters)."""
+        s = self.s
+        buf = torch.zeros(s.m, x.shape[1], dtype=x.dtype, device=x.device)
+        buf[:s.n_local] = x
+        if not self.on:
+            full = torch.zeros(s.world * s.m, x.shape[1], dtype=x.dtype, device=x.device)
+            full[s.rank * s.m:(s.rank + 1) * s.m] = buf
+            return full
+        self.bytes += buf.numel() * buf.element_size() * s.world
+        if self.nccl:
+            full = torch.empty(s.world * s.m, x.shape[1], dtype=x.dtype, device=x.device)
+            dist.all_gather_into_tensor(full, buf, group=self.group)
+            return full
+        parts = [torch.empty_like(buf) for _ in range(s.world)]
+        dist.all_gather(parts, buf, group=self.group)
+        return torch.cat(parts)
+
+    def full_rows(self, x):
+        """[n_p, F] blocks of every rank -> the unpadded global [N, F] (for results/tests)."""
+        s = self.s
+        full = self.gather_rows(x)
+        return torch.cat([full[q * s.m: q * s.m + s.cuts[q + 1] - s.cuts[q]] for q in range(s.world)])
+
+
+def run_stream(opgraph, stream, shard, tensors, semantics=None, group=None, plan_chunk=512):
+    """Execute one layer's stream on this rank's shard; returns (ExecResult, Executor).
+    `tensors` are the GLOBAL layer tensors (sliced here); outputs are this rank's row blocks."""
+    import time
+
+    from . import executor
+    comm = Comm(shard, group)
+    ex = executor.Executor(opgraph, stream, shard.graph, shard.local_tensors(tensors), semantics, plan_chunk,
+                           dist=comm)
+    cuda = shard.graph.device.type == "cuda"
+    if cuda:
+        torch.cuda.synchronize(shard.graph.device)
+    t0 = time.perf_counter()
+    outputs = ex.run()
+    if cuda:
+        torch.cuda.synchronize(shard.graph.device)
+    res = executor.ExecResult(ex.values, outputs, time.perf_counter() - t0, ex.alg_bytes, ex.launches)
+    return res, ex

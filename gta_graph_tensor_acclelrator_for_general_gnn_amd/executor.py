@@ -95,8 +95,12 @@ MAX_MATERIALIZE_BYTES = 96 << 30  # refuse to materialise a single edge tensor l
 
 
 class Executor:
-    def __init__(self, opgraph, stream, graph, tensors, semantics=None, plan_chunk=512):
+    def __init__(self, opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, dist=None):
         self.g = opgraph
+        # dist (distributed.Comm): node tensors are this rank's row block; gathers are
+        # reduce-scattered to it and dst-side scatters all-gather it (distributed.py)
+        self.dist = dist
+        self.n_nodes = dist.n_local if dist is not None else (graph.n_rows if graph is not None else 0)
         self.stream = stream
         self.graph = graph
         self.tensors = dict(tensors)
@@ -113,7 +117,7 @@ class Executor:
         # weighted/unweighted SpMM aggregates whose gathered table exceeds the chip's L2
         # run column-blocked (L2-resident slices) when the shape allows it
         self.blocked_min_table_bytes = 32 << 20
-        self.blocked_blocks = 16
+        self.blocked_blocks = "auto"  # ops.BlockedPlan.auto_blocks, or a fixed count (0 = never)
         self.consumers = {i: [] for i in range(len(opgraph))}
         for i in range(len(opgraph)):
             for src in opgraph.inputs[i]:
@@ -121,7 +125,7 @@ class Executor:
                     self.consumers[src.op].append(i)
         #   fuse_softmax: GAT's score -> SF -> per-row sum (-> divide) chain runs as one
         #   gta_edge_softmax launch (results equal to fp32 rounding, not bitwise)
-        self.fuse_softmax = True
+        self.fuse_softmax = dist is None  # per-row sums span ranks: unfused ops + exchanges
         self.softmax = self._match_softmax()
 
     # ---------------------------------------------------------------- inputs
@@ -152,11 +156,11 @@ class Executor:
     def _wrap_ext(self, t):
         if t.dim() == 1:
             t = t.view(-1, 1)
-        if t.shape[0] == self.graph.nnz and t.shape[0] != self.graph.n_rows:
+        if t.shape[0] == self.graph.nnz and t.shape[0] != self.n_nodes:
             return EdgeT(t)
         if t.shape[0] == 1:
             return ("row", t)
-        if t.shape[0] == self.graph.n_rows and t.shape[0] != self.graph.nnz:
+        if t.shape[0] == self.n_nodes and t.shape[0] != self.graph.nnz:
             return NodeT(t)
         return EdgeT(t)  # ambiguous N == E: edge tensor
 
@@ -384,10 +388,14 @@ class Executor:
     def _spmm(self, xt, mode, wt):
         """SpMM-form aggregate: column-blocked when the gathered table outgrows L2, else row-chunked."""
         heads = 0 if wt is None else wt.shape[1]
-        if (mode == "src" and self.blocked_blocks and xt.numel() * 4 >= self.blocked_min_table_bytes
-                and ops.BlockedPlan.supports(xt.shape[1], heads)
-                and self.graph.blocked_plan(self.blocked_blocks).sorted):
-            return ops.aggregate_blocked(self.graph, xt, wt, blocks=self.blocked_blocks)
+        if (mode == "src" and self.blocked_blocks and xt.shape[0] * xt.shape[1] * 4 >= self.blocked_min_table_bytes
+                and ops.BlockedPlan.supports(xt.shape[1], heads)):
+            B = self.blocked_blocks
+            if B == "auto":
+                B = ops.BlockedPlan.auto_blocks(self.graph, xt.shape[1])
+                B = B if B >= 4 else 0
+            if B and self.graph.blocked_plan(B).sorted:
+                return ops.aggregate_blocked(self.graph, xt, wt, blocks=B)
         return ops.aggregate(self.graph, xt, mode, wt, plan=self._plan())
 
     def _unweighted(self, x):
@@ -397,7 +405,7 @@ class Executor:
 
     def _eval_applynode(self, op, post_sf=None):
         ins = self._inputs(op)
-        n = self.graph.n_rows
+        n = self.n_nodes
         if op.comp == "MM":
             W = self.tensors[f"w:{op.idx}"]
             x = self._node(ins[0])
@@ -432,7 +440,7 @@ class Executor:
         if isinstance(v, NodeT):
             return v.t
         if isinstance(v, tuple) and v[0] == "row":
-            return v[1].expand(self.graph.n_rows, v[1].shape[1]).contiguous()
+            return v[1].expand(self.n_nodes, v[1].shape[1]).contiguous()
         raise TypeError(f"applynode operand is not a node tensor ({type(v).__name__})")
 
     def _eval(self, op, block):
@@ -443,7 +451,10 @@ class Executor:
                 v = NodeT(self._node(v))
             if not isinstance(v, NodeT):
                 raise TypeError(f"scatter op {op.idx} needs a node tensor")
-            s = Scat(v.t, "src" if op.order == "C" else "dst")
+            t = v.t
+            if op.order != "C" and self.dist is not None:
+                t = self.dist.gather_rows(t)
+            s = Scat(t, "src" if op.order == "C" else "dst")
             # a STORE_E'd scatter is only materialised when nothing reads it back (a sink):
             # every consumer kernel gathers by index, which is the same bytes
             if op.idx in block.stored and not (self.elide_scatter_stores and self.consumers[op.idx]):
@@ -465,7 +476,8 @@ class Executor:
         if op.type == "applyedge":
             return self._eval_applyedge(op)
         if op.type == "gather":
-            return self._eval_gather(op)
+            v = self._eval_gather(op)
+            return NodeT(self.dist.reduce_rows(v.t)) if self.dist is not None else v
         if op.type == "applynode":
             return self._eval_applynode(op)
         raise ValueError(op.type)

@@ -157,6 +157,17 @@ class BlockedPlan:
         return self._ws[F]
 
     @staticmethod
+    def auto_blocks(graph, F):
+        """Column blocks for a gathered table of graph.n_cols x F fp32: slices of ~7.5 MB (the
+        measured optimum on the 1-GPU Reddit shape was B = 16 for a 119 MB table, profiles/
+        r01_agg_sweep_*), capped so a row keeps >= 24 edges per block on average (each
+        (block, row) item pays a fixed start-up; an 8-GPU Reddit shard's rows hold ~61 edges).
+        Below 4 the single-pass row-chunk kernel is the better choice."""
+        table_mb = graph.n_cols * F * 4 / 1e6
+        avg_deg = graph.nnz / max(1, graph.n_rows)
+        return int(max(1, min(16, round(table_mb / 7.5), avg_deg // 24)))
+
+    @staticmethod
     def supports(F, heads, x=None):
         vw = F // 64 if F in (64, 128, 256) else 0
         if not vw:

@@ -10,7 +10,7 @@ stop_if_fatal() {  # $1 = rc, $2 = step name; test failures (rc 1) are not fatal
 for s in $STEPS; do
   case $s in
     tests)
-      timeout -k 10 ${T_TESTS:-700} python -m pytest tests -m gpu -x -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
+      timeout -k 10 ${T_TESTS:-700} python -m pytest ${PYTEST_TARGET:-tests} -m gpu -x -q ${PYTEST_ARGS} > gpurun_out/pytest_gpu.log 2>&1
       rc=$?; echo "pytest_gpu rc=$rc"; tail -5 gpurun_out/pytest_gpu.log; stop_if_fatal $rc tests ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
@@ -37,7 +37,7 @@ for s in $STEPS; do
         > gpurun_out/bench2.log 2>&1
       rc=$?; echo "bench2 rc=$rc"; grep '^{' gpurun_out/bench2.log | tail -1; stop_if_fatal $rc bench2 ;;
     layers)
-      timeout -k 10 ${T_LAYERS:-600} python scripts/layer_bench.py > gpurun_out/layers.log 2>&1
+      timeout -k 10 ${T_LAYERS:-600} python scripts/layer_bench.py ${LAYER_ARGS} > gpurun_out/layers.log 2>&1
       rc=$?; echo "layers rc=$rc"; tail -6 gpurun_out/layers.log; stop_if_fatal $rc layers ;;
     sweep)
       timeout -k 10 ${T_SWEEP:-600} python scripts/agg_sweep.py ${SWEEP_ARGS} > gpurun_out/sweep.log 2>&1

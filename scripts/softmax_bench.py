@@ -1,0 +1,59 @@
+"""Time gta_edge_softmax variants on the Reddit-shaped graph (8 heads) and cross-check them."""
+import json
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G, ops  # noqa: E402
+
+
+def timed(fn, reps=10):
+    fn()
+    torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(2)]
+    ev[0].record()
+    for _ in range(reps):
+        fn()
+    ev[1].record()
+    torch.cuda.synchronize()
+    return ev[0].elapsed_time(ev[1]) / reps
+
+
+def main():
+    dev = torch.device("cuda:0")
+    dataset = sys.argv[1] if len(sys.argv) > 1 else "reddit"
+    H = int(sys.argv[2]) if len(sys.argv) > 2 else 8
+    g = G.dataset_graph(dataset, device=dev)
+    torch.manual_seed(0)
+    a = torch.randn(g.n_rows, H, device=dev)
+    b = torch.randn(g.n_rows, H, device=dev)
+    out = torch.empty(g.nnz, H, device=dev)
+    sums = torch.empty(g.n_rows, H, device=dev)
+    alg = g.nnz * (4 + 8 * H) + g.n_rows * (8 + 8 * H)
+    res, ref = {}, None
+    for name, knobs in [("lane0", {"esm_lane": 0}), ("v_k2", {"esm_lane": 1, "esm_keep": 2}),
+                        ("v_k4", {"esm_lane": 1, "esm_keep": 4})]:
+        for k, v in knobs.items():
+            ops.set_debug(k, v)
+        for norm in (True, False):
+            ms = timed(lambda: ops.edge_softmax(g, a, b, normalize=norm, out=out, sums=sums))
+            key = f"{name}:{'norm' if norm else 'raw'}"
+            res[key] = {"ms": ms, "alg_TBps": alg / ms / 1e9}
+            if norm:
+                if ref is None:
+                    ref = out.clone()
+                else:
+                    res[key]["maxdiff_vs_lane0"] = float((out - ref).abs().max())
+            print(key, json.dumps(res[key]), flush=True)
+    ops.set_debug("esm_lane", 1)
+    ops.set_debug("esm_keep", 4)
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", f"softmax_bench_{dataset}_{H}.json"), "w") as f:
+        json.dump({"N": g.n_rows, "E": g.nnz, "H": H, "alg_bytes": alg, "variants": res}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
