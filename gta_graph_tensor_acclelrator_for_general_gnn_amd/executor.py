@@ -125,8 +125,13 @@ class Executor:
                     self.consumers[src.op].append(i)
         #   fuse_softmax: GAT's score -> SF -> per-row sum (-> divide) chain runs as one
         #   gta_edge_softmax launch (results equal to fp32 rounding, not bitwise)
-        self.fuse_softmax = dist is None  # per-row sums span ranks: unfused ops + exchanges
+        self.fuse_softmax = dist is None or not dist.on  # per-row sums span ranks: unfused ops + exchanges
         self.softmax = self._match_softmax()
+        #   mm_first: a gather whose only consumer is a narrowing applynode MM is executed as
+        #   MM-then-aggregate (sum_e w_e x_src) W == sum_e w_e (x W)_src -- the layer's output
+        #   to fp32 rounding, the gather's own value computed only if something asks for it
+        self.mm_first = True
+        self.reorder = self._match_mm_first()
 
     # ---------------------------------------------------------------- inputs
     def _ext(self, op, slot):
@@ -243,6 +248,74 @@ class Executor:
                         pat["D"], pat["S"] = D, S
             found[A.idx] = pat
         return found
+
+    def _match_mm_first(self):
+        """{gather G: MM op M} for G -> M with M the only consumer, narrowing the width, and G
+        reading a scatter C directly or through a (weight) MUL (GraphSAGE / GCN layer 1)."""
+        found = {}
+        for G in self.g.ops:
+            if G.type != "gather" or G.order != "R" or len(self.consumers[G.idx]) != 1:
+                continue
+            M = self.g.ops[self.consumers[G.idx][0]]
+            if M.type != "applynode" or M.comp != "MM" or len(self.g.inputs[M.idx]) != 1:
+                continue
+            if not (M.out_width and G.out_width and M.out_width < G.out_width):
+                continue
+            src = self.g.inputs[G.idx][0]
+            if src.kind != "op":
+                continue
+            P = self.g.ops[src.op]
+            if P.type == "applyedge" and P.comp == "MUL":
+                scat = [x.op for x in self.g.inputs[P.idx] if x.kind == "op" and self.g.ops[x.op].type == "scatter"]
+                if len(scat) != 1 or self.g.ops[scat[0]].order != "C":
+                    continue
+            elif not (P.type == "scatter" and P.order == "C"):
+                continue
+            found[G.idx] = M.idx
+        return found
+
+    def _gather_value(self, op):
+        v = self._eval_gather(op)
+        return NodeT(self.dist.reduce_rows(v.t)) if self.dist is not None else v
+
+    def _eval_mm_first(self, G, M):
+        """Sets M's value to aggregate(x W) and returns G's value lazily; None if the operands
+        do not allow it (head-wise weights, edge-tensor features)."""
+        v = self._source(G, 0)
+        if isinstance(v, Deferred):
+            p = self.g.ops[v.op]
+            if p.comp != "MUL" or self.sem.bin_of(p) != "MUL":
+                return None
+            pins = self._inputs(p)
+            if len(pins) == 1:
+                extra = self._ext(p, 1)
+                pins = pins + ([self._wrap_ext(extra)] if extra is not None else [])
+            xs = [z for z in pins if isinstance(z, Scat) and z.mode == "src"]
+            ws = [z for z in pins if not (isinstance(z, Scat) and z.mode == "src")]
+            if len(xs) != 1 or len(ws) > 1:
+                return None
+            x, w = xs[0].t, None
+            if ws:
+                if isinstance(ws[0], tuple) or ws[0] is None:
+                    return None
+                w = self._to_edge_tensor(ws[0])
+                if w.shape[1] != 1:
+                    return None
+        elif isinstance(v, Scat) and v.mode == "src":
+            x, w = v.t, None
+        else:
+            return None
+        W = self.tensors[f"w:{M.idx}"]
+        if W.shape[0] != x.shape[1]:
+            return None
+        x, W = self._mm_dtypes(x, W)
+        xw = ops.update_mm(x, W)
+        self._count(x.shape[0] * (x.shape[1] * x.element_size() + W.shape[1] * 4) + W.numel() * W.element_size())
+        n, E, F = self.graph.n_rows, self.graph.nnz, xw.shape[1]
+        y = self._spmm(xw, "src", w)
+        self._count(E * (4 + (4 if w is not None else 0) + 4 * F) + n * (8 + 4 * F))
+        self.values[M.idx] = NodeT(self.dist.reduce_rows(y) if self.dist is not None else y)
+        return Lazy(lambda: self._gather_value(G))
 
     def _eval_softmax(self, A, pat):
         """Registers V, G (and D) as views of one gta_edge_softmax launch; returns A's own value."""
@@ -476,8 +549,11 @@ class Executor:
         if op.type == "applyedge":
             return self._eval_applyedge(op)
         if op.type == "gather":
-            v = self._eval_gather(op)
-            return NodeT(self.dist.reduce_rows(v.t)) if self.dist is not None else v
+            if self.mm_first and op.idx in self.reorder:
+                v = self._eval_mm_first(op, self.g.ops[self.reorder[op.idx]])
+                if v is not None:
+                    return v
+            return self._gather_value(op)
         if op.type == "applynode":
             return self._eval_applynode(op)
         raise ValueError(op.type)

@@ -127,3 +127,26 @@ def test_softmax_fusion_cpu_equivalence(golden_dir, manifest, monkeypatch, reord
     ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
     for outs, _ in runs:
         compare(outs, ref, outs.keys())
+
+
+@pytest.mark.parametrize("network", ["GraphSAGE", "GCN", "SGC"])
+def test_mm_first_reordering_cpu(golden_dir, manifest, monkeypatch, network):
+    """gather -> narrowing MM runs as MM -> aggregate: fewer algorithmic bytes, the MM's value
+    equal to the oracle's (sum_e w x) W within fp32 rounding, the gather itself still available."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    rec = [s for s in _streams(manifest) if s["network"] == network and not s["reorder"]][0]
+    sem = Semantics.for_network(network, False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    gc, ip, ix = _cora_graph(golden_dir)
+    tensors = workloads.make_tensors(og, gc, network, seed=2)
+    ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
+    nbytes = {}
+    for on in (True, False):
+        ex = executor.Executor(og, st, gc, tensors, sem)
+        ex.mm_first = on
+        assert ex.reorder
+        ex.run()
+        nbytes[on] = ex.alg_bytes
+        compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
+    assert nbytes[True] < nbytes[False]
