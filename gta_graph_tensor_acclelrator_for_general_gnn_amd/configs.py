@@ -7,8 +7,8 @@
                both MLP GEMMs in bf16 on MFMA (fp32 accumulation)
   gat8-reddit  GAT layer 1 on Reddit, 8 heads, F=602: not a BASELINE config; the full layer
                around the metric's aggregate (edge-softmax, GEMMs, aggregate, ELU)
-(config 0 -- V2/GAT_Cora.yaml through compile/interpret on the CPU -- is the golden-stream
-suite: tests/test_lowering.py, test_compiler.py.)
+(config 0 -- V2/GAT_Cora.yaml through the V2 lowering -- is legacy.py: create_list restated
+byte-exactly (tests/test_legacy_v2.py) and its stream executed on libgta (test_gpu_executor.py).)
 """
 import torch
 

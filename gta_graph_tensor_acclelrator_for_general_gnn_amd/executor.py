@@ -635,6 +635,7 @@ class Executor:
 def run_stream(opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, sync=True):
     ex = Executor(opgraph, stream, graph, tensors, semantics, plan_chunk)
     dev = graph.device
+    sync = sync and dev.type == "cuda"
     if sync:
         torch.cuda.synchronize(dev)
     t0 = time.perf_counter()

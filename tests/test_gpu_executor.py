@@ -132,3 +132,13 @@ def test_gat_softmax_fusion_on_gpu(golden_dir, manifest, cora, dev, reorder):
         fin = torch.isfinite(b)
         assert torch.equal(torch.isfinite(a), fin)
         assert (a[fin] - b[fin]).abs().max() <= 1e-4 * b[fin].abs().max() + 1e-6
+
+
+@pytest.mark.parametrize("k", [0, 1, 4, 5, 6])
+def test_legacy_v2_stream_on_gpu(golden_dir, dev, k):
+    """BASELINE config 0's stream (V2 create_list lowering) executed on libgta vs the fp64 oracle."""
+    import json
+    from .test_legacy_v2 import run_v2
+    case = json.load(open(os.path.join(golden_dir, "v2", "manifest.json")))[k]
+    res = run_v2(golden_dir, case, dev=dev)
+    assert res.launches > 0

@@ -1,0 +1,82 @@
+"""Legacy V2 path (BASELINE config 0): V2 op graph -> create_list stream -> execution.
+
+lower_v2 is pinned byte-for-byte to the reference's own create_list outputs
+(tests/golden/v2/, made by tests/golden/make_golden_v2.py; case 0 is the
+committed V2/fused.yaml), including its IndexError on an empty output list.
+The V2 stream is executed on the CPU stand-in kernels here and on libgta in
+test_gpu_executor.py, against the fp64 oracle (max|d|/max|ref| <= 1e-4).
+"""
+import json
+import os
+
+import pytest
+import torch
+import yaml
+
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import executor, frontend, graph as G, ir, legacy, workloads
+from oracle.exec_ref import execute_ref
+
+from . import fake_ops
+from .test_ir_executor_cpu import compare
+
+
+def _v2(golden_dir):
+    return json.load(open(os.path.join(golden_dir, "v2", "manifest.json")))
+
+
+def _ops(golden_dir, name):
+    f = "v2_GAT_Cora.yaml" if name == "GAT_Cora.yaml" else "v2_simpletest.yaml"
+    return yaml.safe_load(open(os.path.join(golden_dir, f)))
+
+
+@pytest.mark.parametrize("k", range(7))
+def test_lower_v2_byte_identical(golden_dir, k):
+    case = _v2(golden_dir)[k]
+    out = legacy.dump(legacy.lower_v2(case["dataset"], _ops(golden_dir, case["op_graph"]), case["op_list"],
+                                      case["tile_size"], case["node_num"]))
+    assert out == open(os.path.join(golden_dir, "v2", case["file"])).read()
+
+
+def test_case0_is_the_committed_fused_yaml(golden_dir):
+    a = open(os.path.join(golden_dir, "v2", "case0.yaml")).read()
+    assert a == open(os.path.join(golden_dir, "v2_fused.yaml")).read()
+
+
+def test_lower_v2_error_case(golden_dir):
+    err = [c for c in _v2(golden_dir) if "error_case" in c][0]
+    ops = _ops(golden_dir, "GAT_Cora.yaml")
+    ops[3]["OUTPUT"]["output_list"] = []
+    with pytest.raises(IndexError):
+        legacy.lower_v2("citeseer", ops, err["op_list"], [64] * 4, 3327)
+    assert err["raises"] == "IndexError"
+
+
+def test_comp_types_match_genGraphOP_gat(golden_dir):
+    ref = [r["COMP_TYPE"] for r in frontend.gen_ops("GAT", 1, 2708, 10556, 1433, False, 16)]
+    assert legacy.comp_types(_ops(golden_dir, "GAT_Cora.yaml")) == ref
+
+
+def run_v2(golden_dir, case, dev=None):
+    ops = _ops(golden_dir, case["op_graph"])
+    net = "GAT" if case["op_graph"] == "GAT_Cora.yaml" else "simpletest"
+    n = ops[0]["INPUT"]["feature_number"][0]
+    e = max(r["OUTPUT"]["output_number"] for r in ops if r["TYPE"] == "scatter")
+    gc = G.synthetic(n, e, seed=7)
+    recs = legacy.lower_v2(case["dataset"], ops, case["op_list"], case["tile_size"], case["node_num"])
+    sem = legacy.SEMANTICS[net]
+    og = ir.OpGraph(legacy.typed_records(ops), sem.inputs)
+    tensors = workloads.make_tensors(og, gc, net, seed=1)
+    gd = gc if dev is None else gc.to(dev)
+    td = tensors if dev is None else {k: v.to(dev) for k, v in tensors.items()}
+    res, ex = legacy.execute_v2(ops, recs, gd, td, net, op_list=case["op_list"])
+    ip, ix = gc.numpy()
+    ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
+    compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)), rtol=1e-4)
+    return res
+
+
+@pytest.mark.parametrize("k", [0, 1, 4, 5, 6])
+def test_execute_v2_stream_cpu(golden_dir, monkeypatch, k):
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    res = run_v2(golden_dir, _v2(golden_dir)[k])
+    assert res.launches > 0 and all(torch.isfinite(t).all() for t in res.outputs.values())
