@@ -677,6 +677,97 @@ k_agg_seg2d(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
   o.store(slabs + (static_cast<int64_t>(b) * n_rows + row) * (kWave * VW) + col);
 }
 
+// Quarter-wave form of k_agg_seg2d: a wave runs FOUR consecutive (block, row) items,
+// 16 lanes each (lane covers VW = F/16 floats as float4s), so one wave instruction
+// gathers four source rows and the per-item start-up (record, index and first
+// gather round trips, slab store) is shared by four items.  Within a 16-lane
+// group the chunk's 16 source indices arrive in one coalesced load and are
+// broadcast lane by lane with ds_swizzle (pattern fixed per unrolled step); lanes
+// of a finished item are masked off and issue no loads.
+__device__ __forceinline__ int bcast16(int v, int k) {  // lane (l & 0x30) | k, k in [0, 16)
+  switch (k) {
+#define GTA_B16(K_) case K_: return __builtin_amdgcn_ds_swizzle(v, 0x10 | ((K_) << 5));
+    GTA_B16(0) GTA_B16(1) GTA_B16(2) GTA_B16(3) GTA_B16(4) GTA_B16(5) GTA_B16(6) GTA_B16(7)
+    GTA_B16(8) GTA_B16(9) GTA_B16(10) GTA_B16(11) GTA_B16(12) GTA_B16(13) GTA_B16(14) GTA_B16(15)
+#undef GTA_B16
+  }
+  return v;
+}
+
+template <int VW, int U, bool WEIGHTED, int NT = 0>  // NT bit 0: non-temporal index/weight loads, bit 1: slab stores
+__global__ void __launch_bounds__(kBlock)
+k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items, const float* __restrict__ x,
+           int64_t ldx, const float* __restrict__ w, int64_t ldw, int lph, float* __restrict__ slabs,
+           const SegItem* __restrict__ items) {
+  constexpr int F = 16 * VW;
+  constexpr int NQ = VW / 4;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int l16 = lane & 15;
+  const int64_t k = (static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform()) * 4 + (lane >> 4);
+  SegItem it{0, 0, 0};
+  if (k < n_items) it = items[k];
+  const int len = it.len;
+  int mx = max(len, __shfl_xor(len, 16));
+  mx = max(mx, __shfl_xor(mx, 32));
+  const int maxlen = __builtin_amdgcn_readfirstlane(mx);
+  if (maxlen == 0) return;
+  const int64_t eb = it.beg;
+  const int col = l16 * VW;
+  const int head = WEIGHTED ? l16 / lph : 0;
+  float acc[VW];
+#pragma unroll
+  for (int q = 0; q < VW; ++q) acc[q] = 0.f;
+  auto ldi = [&](int64_t e) { return (NT & 1) ? __builtin_nontemporal_load(indices + e) : indices[e]; };
+  int idxv = (l16 < len) ? ldi(eb + l16) : 0;
+  for (int c = 0; c < maxlen; c += 16) {
+    const int idxn = (c + 16 + l16 < len) ? ldi(eb + c + 16 + l16) : 0;
+#pragma unroll
+    for (int s = 0; s < 16; s += U) {
+      if (c + s >= maxlen) break;
+      float4 xv[U][NQ];
+      float wu[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int src = bcast16(idxv, s + u);
+        const bool ok = c + s + u < len;
+        if (ok) {
+          const float4* p = reinterpret_cast<const float4*>(x + static_cast<int64_t>(src) * ldx + col);
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) xv[u][q] = p[q];
+          if (WEIGHTED) {
+            const float* wp = w + (eb + c + s + u) * ldw + head;
+            wu[u] = (NT & 1) ? __builtin_nontemporal_load(wp) : *wp;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < NQ; ++q) xv[u][q] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (WEIGHTED) wu[u] = 0.f;
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+          const float* xf = reinterpret_cast<const float*>(&xv[u][q]);
+#pragma unroll
+          for (int t = 0; t < 4; ++t)
+            acc[4 * q + t] = WEIGHTED ? fmaf(wu[u], xf[t], acc[4 * q + t]) : acc[4 * q + t] + xf[t];
+        }
+      }
+    }
+    idxv = idxn;
+  }
+  if (len > 0) {
+    const int b = static_cast<int>(k / n_rows);
+    float* o = slabs + (static_cast<int64_t>(b) * n_rows + it.row) * F + col;
+#pragma unroll
+    for (int q = 0; q < VW; ++q) {
+      if (NT & 2) __builtin_nontemporal_store(acc[q], o + q);
+      else o[q] = acc[q];
+    }
+  }
+}
+
 template <int VW>
 __global__ void __launch_bounds__(kBlock)
 k_seg_reduce(int64_t n_rows, const float* __restrict__ slabs, const float* __restrict__ row_scale,
@@ -1280,6 +1371,9 @@ int g_force_vw = 0;
 int g_agg_nt = 0;     // non-temporal index/weight loads in the SpMM form
 int g_agg_lean = 1;   // k_agg_lean for F = 64*VW SpMM shapes
 int64_t g_seg_waves = 0;  // persistent waves of the column-blocked kernel (0 = 8 per SIMD)
+int g_seg_quarter = 1;     // quarter-wave (4 items per wave) form of the blocked aggregate
+int g_seg_nt = 0;          // non-temporal bits of the quarter-wave form (F = 128, U = 8)
+int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
 int g_esm_lane = 1;        // edge-per-lane edge-softmax when H in {4,8,16} and rows are 16-B aligned
 int g_esm_keep = 4;        // chunks of 64 edges held in VGPRs by the edge-per-lane form (2 or 4)
 
@@ -1301,6 +1395,9 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "agg_nt") { g_agg_nt = static_cast<int>(value); return 0; }
   if (k == "agg_lean") { g_agg_lean = static_cast<int>(value); return 0; }
   if (k == "seg_waves") { g_seg_waves = value; return 0; }
+  if (k == "seg_nt") { g_seg_nt = static_cast<int>(value); return 0; }
+  if (k == "seg_u") { g_seg_u = static_cast<int>(value); return 0; }
+  if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
   if (k == "esm_lane") { g_esm_lane = static_cast<int>(value); return 0; }
   if (k == "esm_keep") { g_esm_keep = static_cast<int>(value); return 0; }
   return fail(GTA_ERR_ARG, "gta_debug_set: unknown key " + k);
@@ -1491,6 +1588,33 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     float* slabs = static_cast<float*>(workspace);
     const int64_t items = n_rows * B;
     const dim3 g2(static_cast<unsigned>((items + kWavesPerBlock - 1) / kWavesPerBlock)), blk2(kBlock);
+    const int vq = static_cast<int>(F / 16);
+    const int lph = w ? static_cast<int>((F / heads) / vq) : 0;
+    const bool quarter = g_seg_quarter && (vq == 4 || vq == 8 || vq == 16) && ldx % 4 == 0 && aligned(x, 16) &&
+                         (!w || ((F / heads) % vq == 0 && lph >= 1 && 16 % lph == 0));
+    if (quarter) {
+      const dim3 g4(static_cast<unsigned>((items + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock)));
+#define GTA_SEG4(VW_, U_)                                                                                   \
+  if (w) k_agg_seg4<VW_, U_, true><<<g4, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, lph, slabs, \
+                                                       static_cast<const SegItem*>(v.items));               \
+  else k_agg_seg4<VW_, U_, false><<<g4, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, lph, slabs,  \
+                                                      static_cast<const SegItem*>(v.items))
+#define GTA_SEG4NT(VW_, U_, NT_)                                                                             \
+  if (w) k_agg_seg4<VW_, U_, true, NT_><<<g4, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, lph, slabs, \
+                                                            static_cast<const SegItem*>(v.items));               \
+  else k_agg_seg4<VW_, U_, false, NT_><<<g4, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, lph, slabs,  \
+                                                           static_cast<const SegItem*>(v.items))
+      if (vq == 4) { GTA_SEG4(4, 4); }
+      else if (vq == 8) {
+        if (g_seg_u == 2) { GTA_SEG4(8, 2); } else if (g_seg_u == 4) { GTA_SEG4(8, 4); }
+        else if (g_seg_nt == 1) { GTA_SEG4NT(8, 8, 1); } else if (g_seg_nt == 2) { GTA_SEG4NT(8, 8, 2); }
+        else if (g_seg_nt == 3) { GTA_SEG4NT(8, 8, 3); } else { GTA_SEG4(8, 8); }
+      }
+      else { GTA_SEG4(16, 2); }
+#undef GTA_SEG4
+#undef GTA_SEG4NT
+      GTA_LAUNCHED("k_agg_seg4");
+    } else {
 #define GTA_SEG2D(VW_, GL_) \
   k_agg_seg2d<VW_, GL_><<<g2, blk2, 0, s>>>(indptr, indices, n_rows, x, ldx, w, ldw, slabs, sv, \
                                             static_cast<const SegItem*>(v.items))
@@ -1503,6 +1627,7 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     }
 #undef GTA_SEG2D
     GTA_LAUNCHED("k_agg_seg2d");
+    }
     const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
     if (vw == 2) k_seg_reduce<2><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, sv);
     else if (vw == 4) k_seg_reduce<4><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, sv);

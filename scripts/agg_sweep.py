@@ -40,14 +40,19 @@ def main():
         if parts[0].startswith("blk"):  # column-blocked path, B = blk<B>[:w<persistent waves>]
             wv = int(parts[1][1:]) if len(parts) > 1 and parts[1].startswith("w") else 0
             single = 0 if "multi" in parts[1:] else 1
-            variants.append((v, -int(parts[0][3:]), None, wv, single))
+            quarter = 0 if "q0" in parts[1:] else 1  # q0: one item per wave (k_agg_seg2d)
+            us = [int(p_[1:]) for p_ in parts[1:] if p_.startswith("u")]
+            quarter = quarter * (us[0] if us else 8)  # u<U>: edges per step of the quarter-wave form
+            nts = [int(p_[2:]) for p_ in parts[1:] if p_.startswith("nt")]
+            wv = wv + 1000 * (nts[0] if nts else 0)  # nt<bits>: non-temporal loads (1) / slab stores (2)
+            variants.append((v, -int(parts[0][3:]), quarter, wv, single))
             continue
         lpe = int(parts[0].replace("lpe", ""))
         chunk = None if parts[1] == "none" else int(parts[1].replace("c", ""))
         nt = int("nt" in parts[2:])
         lean = 0 if "lean0" in parts[2:] else 1
         variants.append((v, lpe, chunk, nt, lean))
-    plans = {v[2]: (g.plan(v[2]) if v[2] else None) for v in variants}
+    plans = {v[2]: (g.plan(v[2]) if v[2] else None) for v in variants if v[1] > 0}
     for v in variants:
         if v[1] < 0:
             g.blocked_plan(-v[1])
@@ -56,7 +61,10 @@ def main():
     for r in range(args.rounds):
         for name, lpe, chunk, nt, lean in variants:
             if lpe < 0:
-                ops.set_debug("seg_waves", nt)
+                ops.set_debug("seg_waves", nt % 1000)
+                ops.set_debug("seg_nt", nt // 1000)
+                ops.set_debug("seg_quarter", 1 if chunk else 0)
+                ops.set_debug("seg_u", chunk or 8)
 
                 def run(lpe=lpe, lean=lean):
                     ops.aggregate_blocked(g, x, alpha, out=y, blocks=-lpe, single_launch=bool(lean))

@@ -317,3 +317,29 @@ def test_edge_softmax_other_sf_and_errors(dev):
         ops.edge_softmax(g, a[:, :6].contiguous(), b[:, :6].contiguous())
     with pytest.raises(ValueError):
         ops.edge_softmax(g, a, b[:, :4].contiguous())
+
+
+@pytest.mark.parametrize("knobs", [{"seg_quarter": 0}, {"seg_u": 2}, {"seg_u": 4}, {"seg_nt": 3}])
+@pytest.mark.parametrize("F,heads", [(128, 8), (128, 0), (64, 4), (256, 16), (128, 1)])
+def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
+    """Every form of the blocked kernel (one item per wave, quarter-wave with 2/4/8 edges per
+    step, non-temporal bits) == the fp64 oracle and == the default form bitwise."""
+    n, e = 900, 30000
+    g = G.synthetic(n, e, seed=F + heads, device=dev)
+    ip, ix = g.numpy()
+    rng = np.random.default_rng(F)
+    x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
+    w = torch.from_numpy(rng.random((g.nnz, heads)).astype(np.float32)).to(dev) if heads else None
+    y0 = ops.aggregate_blocked(g, x, w, blocks=8)
+    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 0}
+    try:
+        for k, v in knobs.items():
+            ops.set_debug(k, v)
+        y = ops.aggregate_blocked(g, x, w, blocks=8)
+    finally:
+        for k in knobs:
+            ops.set_debug(k, defaults[k])
+    xn, wn = x.cpu().numpy(), None if w is None else w.cpu().numpy()
+    _check(y, isa_ref.aggregate(ip, ix, xn, "src", wn), isa_ref.aggregate_abs(ip, ix, xn, "src", wn), f"{knobs}")
+    if "seg_quarter" not in knobs:
+        assert torch.equal(y, y0)  # same per-item edge order in every quarter-wave form
