@@ -169,15 +169,19 @@ class BlockedPlan:
 
     @staticmethod
     def supports(F, heads, x=None):
-        vw = F // 64 if F in (64, 128, 256) else 0
-        if not vw:
+        """Shapes libgta's blocked kernels take: F in {64, 128, 256} and, with head weights,
+        the quarter-wave form's lanes per head (F/heads)/(F/16) in {1, 2, 4, 8, 16} or the
+        one-item-per-wave form's (F/heads)/(F/64) in {4, 8, 16}."""
+        if F not in (64, 128, 256):
             return False
-        if heads:
-            if F % heads or (F // heads) % vw:
-                return False
-            if (F // heads) // vw not in (4, 8, 16):
-                return False
-        return True
+        if not heads:
+            return True
+        if F % heads:
+            return False
+        fh, vq, vw = F // heads, F // 16, F // 64
+        quarter = fh % vq == 0 and (fh // vq) in (1, 2, 4, 8, 16)
+        single = fh % vw == 0 and (fh // vw) in (4, 8, 16)
+        return quarter or single
 
 
 def aggregate_blocked(graph, x, w=None, row_scale=None, out=None, accumulate=False, plan=None, blocks=32,

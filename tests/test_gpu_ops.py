@@ -335,7 +335,12 @@ def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     try:
         for k, v in knobs.items():
             ops.set_debug(k, v)
-        y = ops.aggregate_blocked(g, x, w, blocks=8)
+        try:
+            y = ops.aggregate_blocked(g, x, w, blocks=8)
+        except ops._lib.GTAError:
+            if "seg_quarter" in knobs and heads and ((F // heads) // (F // 64)) not in (4, 8, 16):
+                pytest.skip("the one-item-per-wave form needs (F/heads)/(F/64) in {4, 8, 16}")
+            raise
     finally:
         for k in knobs:
             ops.set_debug(k, defaults[k])
