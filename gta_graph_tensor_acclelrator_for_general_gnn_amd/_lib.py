@@ -44,6 +44,7 @@ SIGNATURES = {
     "gta_edge_softmax": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp]),
     "gta_apply_node": (_i32, [_i32, _i32, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp]),
     "gta_update_mm": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
+    "gta_update_mm_t": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
     "gta_tile_nnz": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "gta_debug_set": (_i32, [_cp, _i64]),
 }

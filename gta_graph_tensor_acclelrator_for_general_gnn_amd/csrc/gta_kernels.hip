@@ -1297,6 +1297,167 @@ k_mm_bf16(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
       }
 }
 
+// Row-streaming UPDATE for the skinny shapes of GNN layers (M = nodes or edges,
+// K and N at most a few hundred).  A block owns BN = 16*NT output columns (all of
+// N up to 128, so X is read from HBM once) and walks 128-row groups g, g+grid, ...
+// Each wave holds 32 rows x BN in MFMA accumulators; its A fragments come
+// straight from global memory in the MFMA register layout (no LDS round trip).
+// W arrives TRANSPOSED (wt[n][k]) and is staged per K chunk into LDS with 16-B
+// copies -- once per block when K fits one chunk -- so a B fragment is one 16-B
+// LDS read.
+//   fp32:  v_mfma_f32_16x16x4_f32, lane (r, g) loads x[r][k0+4g .. +3]; sub-step j
+//          contracts k = k0+4g+j (B read with the same k map).
+//   bf16:  v_mfma_f32_16x16x32_bf16, lane (r, g) holds x[r][k0+8g .. +7] (fp32 X is
+//          rounded to bf16 in registers, round to nearest even).
+template <typename TA, typename WT, int NT>
+__global__ void __launch_bounds__(kBlock)
+k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
+          const WT* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo) {
+  constexpr bool BF = sizeof(WT) == 2;
+  constexpr int KS = BF ? 32 : 16;         // k covered by one A-fragment load
+  constexpr int KC = BF ? (NT >= 8 ? 128 : 256) : (NT >= 8 ? 64 : 128);  // K chunk staged in LDS (<= 35 KB)
+  constexpr int KP = KC + (BF ? 8 : 4);    // padded LDS row (16-B aligned)
+  constexpr int BN = 16 * NT;
+  constexpr int WV = 16 / sizeof(WT);      // W elements per 16-B copy
+  __shared__ __attribute__((aligned(16))) WT Bt[BN][KP];
+  const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int n0 = blockIdx.y * BN;
+  constexpr int AV = BF ? 8 : 4;  // A values per lane per fragment
+  const bool avec = (ldx % AV == 0) && aligned(x, sizeof(TA) * AV);
+  const bool wvec = (ldwt % WV == 0) && aligned(wt, 16);
+  const int64_t n_groups = (M + 127) / 128;
+  const bool one_chunk = K <= KC;
+
+  auto stage = [&](int kc) {
+    if (wvec) {
+      for (int e = t; e < BN * (KC / WV); e += kBlock) {
+        const int n = e / (KC / WV), kv = (e - n * (KC / WV)) * WV;
+        const int nn = n0 + n, k = kc + kv;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (nn < N && k + WV <= K) {
+          v = *reinterpret_cast<const uint4*>(wt + static_cast<int64_t>(nn) * ldwt + k);
+        } else if (nn < N && k < K) {
+          WT tmp[WV];
+#pragma unroll
+          for (int q = 0; q < WV; ++q) tmp[q] = (k + q < K) ? wt[static_cast<int64_t>(nn) * ldwt + k + q] : WT(0);
+          v = *reinterpret_cast<const uint4*>(tmp);
+        }
+        *reinterpret_cast<uint4*>(&Bt[n][kv]) = v;
+      }
+    } else {
+      for (int e = t; e < BN * KC; e += kBlock) {
+        const int n = e / KC, kk = e - n * KC;
+        const int nn = n0 + n, k = kc + kk;
+        Bt[n][kk] = (nn < N && k < K) ? wt[static_cast<int64_t>(nn) * ldwt + k] : WT(0);
+      }
+    }
+  };
+  if (one_chunk) {
+    stage(0);
+    __syncthreads();
+  }
+  for (int64_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
+    const int64_t mw = grp * 128 + wv * 32;
+    const TA* ap[2];
+    bool aok[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int64_t m = mw + 16 * i + r16;
+      aok[i] = m < M;
+      const int64_t src = aok[i] ? (row_idx ? static_cast<int64_t>(row_idx[m]) : m) : 0;
+      ap[i] = x + src * ldx;
+    }
+    f32x4 acc[2][NT];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int c = 0; c < NT; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    for (int kc = 0; kc < K; kc += KC) {
+      if (!one_chunk) {
+        stage(kc);
+        __syncthreads();
+      }
+      const int kend = (K - kc < KC) ? K - kc : KC;
+      auto load_a = [&](int ks, float (&av)[2][AV]) {
+        const int k0 = kc + ks + AV * g;  // first k of this lane's fragment
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          if (avec && aok[i] && k0 + AV <= K) {
+            if constexpr (sizeof(TA) == 4) {
+#pragma unroll
+              for (int q = 0; q < AV / 4; ++q) {
+                const float4 v4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(ap[i]) + k0 + 4 * q);
+                av[i][4 * q] = v4.x; av[i][4 * q + 1] = v4.y; av[i][4 * q + 2] = v4.z; av[i][4 * q + 3] = v4.w;
+              }
+            } else {
+              const uint4 u = *reinterpret_cast<const uint4*>(ap[i] + k0);
+              const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
+#pragma unroll
+              for (int q = 0; q < 4; ++q) {
+                av[i][2 * q] = __uint_as_float(uw[q] << 16);
+                av[i][2 * q + 1] = __uint_as_float(uw[q] & 0xffff0000u);
+              }
+            }
+          } else {
+#pragma unroll
+            for (int q = 0; q < AV; ++q) {
+              float v = 0.f;
+              if (aok[i] && k0 + q < K) {
+                if constexpr (sizeof(TA) == 4) v = reinterpret_cast<const float*>(ap[i])[k0 + q];
+                else v = __uint_as_float(static_cast<uint32_t>(reinterpret_cast<const uint16_t*>(ap[i])[k0 + q]) << 16);
+              }
+              av[i][q] = v;
+            }
+          }
+        }
+      };
+#pragma unroll 1
+      for (int ks = 0; ks < kend; ks += KS) {
+        float av[2][AV];
+        load_a(ks, av);
+        if constexpr (BF) {
+          bf16x8 a8[2];
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) a8[i][q] = static_cast<short>(to_bf16_bits(av[i][q]));
+#pragma unroll
+          for (int c = 0; c < NT; ++c) {
+            const bf16x8 b8 = *reinterpret_cast<const bf16x8*>(&Bt[16 * c + r16][ks + 8 * g]);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+              acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8[i], b8, acc[i][c], 0, 0, 0);
+          }
+        } else {
+#pragma unroll
+          for (int c = 0; c < NT; ++c) {
+            const float4 b4 = *reinterpret_cast<const float4*>(&Bt[16 * c + r16][ks + 4 * g]);
+            const float bj[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+#pragma unroll
+              for (int i = 0; i < 2; ++i)
+                acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][j], bj[j], acc[i][c], 0, 0, 0);
+          }
+        }
+      }
+      if (!one_chunk) __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int c = 0; c < NT; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t m = mw + 16 * i + 4 * g + r;
+          const int n = n0 + 16 * c + r16;
+          if (m < M && n < N) out[m * ldo + n] = sf_apply(sf, acc[i][c][r]);
+        }
+  }
+}
+
 // ---------------------------------------------------------------------------
 // f2: tile-nnz histogram (integer atomics: result is order independent)
 // ---------------------------------------------------------------------------
@@ -1374,6 +1535,7 @@ int64_t g_seg_waves = 0;  // persistent waves of the column-blocked kernel (0 = 
 int g_seg_quarter = 1;     // quarter-wave (4 items per wave) form of the blocked aggregate
 int g_seg_nt = 0;          // non-temporal bits of the quarter-wave form (F = 128, U = 8)
 int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
+int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
 int g_esm_lane = 1;        // edge-per-lane edge-softmax when H in {4,8,16} and rows are 16-B aligned
 int g_esm_keep = 4;        // chunks of 64 edges held in VGPRs by the edge-per-lane form (2 or 4)
 
@@ -1398,6 +1560,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "seg_nt") { g_seg_nt = static_cast<int>(value); return 0; }
   if (k == "seg_u") { g_seg_u = static_cast<int>(value); return 0; }
   if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
+  if (k == "mm_blocks_per_cu") { g_mm_blocks_per_cu = value; return 0; }
   if (k == "esm_lane") { g_esm_lane = static_cast<int>(value); return 0; }
   if (k == "esm_keep") { g_esm_keep = static_cast<int>(value); return 0; }
   return fail(GTA_ERR_ARG, "gta_debug_set: unknown key " + k);
@@ -1574,12 +1737,13 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     }
   }
   if (!vw) return fail(GTA_ERR_UNSUPPORTED, "aggregate_blocked: F must be 64, 128 or 256 (one edge per wave row)");
+  bool gl_ok = true;  // head layout of the one-item-per-wave forms
   if (w) {
     if (heads <= 0 || F % heads) return fail(GTA_ERR_ARG, "aggregate_blocked: heads must divide F");
     gl = static_cast<int>(F / heads) / vw;
-    if ((F / heads) % vw || (gl != 4 && gl != 8 && gl != 16))
-      return fail(GTA_ERR_UNSUPPORTED, "aggregate_blocked: (F/heads)/VW must be 4, 8 or 16");
+    gl_ok = (F / heads) % vw == 0 && (gl == 4 || gl == 8 || gl == 16);
   }
+  const char* gl_msg = "aggregate_blocked: (F/heads)/VW must be 4, 8 or 16 (or quarter-wave lanes per head 1..16)";
   const int B = static_cast<int>(blocks);
   BlockedView v = blocked_view(const_cast<void*>(plan), n_rows, B);
   hipStream_t s = S(stream);
@@ -1615,6 +1779,7 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
 #undef GTA_SEG4NT
       GTA_LAUNCHED("k_agg_seg4");
     } else {
+      if (!gl_ok) return fail(GTA_ERR_UNSUPPORTED, gl_msg);
 #define GTA_SEG2D(VW_, GL_) \
   k_agg_seg2d<VW_, GL_><<<g2, blk2, 0, s>>>(indptr, indices, n_rows, x, ldx, w, ldw, slabs, sv, \
                                             static_cast<const SegItem*>(v.items))
@@ -1635,6 +1800,7 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     GTA_LAUNCHED("k_seg_reduce");
     return GTA_OK;
   }
+  if (!gl_ok) return fail(GTA_ERR_UNSUPPORTED, gl_msg);
   // persistent waves: enough for 8 per SIMD on every CU, never more than one per row
   const int64_t waves = std::min<int64_t>(n_rows, g_seg_waves > 0 ? g_seg_waves : 256 * 32);
   const dim3 grid(static_cast<unsigned>((waves + kWavesPerBlock - 1) / kWavesPerBlock)), blk(kBlock);
@@ -1777,6 +1943,7 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
   if (!x || !w || !out || M < 0 || K <= 0 || N <= 0) return fail(GTA_ERR_ARG, "update_mm: bad arguments");
   if (K > INT32_MAX || N > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "update_mm: K/N too large");
   if (M == 0) return GTA_OK;
+  if (dtype != GTA_F32 && dtype != GTA_BF16 && dtype != GTA_F32_BF16) return fail(GTA_ERR_ARG, "update_mm: bad dtype");
   const dim3 grid(static_cast<unsigned>((M + 63) / 64), static_cast<unsigned>((N + 63) / 64));
   if (dtype == GTA_F32) {
     k_mm_f32<<<grid, dim3(kBlock), 0, S(stream)>>>(static_cast<const float*>(x), ldx, row_idx, M,
@@ -1794,6 +1961,34 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
     return fail(GTA_ERR_ARG, "update_mm: bad dtype");
   }
   GTA_LAUNCHED("k_mm");
+  return GTA_OK;
+}
+
+int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
+                    int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream) {
+  if (!x || !wt || !out || M < 0 || K <= 0 || N <= 0 || ldwt < K) return fail(GTA_ERR_ARG, "update_mm_t: bad arguments");
+  if (K > INT32_MAX || N > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t: K/N too large");
+  if (dtype != GTA_F32 && dtype != GTA_BF16 && dtype != GTA_F32_BF16) return fail(GTA_ERR_ARG, "update_mm_t: bad dtype");
+  if (M == 0) return GTA_OK;
+  const int nt = N <= 16 ? 1 : N <= 32 ? 2 : N <= 64 ? 4 : 8;
+  const int64_t groups = (M + 127) / 128;
+  const int64_t per_cu = g_mm_blocks_per_cu > 0 ? g_mm_blocks_per_cu : 8;
+  const int kc = (dtype == GTA_F32) ? (nt >= 8 ? 64 : 128) : (nt >= 8 ? 128 : 256);  // k_mm_rows KC
+  const int64_t cap = (K <= kc) ? 256 * per_cu : groups;  // W staged once: persistent row-group loop
+  const dim3 gr(static_cast<unsigned>(std::min<int64_t>(groups, cap)),
+                static_cast<unsigned>((N + 16 * nt - 1) / (16 * nt)));
+#define GTA_MMR(TA_, WT_, NT_)                                                                                \
+  k_mm_rows<TA_, WT_, NT_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const TA_*>(x), ldx, row_idx, M,  \
+                                                               static_cast<int>(K), static_cast<const WT_*>(wt), \
+                                                               ldwt, static_cast<int>(N), sf, out, ldo)
+#define GTA_MMR_NT(TA_, WT_) \
+  if (nt == 1) GTA_MMR(TA_, WT_, 1); else if (nt == 2) GTA_MMR(TA_, WT_, 2); else if (nt == 4) GTA_MMR(TA_, WT_, 4); else GTA_MMR(TA_, WT_, 8)
+  if (dtype == GTA_F32) { GTA_MMR_NT(float, float); }
+  else if (dtype == GTA_BF16) { GTA_MMR_NT(uint16_t, uint16_t); }
+  else { GTA_MMR_NT(float, uint16_t); }
+#undef GTA_MMR_NT
+#undef GTA_MMR
+  GTA_LAUNCHED("k_mm_rows");
   return GTA_OK;
 }
 

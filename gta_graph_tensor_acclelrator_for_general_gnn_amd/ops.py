@@ -11,6 +11,8 @@ One function per ISA op / fused pattern of the GTA stream:
   tile_nnz     calculate_sparsity (code/preprocessing.py:12-40)            -> gta_tile_nnz
 Shapes and strides are validated on the host before any launch.
 """
+import weakref
+
 import torch
 
 from . import _lib
@@ -38,7 +40,11 @@ def _need_gpu(*ts):
 def _rows(t, name, dtype=torch.float32):
     if t.dtype != dtype:
         raise TypeError(f"{name}: expected {dtype}, got {t.dtype}")
-    if t.dim() != 2 or t.stride(1) != 1 or t.stride(0) < t.shape[1]:
+    if t.dim() != 2:
+        raise ValueError(f"{name}: need a row-major 2-D tensor with unit column stride")
+    if t.shape[0] <= 1:  # a single row: its row stride is meaningless (torch may report 1)
+        return max(t.shape[1], 1)
+    if t.stride(1) != 1 and t.shape[1] > 1 or t.stride(0) < t.shape[1]:
         raise ValueError(f"{name}: need a row-major 2-D tensor with unit column stride")
     return t.stride(0)
 
@@ -354,9 +360,32 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
         out = torch.empty(M, N, dtype=torch.float32, device=x.device)
     ldo = _rows(out, "out")
     dt = _lib.GTA_F32_BF16 if mixed else (_lib.GTA_F32 if x.dtype == torch.float32 else _lib.GTA_BF16)
-    check(_L().gta_update_mm(_ptr(x), ldx, _ptr(row_idx), M, K, _ptr(w), ldw, N, dt, _sf(sf), _ptr(out), ldo,
-                             _stream(x.device)), "update_mm")
+    if MM_FORM == "rows":  # row-streaming kernel on W^T (cached per weight version)
+        wt = _transposed(w)
+        check(_L().gta_update_mm_t(_ptr(x), ldx, _ptr(row_idx), M, K, _ptr(wt), _rows(wt, "w^T", wt.dtype), N, dt, _sf(sf),
+                                   _ptr(out), ldo, _stream(x.device)), "update_mm_t")
+    else:
+        check(_L().gta_update_mm(_ptr(x), ldx, _ptr(row_idx), M, K, _ptr(w), ldw, N, dt, _sf(sf), _ptr(out), ldo,
+                                 _stream(x.device)), "update_mm")
     return out
+
+
+MM_FORM = "rows"  # "rows": gta_update_mm_t (x read once per output); "tile": gta_update_mm 64x64 tiles
+_WT_CACHE = {}
+
+
+def _transposed(w):
+    """W^T [N, K] contiguous, cached per weight tensor object and version (weights are reused on
+    every layer call).  The entry holds a weak reference: a freed weight's address can be reused
+    by another tensor, so the address alone is never the key."""
+    ent = _WT_CACHE.get(id(w))
+    if ent is not None and ent[0]() is w and ent[1] == w._version:
+        return ent[2]
+    if len(_WT_CACHE) >= 64:
+        _WT_CACHE.clear()
+    wt = w.t().contiguous()
+    _WT_CACHE[id(w)] = (weakref.ref(w), w._version, wt)
+    return wt
 
 
 def tile_nnz(graph, T):

@@ -181,6 +181,14 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
                   const void* w, int64_t ldw, int64_t N, int dtype, int sf,
                   float* out, int64_t ldo, void* stream);
 
+/* Same UPDATE with W given TRANSPOSED: wt [N, K] row-major (leading dimension
+ * ldwt >= K), dtype as above.  Runs the row-streaming kernel: a block owns all N
+ * columns (up to 128 per block) and walks 128-row groups, so x is read once; wt
+ * is staged into LDS with 16-B copies.  The contraction order differs from
+ * gta_update_mm (fp32 rounding only). */
+int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
+                    int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream);
+
 /* ---- f2 TILE-NNZ metadata ----------------------------------------------
  * counts[t, j] = #{ e : dst(e) in [t*T, (t+1)*T), src(e) == j, dst(e) != j }
  * for t < ceil(n_rows/T), j < n_cols (int32 [ceil(n_rows/T), n_cols]).

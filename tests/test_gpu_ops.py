@@ -348,3 +348,43 @@ def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     _check(y, isa_ref.aggregate(ip, ix, xn, "src", wn), isa_ref.aggregate_abs(ip, ix, xn, "src", wn), f"{knobs}")
     if "seg_quarter" not in knobs:
         assert torch.equal(y, y0)  # same per-item edge order in every quarter-wave form
+
+
+@pytest.mark.parametrize("form", ["rows", "tile"])
+@pytest.mark.parametrize("M,K,N,dt", [(5000, 602, 128, "f32"), (3001, 100, 300, "f32"), (1000, 129, 8, "f32"),
+                                      (4099, 100, 128, "mixed"), (2000, 256, 200, "bf16"), (700, 77, 33, "bf16"),
+                                      (130, 5, 1, "f32")])
+def test_update_mm_both_forms(dev, form, M, K, N, dt):
+    """Row-streaming (W^T, x read once) and 64x64-tile UPDATE kernels vs fp64 of the same (bf16-rounded)
+    operands, incl. N > 128 (several column blocks), K tails and an x view with odd leading dimension."""
+    rng = np.random.default_rng(M + K + N)
+    xs = torch.from_numpy(rng.standard_normal((M, K + 3)).astype(np.float32))[:, 1:K + 1]  # ldx = K+3, offset 1
+    w = torch.from_numpy((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32))
+    if dt == "bf16":
+        xs, w = xs.to(torch.bfloat16), w.to(torch.bfloat16)
+    elif dt == "mixed":
+        w = w.to(torch.bfloat16)
+    old = ops.MM_FORM
+    ops.MM_FORM = form
+    try:
+        out = ops.update_mm(xs.to(dev), w.to(dev))
+    finally:
+        ops.MM_FORM = old
+    xr = xs.float().numpy().astype(np.float64)
+    if dt != "f32":
+        xr = torch.from_numpy(xr).to(torch.bfloat16).double().numpy()
+    wf = w.float().numpy().astype(np.float64)
+    _check(out, xr @ wf, np.abs(xr) @ np.abs(wf), f"update_mm {form} {dt}")
+
+
+def test_update_mm_weight_cache_never_stale(dev):
+    """A new weight at a freed weight's address (same shape/dtype) must not reuse the old W^T."""
+    x = torch.randn(300, 64, device=dev)
+    for seed in range(6):
+        w = torch.randn(64, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(seed))
+        got = ops.update_mm(x, w)
+        ref = (x.double() @ w.double()).float()
+        assert torch.allclose(got, ref, rtol=1e-4, atol=1e-4), seed
+        w.mul_(2.0)  # in-place update bumps the version: the cache must notice
+        assert torch.allclose(ops.update_mm(x, w), 2 * ref, rtol=1e-4, atol=1e-4), seed
+        del w
