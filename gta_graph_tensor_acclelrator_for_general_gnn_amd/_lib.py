@@ -38,6 +38,9 @@ SIGNATURES = {
     "gta_aggregate_blocked_workspace_bytes": (_i64, [_i64, _i64, _i64]),
     "gta_aggregate_blocked": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _i32,
                                      _vp, _i64, _vp, _vp]),
+    "gta_gat_aggregate_blocked_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
+    "gta_gat_aggregate_blocked": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32,
+                                         _vp, _i64, _vp, _vp, _i64, _vp, _vp]),
     "gta_gather_add": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i32, _vp]),
     "gta_apply_edge": (_i32, [_i32, _i32, _vp, _vp, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp,
                               _i64, _vp]),

@@ -694,11 +694,26 @@ __device__ __forceinline__ int bcast16(int v, int k) {  // lane (l & 0x30) | k, 
   return v;
 }
 
-template <int VW, int U, bool WEIGHTED, int NT = 0>  // NT bit 0: non-temporal index/weight loads, bit 1: slab stores
+// ATT (fused GAT attention, GAT ops 6-12 minus the final SF): the edge weight is
+// not read but computed, v = sf(a[row, h] + b[src, h]) from the two score tables
+// (b gathered like x, from the same column block), and the item's per-head sum of
+// v goes to a second slab; k_seg_reduce_att divides.  No [E, H] tensor is
+// written or read.
+struct AttArgs {
+  const float* a;  // [n_rows, H] destination-side scores (lda)
+  int64_t lda;
+  const float* b;  // [n_cols, H] source-side scores (ldb)
+  int64_t ldb;
+  int sf;
+  int H;
+  float* sslabs;   // [B, n_rows, H] per-item partial sums of v
+};
+
+template <int VW, int U, bool WEIGHTED, int NT = 0, bool ATT = false>  // NT bit 0: non-temporal index/weight loads, bit 1: slab stores
 __global__ void __launch_bounds__(kBlock)
 k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items, const float* __restrict__ x,
            int64_t ldx, const float* __restrict__ w, int64_t ldw, int lph, float* __restrict__ slabs,
-           const SegItem* __restrict__ items) {
+           const SegItem* __restrict__ items, AttArgs att = AttArgs{}) {
   constexpr int F = 16 * VW;
   constexpr int NQ = VW / 4;
   const int lane = threadIdx.x & (kWave - 1);
@@ -713,10 +728,12 @@ k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items,
   if (maxlen == 0) return;
   const int64_t eb = it.beg;
   const int col = l16 * VW;
-  const int head = WEIGHTED ? l16 / lph : 0;
+  const int head = (WEIGHTED || ATT) ? l16 / lph : 0;
   float acc[VW];
 #pragma unroll
   for (int q = 0; q < VW; ++q) acc[q] = 0.f;
+  float arow = 0.f, ssum = 0.f;
+  if (ATT && len > 0) arow = att.a[static_cast<int64_t>(it.row) * att.lda + head];
   auto ldi = [&](int64_t e) { return (NT & 1) ? __builtin_nontemporal_load(indices + e) : indices[e]; };
   int idxv = (l16 < len) ? ldi(eb + l16) : 0;
   for (int c = 0; c < maxlen; c += 16) {
@@ -734,14 +751,17 @@ k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items,
           const float4* p = reinterpret_cast<const float4*>(x + static_cast<int64_t>(src) * ldx + col);
 #pragma unroll
           for (int q = 0; q < NQ; ++q) xv[u][q] = p[q];
-          if (WEIGHTED) {
+          if (ATT) {
+            wu[u] = sf_apply(att.sf, arow + att.b[static_cast<int64_t>(src) * att.ldb + head]);
+            ssum += wu[u];
+          } else if (WEIGHTED) {
             const float* wp = w + (eb + c + s + u) * ldw + head;
             wu[u] = (NT & 1) ? __builtin_nontemporal_load(wp) : *wp;
           }
         } else {
 #pragma unroll
           for (int q = 0; q < NQ; ++q) xv[u][q] = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (WEIGHTED) wu[u] = 0.f;
+          if (WEIGHTED || ATT) wu[u] = 0.f;
         }
       }
 #pragma unroll
@@ -751,7 +771,7 @@ k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items,
           const float* xf = reinterpret_cast<const float*>(&xv[u][q]);
 #pragma unroll
           for (int t = 0; t < 4; ++t)
-            acc[4 * q + t] = WEIGHTED ? fmaf(wu[u], xf[t], acc[4 * q + t]) : acc[4 * q + t] + xf[t];
+            acc[4 * q + t] = (WEIGHTED || ATT) ? fmaf(wu[u], xf[t], acc[4 * q + t]) : acc[4 * q + t] + xf[t];
         }
       }
     }
@@ -765,6 +785,7 @@ k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items,
       if (NT & 2) __builtin_nontemporal_store(acc[q], o + q);
       else o[q] = acc[q];
     }
+    if (ATT && l16 % lph == 0) att.sslabs[(static_cast<int64_t>(b) * n_rows + it.row) * att.H + head] = ssum;
   }
 }
 
@@ -800,6 +821,43 @@ k_seg_reduce(int64_t n_rows, const float* __restrict__ slabs, const float* __res
     for (int q = 0; q < VW; ++q) o.v[q] = scale * acc[q];
   }
   o.store(yp);
+}
+
+// Ordered reduce of the attention form: y[row, c] = sum_b acc_b / sum_b s_b[head(c)]
+// (normalize; rows without edges get 0), or the numerator alone; sums[row, h] =
+// sum_b s_b[h] when requested.  Same block order as k_seg_reduce.
+template <int VW>
+__global__ void __launch_bounds__(kBlock)
+k_seg_reduce_att(int64_t n_rows, const float* __restrict__ slabs, const float* __restrict__ sslabs, int H,
+                 int normalize, float* __restrict__ y, int64_t ldy, float* __restrict__ sums, SegView sv) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  const int32_t* sg = sv.seg + row * (sv.B + 1);
+  const int col = lane * VW;
+  constexpr int F = kWave * VW;
+  const int head = col / (F / H);
+  float acc[VW];
+#pragma unroll
+  for (int q = 0; q < VW; ++q) acc[q] = 0.f;
+  float sh = 0.f, sl = 0.f;  // this lane's head sum; lane < H: head `lane`'s sum (for `sums`)
+  bool any = false;
+  for (int b = 0; b < sv.B; ++b) {
+    if (sg[b] == sg[b + 1]) continue;
+    any = true;
+    Vec<VW> p;
+    p.load(slabs + (static_cast<int64_t>(b) * n_rows + row) * F + col);
+#pragma unroll
+    for (int q = 0; q < VW; ++q) acc[q] += p.v[q];
+    const float* ss = sslabs + (static_cast<int64_t>(b) * n_rows + row) * H;
+    sh += ss[head];
+    if (lane < H) sl += ss[lane];
+  }
+  Vec<VW> o;
+#pragma unroll
+  for (int q = 0; q < VW; ++q) o.v[q] = normalize ? (any ? acc[q] / sh : 0.f) : acc[q];
+  o.store(y + row * ldy + col);
+  if (sums != nullptr && lane < H) sums[row * H + lane] = sl;
 }
 
 // ---- column-blocked plan: segment table + heavy-first row order -----------
@@ -1819,6 +1877,48 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
 #undef GTA_LEANSEG
     GTA_LAUNCHED("k_agg_seg");
   }
+  return GTA_OK;
+}
+
+int64_t gta_gat_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t blocks, int64_t F, int64_t heads) {
+  if (n_rows < 0 || blocks < 1 || F <= 0 || heads <= 0) return fail(GTA_ERR_ARG, "gat_workspace_bytes: bad sizes");
+  return n_rows * blocks * (F + heads) * static_cast<int64_t>(sizeof(float));
+}
+
+int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
+                              const float* x, int64_t ldx, int64_t F, const float* a_dst, int64_t lda,
+                              const float* b_src, int64_t ldb, int64_t heads, int sf, int normalize, float* y,
+                              int64_t ldy, float* sums, const void* plan, int64_t blocks, void* workspace,
+                              void* stream) {
+  if (!indptr || !indices || !x || !a_dst || !b_src || !y || !plan || !workspace || n_rows < 0 || blocks < 1 ||
+      blocks > 63 || heads <= 0 || lda < heads || ldb < heads)
+    return fail(GTA_ERR_ARG, "gat_aggregate_blocked: bad arguments");
+  if (n_rows == 0) return GTA_OK;
+  const int vq = static_cast<int>(F / 16);
+  if ((F != 64 && F != 128 && F != 256) || F % heads || (F / heads) % vq || ldx % 4 || !aligned(x, 16) ||
+      ldy % (F / 64) || !aligned(y, 4 * (F / 64)))
+    return fail(GTA_ERR_UNSUPPORTED, "gat_aggregate_blocked: F in {64,128,256}, 16-B rows, F/heads a multiple of F/16");
+  const int lph = static_cast<int>((F / heads) / vq);
+  if (lph < 1 || 16 % lph) return fail(GTA_ERR_UNSUPPORTED, "gat_aggregate_blocked: lanes per head must divide 16");
+  const int B = static_cast<int>(blocks);
+  BlockedView v = blocked_view(const_cast<void*>(plan), n_rows, B);
+  SegView sv{v.perm, v.seg, B, 0};
+  hipStream_t s = S(stream);
+  float* slabs = static_cast<float*>(workspace);
+  AttArgs att{a_dst, lda, b_src, ldb, sf, static_cast<int>(heads), slabs + n_rows * B * F};
+  const int64_t items = n_rows * B;
+  const dim3 g4(static_cast<unsigned>((items + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock))), blk(kBlock);
+  const SegItem* it = static_cast<const SegItem*>(v.items);
+  if (vq == 4) k_agg_seg4<4, 4, false, 0, true><<<g4, blk, 0, s>>>(indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, it, att);
+  else if (vq == 8) k_agg_seg4<8, 8, false, 0, true><<<g4, blk, 0, s>>>(indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, it, att);
+  else k_agg_seg4<16, 2, false, 0, true><<<g4, blk, 0, s>>>(indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, it, att);
+  GTA_LAUNCHED("k_agg_seg4<att>");
+  const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+  const int H = static_cast<int>(heads);
+  if (F == 64) k_seg_reduce_att<1><<<g3, blk, 0, s>>>(n_rows, slabs, att.sslabs, H, normalize, y, ldy, sums, sv);
+  else if (F == 128) k_seg_reduce_att<2><<<g3, blk, 0, s>>>(n_rows, slabs, att.sslabs, H, normalize, y, ldy, sums, sv);
+  else k_seg_reduce_att<4><<<g3, blk, 0, s>>>(n_rows, slabs, att.sslabs, H, normalize, y, ldy, sums, sv);
+  GTA_LAUNCHED("k_seg_reduce_att");
   return GTA_OK;
 }
 

@@ -127,6 +127,13 @@ class Executor:
         #   gta_edge_softmax launch (results equal to fp32 rounding, not bitwise)
         self.fuse_softmax = dist is None or not dist.on  # per-row sums span ranks: unfused ops + exchanges
         self.softmax = self._match_softmax()
+        #   fuse_attention: the softmax chain's alpha (or v) * scatter_C(x) -> gather runs as one
+        #   column-blocked gta_gat_aggregate_blocked (no [E, heads] tensor); attention_blocks
+        #   None = ops.BlockedPlan.auto_blocks (used when >= 4), or a fixed block count
+        self.fuse_attention = True
+        self.attention_blocks = None
+        self.attn = self._match_attention()
+        self._att_state = {}
         #   mm_first: a gather whose only consumer is a narrowing applynode MM is executed as
         #   MM-then-aggregate (sum_e w_e x_src) W == sum_e w_e (x W)_src -- the layer's output
         #   to fp32 rounding, the gather's own value computed only if something asks for it
@@ -317,6 +324,58 @@ class Executor:
         self.values[M.idx] = NodeT(self.dist.reduce_rows(y) if self.dist is not None else y)
         return Lazy(lambda: self._gather_value(G))
 
+    def _match_attention(self):
+        """{MUL op M: (softmax pattern, gather G2, x scatter S)} for M = scatter_C(x) * alpha (original,
+        alpha = the pattern's D) or * v (trans, v = V), whose only consumer is a gather R."""
+        found = {}
+        ops_, ins, cons = self.g.ops, self.g.inputs, self.consumers
+        for A, pat in self.softmax.items():
+            w_op = pat["D"] if pat["D"] is not None else pat["V"]
+            cands = [c for c in cons[w_op] if c != pat["G"]]
+            if len(cands) != 1:
+                continue
+            M = cands[0]
+            m = ops_[M]
+            if m.type != "applyedge" or m.comp != "MUL" or self.sem.bin_of(m) != "MUL" or len(ins[M]) != 2:
+                continue
+            srcs = [x.op if x.kind == "op" else None for x in ins[M]]
+            other = [o for o in srcs if o != w_op]
+            if len(other) != 1 or other[0] is None:
+                continue
+            S = other[0]
+            if ops_[S].type != "scatter" or ops_[S].order != "C":
+                continue
+            if len(cons[M]) != 1 or ops_[cons[M][0]].type != "gather" or ops_[cons[M][0]].order != "R":
+                continue
+            found[M] = (pat, cons[M][0], S)
+        return found
+
+    def _eval_attention(self, G2, M):
+        """G2 = gather(scatter_C(x) * alpha|v) as one fused launch; None if the shapes do not allow it."""
+        pat, _, S = self.attn[M]
+        st = self._att_state.get(pat["A"])
+        sv = self.values.get(S)
+        if st is None or not isinstance(sv, Scat) or sv.mode != "src":
+            return None
+        a, b, sf = st
+        x = sv.t
+        F, H = x.shape[1], a.shape[1]
+        if x.dtype != torch.float32 or not ops.BlockedPlan.supports_att(F, H):
+            return None
+        B = self.attention_blocks or ops.BlockedPlan.auto_blocks(self.graph, F)
+        if B < (1 if self.attention_blocks else 4) or not ops.blocked_ready(self.graph, B):
+            return None
+        norm = pat["D"] is not None
+        G = pat["G"]
+        gv = self.values.get(G)
+        want = not norm and isinstance(gv, Lazy) and gv.v is None
+        y, sums = ops.gat_aggregate_blocked(self.graph, x, a, b, sf, normalize=norm, want_sums=want, blocks=B)
+        E, n = self.graph.nnz, self.graph.n_rows
+        self._count(E * (4 + 4 * F + 4 * H) + n * (8 + 4 * F + 4 * H))
+        if want:
+            self.values[G] = NodeT(sums)
+        return NodeT(y)
+
     def _eval_softmax(self, A, pat):
         """Registers V, G (and D) as views of one gta_edge_softmax launch; returns A's own value."""
         ins = self._inputs(A)
@@ -329,6 +388,7 @@ class Executor:
             return None
         V, sf, norm = self.g.ops[pat["V"]], self.sem.sf_of(self.g.ops[pat["V"]]), pat["D"] is not None
         E, n = self.graph.nnz, self.graph.n_rows
+        self._att_state[A.idx] = (a, b, sf)
 
         def launch():
             out, sums = ops.edge_softmax(self.graph, a, b, sf, normalize=norm, want_sums=True)
@@ -402,6 +462,13 @@ class Executor:
     def _eval_gather(self, op):
         if op.order != "R":
             raise NotImplementedError("gather ORDER C (to source) is not emitted by genGraphOP")
+        src = self.g.inputs[op.idx][0]
+        if self.fuse_attention and src.kind == "op" and src.op in self.attn:
+            raw = self.values.get(src.op)
+            if isinstance(raw, (Deferred, Lazy)):
+                y = self._eval_attention(op, src.op)
+                if y is not None:
+                    return y
         v = self._source(op, 0)
         n, E = self.graph.n_rows, self.graph.nnz
         if isinstance(v, Deferred):
@@ -519,6 +586,10 @@ class Executor:
     def _eval(self, op, block):
         fused_into = {p: c for p, c, _ in block.fused}
         if op.type == "scatter":
+            src = self.g.inputs[op.idx][0]
+            raw = self.values.get(src.op) if src.kind == "op" else None
+            if isinstance(raw, Lazy) and raw.v is None:  # keep a fused-away producer unforced
+                return Lazy(lambda: (raw.force(), self._eval(op, block))[1])
             v = self._source(op, 0)
             if isinstance(v, tuple):
                 v = NodeT(self._node(v))
@@ -537,6 +608,8 @@ class Executor:
             v = self._eval_softmax(op, self.softmax[op.idx])
             if v is not None:
                 return v
+        if self.fuse_attention and op.idx in self.attn and fused_into.get(op.idx) is None:
+            return Lazy(lambda: self._eval_applyedge(op))  # its gather consumer runs the fused kernel
         if op.type == "applyedge":
             c = fused_into.get(op.idx)
             if c is not None and self.g.ops[c].type == "gather" and op.comp in ("MUL", "MM"):

@@ -162,6 +162,24 @@ class BlockedPlan:
             self._ws[F] = torch.empty(int(nb), dtype=torch.uint8, device=self.graph.device)
         return self._ws[F]
 
+    def workspace_att(self, F, heads):
+        """Slabs of the fused attention aggregate ([B, N, F] partials + [B, N, heads] sums)."""
+        key = ("att", F, heads)
+        if key not in self._ws:
+            nb = check(_L().gta_gat_aggregate_blocked_workspace_bytes(self.graph.n_rows, self.blocks, F, heads),
+                       "gat_workspace_bytes")
+            self._ws[key] = torch.empty(int(nb), dtype=torch.uint8, device=self.graph.device)
+        return self._ws[key]
+
+    @staticmethod
+    def supports_att(F, heads):
+        """Shapes of gta_gat_aggregate_blocked: F in {64, 128, 256}, (F/heads) a multiple of F/16
+        with lanes per head dividing 16."""
+        if F not in (64, 128, 256) or heads <= 0 or F % heads:
+            return False
+        fh, vq = F // heads, F // 16
+        return fh % vq == 0 and 16 % (fh // vq) == 0
+
     @staticmethod
     def auto_blocks(graph, F):
         """Column blocks for a gathered table of graph.n_cols x F fp32: slices of ~7.5 MB (the
@@ -220,6 +238,43 @@ def aggregate_blocked(graph, x, w=None, row_scale=None, out=None, accumulate=Fal
                                      F, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy, int(bool(accumulate)),
                                      _ptr(plan.buf), plan.blocks, _ptr(ws), _stream(x.device)), "aggregate_blocked")
     return out
+
+
+def blocked_ready(graph, blocks):
+    """True when the column-blocked kernels can run on this graph (rows' columns sorted)."""
+    return graph.blocked_plan(blocks).sorted
+
+
+def gat_aggregate_blocked(graph, x, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize=True, out=None, sums=None,
+                          want_sums=False, plan=None, blocks=16):
+    """Fused GAT attention aggregate (gta_gat_aggregate_blocked): with v = sf(a_dst[dst] + b_src[src]),
+    normalize: out[i] = sum_e v x[src] / sum_e v per head (GAT ops 6-12 without the SF); else the
+    numerator alone.  sums[i, h] = sum_e v (want_sums / sums given).  Returns (out, sums)."""
+    _need_gpu(x, a_dst, b_src, out, sums, graph.indptr)
+    F, H = x.shape[1], a_dst.shape[1]
+    if b_src.shape[1] != H:
+        raise ValueError("gat_aggregate_blocked: a_dst and b_src need the same head count")
+    if not BlockedPlan.supports_att(F, H):
+        raise ValueError(f"gat_aggregate_blocked: unsupported F={F}, heads={H}")
+    if x.shape[0] < graph.n_cols or b_src.shape[0] < graph.n_cols or a_dst.shape[0] < graph.n_rows:
+        raise ValueError("gat_aggregate_blocked: x / b_src need n_cols rows, a_dst n_rows")
+    if plan is None:
+        plan = graph.blocked_plan(blocks)
+    if not plan.sorted:
+        raise ValueError("gat_aggregate_blocked needs every CSR row's columns sorted")
+    if out is None:
+        out = torch.empty(graph.n_rows, F, dtype=torch.float32, device=x.device)
+    if sums is None and want_sums:
+        sums = torch.empty(graph.n_rows, H, dtype=torch.float32, device=x.device)
+    if sums is not None and (not sums.is_contiguous() or tuple(sums.shape) != (graph.n_rows, H)):
+        raise ValueError("gat_aggregate_blocked: sums must be a contiguous [N, heads] tensor")
+    ws = plan.workspace_att(F, H)
+    check(_L().gta_gat_aggregate_blocked(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols,
+                                         _ptr(x), _rows(x, "x"), F, _ptr(a_dst), _rows(a_dst, "a_dst"), _ptr(b_src),
+                                         _rows(b_src, "b_src"), H, _sf(sf), 1 if normalize else 0, _ptr(out),
+                                         _rows(out, "out"), _ptr(sums), _ptr(plan.buf), plan.blocks, _ptr(ws),
+                                         _stream(x.device)), "gat_aggregate_blocked")
+    return out, sums
 
 
 def gather_add(graph, xe, out=None, accumulate=False):

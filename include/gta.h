@@ -131,6 +131,24 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
                           const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
                           int64_t blocks, void* workspace, void* stream);
 
+/* ---- K6' fused GAT attention aggregate (GAT ops 6-12 without the final SF) ----
+ * v(e, h) = sf( a_dst[dst(e), h] + b_src[src(e), h] )
+ * normalize: y[i, c] = sum_e v(e, h(c)) x[src(e), c] / sum_e v(e, h(c))   (0 for rows w/o edges)
+ *            = the GAT-original chain alpha = v / sum (ops 6-10), alpha * x (op 11), gather (op 12)
+ * else:      y[i, c] = sum_e v(e, h(c)) x[src(e), c]     (GAT-trans numerator, op 10)
+ * sums[i, h] = sum_e v(e, h) if sums != NULL (GAT-trans denominator, op 9).  h(c) = c / (F/heads).
+ * Column-blocked like gta_aggregate_blocked (same plan; rows' columns sorted): the score
+ * table b is gathered beside x from the same L2-resident slice and no [E, heads] tensor is
+ * ever written.  workspace >= gta_gat_aggregate_blocked_workspace_bytes.  F in {64, 128,
+ * 256}, x rows 16-B aligned, (F/heads) a multiple of F/16.
+ * Reference: GAT op graph vTCAD/GraphOP/genGraphOP.py:51-64; template/GAT_op.png. */
+int64_t gta_gat_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t blocks, int64_t F, int64_t heads);
+int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
+                              const float* x, int64_t ldx, int64_t F, const float* a_dst, int64_t lda,
+                              const float* b_src, int64_t ldb, int64_t heads, int sf, int normalize, float* y,
+                              int64_t ldy, float* sums, const void* plan, int64_t blocks, void* workspace,
+                              void* stream);
+
 /* ---- K2 GATHER ADD (edge -> node) ---------------------------------------
  * y[i, :] (+)= sum_{e in row i} xe[e, :]    == gta_aggregate(x_mode=EDGE, w=NULL)
  * Reference: gather ISA template/ISA_defination.yaml:46-61; LOAD_E + Virtual

@@ -116,6 +116,15 @@ def edge_softmax(indptr, indices, a_dst, b_src, sf_kind="EXP_LEAKY_RELU", normal
         return v / sums[row_of_edge(indptr)], sums
 
 
+def gat_aggregate(indptr, indices, x, a_dst, b_src, sf_kind="EXP_LEAKY_RELU", normalize=True):
+    """GAT ops 6-12 without the final SF, composed from the ISA ops (genGraphOP.py:51-64):
+    original (normalize): gather_R( scatter_C(x) * alpha ), alpha = edge_softmax;
+    trans: numerator gather_R( scatter_C(x) * v ) and denominator gather_R(v).  Returns (y, sums)."""
+    v, sums = edge_softmax(indptr, indices, a_dst, b_src, sf_kind, normalize=False)
+    w = edge_softmax(indptr, indices, a_dst, b_src, sf_kind, normalize=True)[0] if normalize else v
+    return aggregate(indptr, indices, x, "src", w), sums
+
+
 def aggregate(indptr, indices, x, x_mode="src", w=None, row_scale=None):
     """Fused applyedge MUL -> gather ADD with the scatter FETCH removed
     (hardware_info.yaml Inst_fused [applyedge,gather][MUL,ADD]; code/interpreter.py:575-636, 764-802):

@@ -47,6 +47,31 @@ def edge_softmax(graph, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize=True, out=N
     return _t(o), (_t(su) if (want_sums or sums is not None) else None)
 
 
+def gat_aggregate_blocked(graph, x, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize=True, out=None, sums=None,
+                          want_sums=False, plan=None, blocks=16):
+    ip, ix = graph.numpy()
+    y, su = isa_ref.gat_aggregate(ip, ix, _np(x), _np(a_dst), _np(b_src), sf, normalize)
+    return _t(y), (_t(su) if (want_sums or sums is not None) else None)
+
+
+def blocked_ready(graph, blocks):
+    ip, ix = graph.numpy()
+    return all(np.all(np.diff(ix[ip[r]:ip[r + 1]]) >= 0) for r in range(len(ip) - 1))
+
+
+class BlockedPlan:  # shape rules of the real plan (ops.BlockedPlan), no device state
+    @staticmethod
+    def supports_att(F, heads):
+        if F not in (64, 128, 256) or heads <= 0 or F % heads:
+            return False
+        fh, vq = F // heads, F // 16
+        return fh % vq == 0 and 16 % (fh // vq) == 0
+
+    @staticmethod
+    def auto_blocks(graph, F):
+        return 1
+
+
 def apply_node(bin, sf, a, b=None, out=None, b_broadcast_row=False):
     return _t(isa_ref.apply_node(bin, sf, _np(a), _np(b), b_broadcast_row))
 

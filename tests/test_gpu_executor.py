@@ -142,3 +142,27 @@ def test_legacy_v2_stream_on_gpu(golden_dir, dev, k):
     case = json.load(open(os.path.join(golden_dir, "v2", "manifest.json")))[k]
     res = run_v2(golden_dir, case, dev=dev)
     assert res.launches > 0
+
+
+@pytest.mark.parametrize("reorder", [False, True])
+def test_gat_attention_fusion_on_gpu(golden_dir, manifest, cora, dev, reorder, monkeypatch):
+    """alpha|v * scatter_C(h) -> gather as one gta_gat_aggregate_blocked launch (forced on Cora with
+    attention_blocks): every op, fused-away ones included, matches the fp64 oracle."""
+    sem = Semantics.for_network("GAT", reorder)
+    ip, ix = cora
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
+    calls = []
+    monkeypatch.setattr(ops, "gat_aggregate_blocked",
+                        lambda *a, _real=ops.gat_aggregate_blocked, **k: calls.append(1) or _real(*a, **k))
+    for rec in [s for s in _all_streams(manifest) if s["network"] == "GAT" and s["reorder"] == reorder
+                and s["dataset"] == "cora"][:4]:
+        og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+        st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+        gd = G.from_numpy(ip, ix, device=dev)
+        tc = workloads.make_tensors(og, G.from_numpy(ip, ix), "GAT", seed=6)
+        ex = executor.Executor(og, st, gd, {k: v.to(dev) for k, v in tc.items()}, sem)
+        ex.attention_blocks = 3
+        ex.run()
+        ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tc.items()})
+        compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)), rtol=2e-4)
+    assert calls

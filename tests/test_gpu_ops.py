@@ -388,3 +388,36 @@ def test_update_mm_weight_cache_never_stale(dev):
         w.mul_(2.0)  # in-place update bumps the version: the cache must notice
         assert torch.allclose(ops.update_mm(x, w), 2 * ref, rtol=1e-4, atol=1e-4), seed
         del w
+
+
+@pytest.mark.parametrize("F,heads", [(128, 8), (128, 16), (128, 1), (64, 4), (64, 16), (256, 8), (256, 16)])
+@pytest.mark.parametrize("normalize", [True, False])
+@pytest.mark.parametrize("blocks", [1, 5, 16])
+def test_gat_aggregate_blocked_matches_oracle(dev, F, heads, normalize, blocks):
+    """Fused GAT attention aggregate vs the oracle's op-by-op composition (edge softmax, alpha * x,
+    gather); empty rows give 0 (normalize) and a 3000-edge row spans every block."""
+    n, e = 800, 20000
+    rng = np.random.default_rng(F + heads + blocks)
+    deg = np.diff(G.synthetic(n, e, seed=3).numpy()[0]).copy()
+    deg[11] = 3000
+    deg[[3, 4]] = 0
+    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    ix = np.concatenate([np.sort(rng.integers(0, n, d)) for d in deg]).astype(np.int32)
+    g = G.from_numpy(ip, ix, device=dev)
+    x = rng.standard_normal((n, F)).astype(np.float32)
+    a = rng.standard_normal((n, heads)).astype(np.float32)
+    b = rng.standard_normal((n, heads)).astype(np.float32)
+    y, sums = ops.gat_aggregate_blocked(g, torch.from_numpy(x).to(dev), torch.from_numpy(a).to(dev),
+                                        torch.from_numpy(b).to(dev), normalize=normalize, want_sums=True,
+                                        blocks=blocks)
+    ref, rsum = isa_ref.gat_aggregate(ip, ix, x.astype(np.float64), a.astype(np.float64), b.astype(np.float64),
+                                      "EXP_LEAKY_RELU", normalize)
+    _check(sums, rsum, rsum, f"gat sums F={F} H={heads}")
+    v, _ = isa_ref.edge_softmax(ip, ix, a.astype(np.float64), b.astype(np.float64), "EXP_LEAKY_RELU", False)
+    scale = isa_ref.aggregate(ip, ix, np.abs(x.astype(np.float64)), "src", v)  # sum |v x|
+    if normalize:
+        hs = np.repeat(np.where(rsum > 0, rsum, 1.0), F // heads, axis=1)
+        scale = scale / hs * 4  # |y| terms relative to the row sum (numerator + denominator rounding)
+    _check(y, ref, scale, f"gat y F={F} H={heads} norm={normalize}")
+    if normalize:
+        assert torch.all(y[3] == 0) and torch.all(y[4] == 0)

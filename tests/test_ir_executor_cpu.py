@@ -150,3 +150,28 @@ def test_mm_first_reordering_cpu(golden_dir, manifest, monkeypatch, network):
         nbytes[on] = ex.alg_bytes
         compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
     assert nbytes[True] < nbytes[False]
+
+
+@pytest.mark.parametrize("reorder", [False, True])
+def test_attention_fusion_cpu(golden_dir, manifest, monkeypatch, reorder):
+    """GAT's alpha|v * scatter_C(h) -> gather runs as one fused attention aggregate (forced on the
+    small graph with attention_blocks); every op, fused-away ones included, matches the oracle."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    sem = Semantics.for_network("GAT", reorder)
+    for rec in [s for s in _streams(manifest) if s["network"] == "GAT" and s["reorder"] == reorder][:3]:
+        og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+        st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+        gc, ip, ix = _cora_graph(golden_dir)
+        tensors = workloads.make_tensors(og, gc, "GAT", seed=4)
+        ex = executor.Executor(og, st, gc, tensors, sem)
+        ex.attention_blocks = 2
+        calls = []
+        monkeypatch.setattr(fake_ops, "gat_aggregate_blocked",
+                            lambda *a, _real=fake_ops.gat_aggregate_blocked, **k: calls.append(1) or _real(*a, **k))
+        ex.run()
+        monkeypatch.undo()
+        monkeypatch.setattr(executor, "ops", fake_ops)
+        F, H = og.ops[3].out_width, og.ops[1].out_width
+        assert bool(calls) == fake_ops.BlockedPlan.supports_att(F, H), (rec["file"], F, H)
+        ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
+        compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
