@@ -11,7 +11,9 @@ HBM before the timed region.
 
 --gpus N (launched by torch.distributed.run): edges are partitioned by source
 column ranges; each rank aggregates its shard per destination-row chunk and
-RCCL all-reduces the partial Y chunk by chunk (total work fixed: "strong").
+RCCL reduce-scatters the partial Y chunk by chunk, so each rank ends with the
+summed rows of its own node range (distributed.py's layout; --collective
+all_reduce gives every rank all of Y instead).  Total work fixed: "strong".
 
 Printed JSON (rank 0): value = edges/s of the whole job; roofline = the
 aggregate kernel's algorithmic HBM bytes (548 B/edge + 520 B/node, SURVEY.md
@@ -31,7 +33,7 @@ import torch.distributed as dist
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G, ops, partition  # noqa: E402
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, graph as G, ops, partition  # noqa: E402
 
 N_REDDIT, E_REDDIT = 232965, 114615892
 F, HEADS = 128, 8
@@ -109,6 +111,9 @@ def main():
                     help="column blocks of the blocked aggregate (0 = auto: ~7.5 MB X slices, >= 24 edges/row/block)")
     ap.add_argument("--n", type=int, default=N_REDDIT)
     ap.add_argument("--e", type=int, default=E_REDDIT)
+    ap.add_argument("--collective", choices=["reduce_scatter", "all_reduce"], default="reduce_scatter",
+                    help="N>1 exchange: reduce-scatter hands each rank the summed rows of its own node range "
+                         "(distributed.py layout, half the bytes); all-reduce gives every rank all of Y")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -131,16 +136,32 @@ def main():
 
     g, x, alpha = make_inputs(args.n, args.e, dev)
     nnz_total = g.nnz
+    rs = world > 1 and args.collective == "reduce_scatter"
     if world > 1:
-        shard = partition.make_shard(g, rank, world)
+        n_chunks = args.row_chunks or 8
+        if rs:
+            shard = distributed.DistShard(g, rank, world, chunks=n_chunks)
+        else:
+            shard = partition.make_shard(g, rank, world)
         gl = shard.graph
         xl = x[shard.c0:shard.c1].contiguous()
         wl = alpha[shard.edge_ids].contiguous()
-        n_chunks = args.row_chunks or 8
     else:
         shard, gl, xl, wl = None, g, x, alpha
         n_chunks = args.row_chunks or 1
-    chunked = partition.ChunkedRows(gl, n_chunks=n_chunks, chunk=args.chunk if args.impl == "plan" else 0)
+
+    def make_chunks(chunk):
+        if not rs:
+            return partition.ChunkedRows(gl, n_chunks=n_chunks, chunk=chunk)
+        parts = []  # chunk k = padded rows [k*W*mk, (k+1)*W*mk): one part per rank
+        for k in range(shard.chunks):
+            r0, r1 = shard.chunk_rows(k)
+            gg = partition.sub_rows(gl, r0, r1)
+            parts.append((r0, r1, gg, gg.plan(chunk) if chunk else None))
+        c = partition.ChunkedRows.__new__(partition.ChunkedRows)
+        c.graph, c.parts = gl, parts
+        return c
+    chunked = make_chunks(args.chunk if args.impl == "plan" else 0)
     impl = args.impl
     if impl == "blocked" and not args.blocks:
         args.blocks = auto_blocks(gl, F)
@@ -151,8 +172,9 @@ def main():
             if not (ops.BlockedPlan.supports(F, HEADS) and gg.blocked_plan(args.blocks).sorted):
                 impl = "plan"
         if impl == "plan":
-            chunked = partition.ChunkedRows(gl, n_chunks=n_chunks, chunk=args.chunk)
-    y = torch.empty(g.n_rows, F, device=dev)
+            chunked = make_chunks(args.chunk)
+    y = torch.empty(gl.n_rows if rs else g.n_rows, F, device=dev)
+    y_own = torch.empty(shard.chunks * shard.mk, F, device=dev) if rs else None  # this rank's reduced rows
     stream = torch.cuda.current_stream(dev)
 
     def agg_chunk(gg, xx, ww, out, plan):
@@ -161,7 +183,20 @@ def main():
         return ops.aggregate(gg, xx, "src", ww, out=out, plan=plan)
 
     def step():
-        partition.distributed_aggregate(chunked, xl, wl, y, aggregate_fn=agg_chunk)
+        if not rs:
+            partition.distributed_aggregate(chunked, xl, wl, y, aggregate_fn=agg_chunk)
+            return
+        works = []
+        for k, (r0, r1, gg, plan) in enumerate(chunked.parts):
+            agg_chunk(gg, xl, wl, y[r0:r1], plan)
+            own = y_own[k * shard.mk:(k + 1) * shard.mk]
+            if backend == "nccl":  # RCCL reduce-scatter of chunk k while chunk k+1 computes
+                works.append(dist.reduce_scatter_tensor(own, y[r0:r1], async_op=True))
+            else:  # gloo (1-GPU rehearsal): no reduce-scatter
+                dist.all_reduce(y[r0:r1])
+                own.copy_(y[r0 + rank * shard.mk:r0 + (rank + 1) * shard.mk])
+        for wk in works:
+            wk.wait()
 
     for _ in range(args.warmup):
         step()
@@ -201,10 +236,20 @@ def main():
     y_mine = y.clone()
     if world > 1:
         ref = ops.aggregate(g, x, "src", alpha, plan=args.chunk)
+        if rs:  # reassemble Y from every rank's reduced rows
+            parts = [torch.empty_like(y_own) for _ in range(world)]
+            dist.all_gather(parts, y_own)
+            full = torch.empty_like(ref)
+            for q in range(world):
+                rows = shard.global_rows(q).to(dev)
+                ok = rows >= 0
+                full[rows[ok]] = parts[q][ok]
+            y_mine, what = full, "reduce-scattered shards (reassembled) vs 1-GPU aggregate"
+        else:
+            what = "allreduced shards vs 1-GPU aggregate"
         err = float((y_mine - ref).abs().max().item())
         scale = float(ref.abs().max().item())
-        parity = {"check": "allreduced shards vs 1-GPU aggregate", "max_abs_err": err, "max_abs_ref": scale,
-                  "ok": err <= 1e-4 * scale + 1e-5}
+        parity = {"check": what, "max_abs_err": err, "max_abs_ref": scale, "ok": err <= 1e-4 * scale + 1e-5}
     else:
         step()
         parity = {"check": "repeat run bitwise identical", "ok": bool(torch.equal(y, y_mine))}
@@ -238,7 +283,9 @@ def main():
                 "alpha=per-head softmax over in-edges",
         "config": {"workload": "GAT layer-1 aggregate block [3,11,12] (scatter C -> applyedge MUL -> gather ADD)",
                    "graph": "reddit-shaped", "N": args.n, "E": nnz_total, "F": F, "heads": HEADS,
-                   "parallelism": f"edge-partition by source column x{world}" + (" + RCCL all-reduce" if world > 1 else ""),
+                   "parallelism": f"edge-partition by source column x{world}" + (
+                       (" + RCCL reduce-scatter per row chunk (each rank ends with its node range's rows)" if rs
+                        else " + RCCL all-reduce per row chunk") if world > 1 else ""),
                    "impl": impl, "blocks": args.blocks if impl == "blocked" else None,
                    "plan_chunk": args.chunk if impl == "plan" else None, "row_chunks": n_chunks},
         "achieved_GBps": nnz_total and alg_bytes(g.n_rows, nnz_total) / (ms_per_step / 1e3) / 1e9,

@@ -27,13 +27,19 @@ from .graph import Graph
 class DistShard:
     """Rank `rank`'s part of `graph` (see module docstring)."""
 
-    def __init__(self, graph, rank, world, cuts=None):
+    def __init__(self, graph, rank, world, cuts=None, chunks=1):
+        """chunks > 1: the padded rows are laid out chunk-major -- row j of chunk k of block q at
+        k*world*mk + q*mk + j (mk = ceil(m / chunks)) -- so every chunk is a contiguous
+        [world*mk, F] range holding one part per rank: one reduce-scatter per chunk, issued
+        while the next chunk computes (bench.py's overlap)."""
         cuts = partition.column_cuts(graph, world) if cuts is None else torch.as_tensor(cuts)
         self.cuts = [int(c) for c in cuts]
         self.rank, self.world = rank, world
         self.c0, self.c1 = self.cuts[rank], self.cuts[rank + 1]
         self.n_local = self.c1 - self.c0
         self.m = max(self.cuts[q + 1] - self.cuts[q] for q in range(world))
+        self.chunks = max(1, int(chunks))
+        self.mk = -(-self.m // self.chunks)
         self.n_global, self.e_global = graph.n_rows, graph.nnz
         dev = graph.device
         src = graph.indices
@@ -41,12 +47,32 @@ class DistShard:
         rows = graph.row_of_edge().long()[keep]
         cuts_t = torch.tensor(self.cuts, device=dev, dtype=torch.int64)
         blk = torch.searchsorted(cuts_t, rows, right=True) - 1
-        prow = blk * self.m + (rows - cuts_t[blk])  # padded destination row (monotone in rows)
-        counts = torch.bincount(prow, minlength=world * self.m)
-        indptr = torch.zeros(world * self.m + 1, dtype=torch.int64, device=dev)
+        i = rows - cuts_t[blk]
+        prow = (i // self.mk) * (world * self.mk) + blk * self.mk + i % self.mk  # monotone in rows per chunk
+        n_pad = self.chunks * world * self.mk
+        order = None
+        if self.chunks > 1:  # rows of different chunks interleave: regroup edges by padded row (stable)
+            order = torch.sort(prow, stable=True).indices
+            prow = prow[order]
+        counts = torch.bincount(prow, minlength=n_pad)
+        indptr = torch.zeros(n_pad + 1, dtype=torch.int64, device=dev)
         indptr[1:] = torch.cumsum(counts, 0)
-        self.graph = Graph(indptr, (src[keep].long() - self.c0).to(torch.int32), n_cols=self.n_local)
+        local_src = (src[keep].long() - self.c0).to(torch.int32)
         self.edge_ids = torch.nonzero(keep, as_tuple=False).flatten()
+        if order is not None:
+            local_src, self.edge_ids = local_src[order], self.edge_ids[order]
+        self.graph = Graph(indptr, local_src, n_cols=self.n_local)
+
+    def chunk_rows(self, k):
+        """Padded row range [r0, r1) of chunk k (contains one mk-row part per rank)."""
+        w = self.world * self.mk
+        return k * w, (k + 1) * w
+
+    def global_rows(self, q):
+        """Global row ids of rank q's reduced rows, in its [chunks*mk] output order (-1 = pad)."""
+        n_q = self.cuts[q + 1] - self.cuts[q]
+        j = torch.arange(self.chunks * self.mk)
+        return torch.where(j < n_q, self.cuts[q] + j, torch.full_like(j, -1))
 
     def local_tensors(self, tensors):
         """Global layer tensors -> this rank's: node tensors [N, *] -> row block, edge tensors
@@ -81,6 +107,7 @@ class Comm:
     def reduce_rows(self, y):
         """Partial aggregate over padded rows [world*m, F] -> this rank's summed block [n_p, F]."""
         s = self.s
+        assert s.chunks == 1, "layer execution uses the one-chunk layout"
         if not self.on:
             return y[s.rank * s.m: s.rank * s.m + s.n_local]
         self.bytes += y.numel() * y.element_size()
