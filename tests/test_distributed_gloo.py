@@ -108,3 +108,32 @@ def test_shard_layout_single_process():
         np.testing.assert_array_equal(np.repeat(np.arange(world * s.m), np.diff(sip)), prow)
         total += len(eids)
     assert total == g.nnz
+
+
+@pytest.mark.parametrize("world,chunks", [(3, 4), (2, 1), (4, 3), (8, 8)])
+def test_chunk_major_shard_layout(world, chunks):
+    """bench.py's reduce-scatter layout: padded row k*W*mk + q*mk + j holds global row
+    cuts[q] + k*mk + j; every chunk is one contiguous range with one part per rank; edges keep
+    their CSR order; global_rows() inverts the map for each rank's reduced rows."""
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, graph as G
+    g = G.synthetic(1000, 20000, seed=2)
+    ip, ix = g.numpy()
+    rows_of = np.repeat(np.arange(len(ip) - 1), np.diff(ip))
+    total = 0
+    for r in range(world):
+        s = distributed.DistShard(g, r, world, chunks=chunks)
+        sip, six = s.graph.numpy()
+        assert s.graph.n_rows == chunks * world * s.mk
+        prow = np.repeat(np.arange(len(sip) - 1), np.diff(sip))
+        k, rem = prow // (world * s.mk), prow % (world * s.mk)
+        q, j = rem // s.mk, rem % s.mk
+        eids = s.edge_ids.numpy()
+        np.testing.assert_array_equal(np.array(s.cuts)[q] + k * s.mk + j, rows_of[eids])
+        np.testing.assert_array_equal(ix[eids] - s.c0, six)
+        for a, b in zip(sip[:-1], sip[1:]):
+            assert np.all(np.diff(eids[a:b]) > 0)
+        gr = s.global_rows(r).numpy()
+        own = gr[gr >= 0]
+        np.testing.assert_array_equal(own, np.arange(s.c0, s.c1))
+        total += len(eids)
+    assert total == g.nnz
