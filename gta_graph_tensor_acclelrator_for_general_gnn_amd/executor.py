@@ -80,6 +80,7 @@ class ExecResult:
         self.elapsed_s, self.alg_bytes, self.launches = elapsed_s, alg_bytes, launches
         self.model_cycles = None  # simulate()'s first result (code/simulator.py:502), if requested
         self.model_rw = None      # simulate()'s second result: modelled DRAM bytes
+        self.trace = None         # Chrome trace events when execute(..., trace=...) asked for them
 
     def simulate_tuple(self):
         """(cycles, rw) in the shape the reference's simulate() returns."""
@@ -109,6 +110,10 @@ class Executor:
         self.values = {}
         self.alg_bytes = 0
         self.launches = 0
+        # trace: per evaluated op, device time (HIP events), algorithmic bytes and launches, as
+        # Chrome trace events in the reference's schema (vTCAD/code/simulator.py:360-382)
+        self.trace = False
+        self.trace_events = None
         # execution-level fusion beyond the stream's (results bitwise unchanged):
         #   elide_scatter_stores: a STORE_E'd scatter read back by a later block is read by index
         #   fuse_sf: an SF whose producer feeds only it runs as the producer's post-op
@@ -677,12 +682,19 @@ class Executor:
         missing = set(range(len(self.g))) - covered
         if missing:
             raise ValueError(f"stream does not cover ops {sorted(missing)}")
+        tracer = _Tracer(self) if self.trace else None
         for bi in self.block_order():
             block = self.stream.blocks[bi]
             for i in self.g.topo(block.ops):
                 if i in self.values:  # produced early as a fused post-op
                     continue
+                if tracer:
+                    tracer.begin()
                 self.values[i] = self._eval(self.g.ops[i], block)
+                if tracer:
+                    tracer.end(i, block)
+        if tracer:
+            self.trace_events = tracer.events()
         outputs = {}
         for op in self.g.ops:
             if not op.out_list:
@@ -705,8 +717,74 @@ class Executor:
         return self._final(self.values[op_idx])
 
 
-def run_stream(opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, sync=True):
+class _Tracer:
+    """Brackets each op evaluation with HIP events on the current stream (host clock on CPU)."""
+
+    def __init__(self, ex):
+        self.ex = ex
+        dev = ex.graph.device if ex.graph is not None else torch.device("cpu")
+        self.cuda = dev.type == "cuda"
+        self.dev = dev
+        self.recs = []
+        self.t0 = self._mark()
+
+    def _mark(self):
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(torch.cuda.current_stream(self.dev))
+            return e
+        return time.perf_counter()
+
+    def _us(self, a, b):
+        if self.cuda:
+            return a.elapsed_time(b) * 1e3
+        return (b - a) * 1e6
+
+    def begin(self):
+        self.cur = (self._mark(), self.ex.alg_bytes, self.ex.launches)
+
+    def end(self, i, block):
+        m0, b0, l0 = self.cur
+        self.recs.append((i, block, m0, self._mark(), self.ex.alg_bytes - b0, self.ex.launches - l0))
+
+    def events(self):
+        if self.cuda:
+            torch.cuda.synchronize(self.dev)
+        out = []
+        for i, block, m0, m1, nbytes, nl in self.recs:
+            op = self.ex.g.ops[i]
+            insts = [ins for ins in getattr(block, "insts", []) if ins.kind == "comp" and
+                     any(p[0] == i for p in ins.parts)]
+            name = insts[0].type if insts else f"{op.type.upper()}_{op.comp}"
+            cat = insts[0].id if insts else f"{i}_{op.type}_0"
+            out.append({"name": name, "cat": cat, "ph": "X", "ts": self._us(self.t0, m0),
+                        "dur": self._us(m0, m1), "pid": "MI355X", "tid": f"block {block.index}",
+                        "args": {"op": i, "alg_bytes": nbytes, "launches": nl}})
+        return out
+
+
+def save_chrome_trace(events, path):
+    """Chrome trace JSON (chrome://tracing, Perfetto), as the reference's save_timeline_to_json."""
+    import json
+    import os
+    os.makedirs(os.path.dirname(os.path.abspath(path)), exist_ok=True)
+    with open(path, "w") as f:
+        json.dump(events, f, indent=1)
+
+
+def aggregate_trace(events):
+    """{name: (count, total µs, total algorithmic bytes)} -- the reference's aggregate_timeline /
+    aggregate_rw_record (code/simulator.py:107-146) over measured events."""
+    agg = {}
+    for e in events:
+        c, t, b = agg.get(e["name"], (0, 0.0, 0))
+        agg[e["name"]] = (c + 1, t + e["dur"], b + e["args"]["alg_bytes"])
+    return agg
+
+
+def run_stream(opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, sync=True, trace=False):
     ex = Executor(opgraph, stream, graph, tensors, semantics, plan_chunk)
+    ex.trace = trace
     dev = graph.device
     sync = sync and dev.type == "cuda"
     if sync:
@@ -747,7 +825,7 @@ def attach_model(res, stream_records, tile_size_list, graph, model="rw", isSinpu
 
 def execute(tile_size_list, dataset, network, layer, isReorder, isSinput=False, *, graph, tensors,
             inst_root="Results/Insts", op_root="Network", inst_path=None, op_path=None, semantics=None,
-            plan_chunk=512, model="rw"):
+            plan_chunk=512, model="rw", trace=None):
     """Drop-in for simulate(tile_size_list, dataset, network, layer, isReorder, isSinput)
     (code/simulator.py:370): same leading arguments, same files, real execution.
 
@@ -755,12 +833,17 @@ def execute(tile_size_list, dataset, network, layer, isReorder, isSinput=False, 
     reference's modelled numbers for the same stream: model_rw (always, closed
     form) and model_cycles (model="full"; exact restatement of the cycle loop,
     Python-speed, meant for Cora/Flickr-sized graphs).  `res.simulate_tuple()`
-    is what simulate() would have returned."""
+    is what simulate() would have returned.  trace: True (events in res.trace) or a path for a
+    Chrome trace JSON of the measured per-op device time, as the reference's chrome_timeline.json."""
     sem = semantics or Semantics.for_network(network, isReorder)
     op_path = op_path or ir.op_yaml_path(network, dataset, layer, isReorder, op_root)
     inst_path = inst_path or ir.inst_path(network, dataset, layer, isReorder, inst_root)
     g = ir.OpGraph.load(op_path, sem.inputs)
     records = ir.read_yaml(inst_path)
     s = ir.Stream(records)
-    res, _ = run_stream(g, s, graph, tensors, sem, plan_chunk)
+    res, ex = run_stream(g, s, graph, tensors, sem, plan_chunk, trace=trace is not None)
+    if trace is not None:
+        res.trace = ex.trace_events
+        if isinstance(trace, str):
+            save_chrome_trace(ex.trace_events, trace)
     return attach_model(res, records, tile_size_list, graph, model, isSinput, dataset)

@@ -8,10 +8,10 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-from gta_graph_tensor_acclelrator_for_general_gnn_amd import configs  # noqa: E402
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import configs, executor  # noqa: E402
 
 
-def main(names=None, reps=5):
+def main(names=None, reps=5, trace=False):
     dev = torch.device("cuda:0")
     out = {}
     for name in (names or list(configs.CONFIGS)):
@@ -32,6 +32,16 @@ def main(names=None, reps=5):
             if r:
                 times.append(time.perf_counter() - t1)
         ms = 1e3 * sorted(times)[len(times) // 2]
+        if trace:  # one more forward with per-op HIP-event tracing (Chrome JSON)
+            x = None
+            events = []
+            for lay, t in zip(layers, tensors):
+                if x is not None:
+                    t["x"] = x
+                res, ex = executor.run_stream(lay.opgraph, lay.stream, g, t, lay.sem, trace=True)
+                events += ex.trace_events
+                x = res.outputs[sorted(res.outputs)[-1]]
+            executor.save_chrome_trace(events, os.path.join(ROOT, "gpurun_out", f"trace_{name}.json"))
         out[name] = {"N": g.n_rows, "E": g.nnz, "layers": [l.layer for l in layers],
                      "op_array": [l.op_array for l in layers], "tile_size_list": [l.tile_size_list for l in layers],
                      "ms_per_forward": ms, "edges_per_s": g.nnz * len(layers) / (ms / 1e3), "build_s": build_s}
@@ -44,4 +54,5 @@ def main(names=None, reps=5):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1:] or None)
+    argv = [a for a in sys.argv[1:] if a != "--trace"]
+    main(argv or None, trace="--trace" in sys.argv[1:])

@@ -166,3 +166,24 @@ def test_gat_attention_fusion_on_gpu(golden_dir, manifest, cora, dev, reorder, m
         ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tc.items()})
         compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)), rtol=2e-4)
     assert calls
+
+
+def test_execute_chrome_trace_on_gpu(golden_dir, manifest, cora, dev, tmp_path, monkeypatch):
+    """execute(..., trace=path) writes the measured per-op timeline (HIP events) as Chrome JSON."""
+    import json
+    import shutil
+    rec = [s for s in manifest["streams"] if s.get("file") == "GCN-cora-layer1-original-c0.yaml"][0]
+    monkeypatch.chdir(tmp_path)
+    os.makedirs("Results/Insts")
+    os.makedirs("Network/GCN/GCN-cora/GCN-original")
+    shutil.copy(os.path.join(golden_dir, "streams", rec["file"]), "Results/Insts/GCN-cora-layer1-original.yaml")
+    shutil.copy(os.path.join(golden_dir, "ops", rec["op_yaml"]), "Network/GCN/GCN-cora/GCN-original/GCN-layer1-original.yaml")
+    ip, ix = cora
+    gd = G.from_numpy(ip, ix, device=dev)
+    og = ir.OpGraph.load("Network/GCN/GCN-cora/GCN-original/GCN-layer1-original.yaml")
+    tensors = workloads.make_tensors(og, gd, "GCN", seed=0)
+    res = executor.execute(rec["tile_size_list"], "cora", "GCN", "layer1", False, False, graph=gd, tensors=tensors,
+                           trace="trace/chrome_timeline.json")
+    ev = json.load(open("trace/chrome_timeline.json"))
+    assert ev == res.trace and len(ev) >= 1
+    assert all(e["ph"] == "X" and e["dur"] >= 0 for e in ev) and sum(e["dur"] for e in ev) > 0

@@ -175,3 +175,25 @@ def test_attention_fusion_cpu(golden_dir, manifest, monkeypatch, reorder):
         assert bool(calls) == fake_ops.BlockedPlan.supports_att(F, H), (rec["file"], F, H)
         ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
         compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
+
+
+def test_chrome_trace_cpu(golden_dir, manifest, monkeypatch, tmp_path):
+    """trace=True: one complete ("X") event per evaluated op in the reference's Chrome schema
+    (vTCAD/code/simulator.py:360-382), names from the stream's COMP instructions, bytes summed."""
+    import json
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    rec = [s for s in _streams(manifest) if s["network"] == "GAT" and not s["reorder"]][0]
+    sem = Semantics.for_network("GAT", False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    gc, ip, ix = _cora_graph(golden_dir)
+    res, ex = executor.run_stream(og, st, gc, workloads.make_tensors(og, gc, "GAT"), sem, trace=True)
+    ev = ex.trace_events
+    assert ev and all(e["ph"] == "X" and e["dur"] >= 0 and {"name", "cat", "ts", "pid", "tid"} <= set(e) for e in ev)
+    assert sum(e["args"]["alg_bytes"] for e in ev) == ex.alg_bytes
+    assert any(e["name"].startswith("COMP_") for e in ev)
+    path = tmp_path / "trace" / "chrome_timeline.json"
+    executor.save_chrome_trace(ev, str(path))
+    assert json.load(open(path)) == ev
+    agg = executor.aggregate_trace(ev)
+    assert sum(c for c, _, _ in agg.values()) == len(ev)
