@@ -415,7 +415,7 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
         out = torch.empty(M, N, dtype=torch.float32, device=x.device)
     ldo = _rows(out, "out")
     dt = _lib.GTA_F32_BF16 if mixed else (_lib.GTA_F32 if x.dtype == torch.float32 else _lib.GTA_BF16)
-    if MM_FORM == "rows":  # row-streaming kernel on W^T (cached per weight version)
+    if MM_FORM == "rows" and M >= MM_ROWS_MIN_M:  # row-streaming kernel on W^T (cached per weight version)
         wt = _transposed(w)
         check(_L().gta_update_mm_t(_ptr(x), ldx, _ptr(row_idx), M, K, _ptr(wt), _rows(wt, "w^T", wt.dtype), N, dt, _sf(sf),
                                    _ptr(out), ldo, _stream(x.device)), "update_mm_t")
@@ -426,6 +426,7 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
 
 
 MM_FORM = "rows"  # "rows": gta_update_mm_t (x read once per output); "tile": gta_update_mm 64x64 tiles
+MM_ROWS_MIN_M = 32768  # below this the 128-row groups are too few to fill 256 CUs: 64x64 tiles win
 _WT_CACHE = {}
 
 

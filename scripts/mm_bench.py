@@ -41,6 +41,7 @@ def main():
         outs = {}
         for form in (0, 1):
             ops.MM_FORM = "rows" if form else "tile"
+            ops.MM_ROWS_MIN_M = 0
             if form:
                 for bpc in (2, 8):
                     ops.set_debug("mm_blocks_per_cu", bpc)

@@ -364,12 +364,12 @@ def test_update_mm_both_forms(dev, form, M, K, N, dt):
         xs, w = xs.to(torch.bfloat16), w.to(torch.bfloat16)
     elif dt == "mixed":
         w = w.to(torch.bfloat16)
-    old = ops.MM_FORM
-    ops.MM_FORM = form
+    old = ops.MM_FORM, ops.MM_ROWS_MIN_M
+    ops.MM_FORM, ops.MM_ROWS_MIN_M = form, 0
     try:
         out = ops.update_mm(xs.to(dev), w.to(dev))
     finally:
-        ops.MM_FORM = old
+        ops.MM_FORM, ops.MM_ROWS_MIN_M = old
     xr = xs.float().numpy().astype(np.float64)
     if dt != "f32":
         xr = torch.from_numpy(xr).to(torch.bfloat16).double().numpy()
@@ -379,7 +379,7 @@ def test_update_mm_both_forms(dev, form, M, K, N, dt):
 
 def test_update_mm_weight_cache_never_stale(dev):
     """A new weight at a freed weight's address (same shape/dtype) must not reuse the old W^T."""
-    x = torch.randn(300, 64, device=dev)
+    x = torch.randn(40000, 64, device=dev)  # large enough for the row-streaming (W^T) form
     for seed in range(6):
         w = torch.randn(64, 32, device=dev, generator=torch.Generator(device=dev).manual_seed(seed))
         got = ops.update_mm(x, w)
