@@ -1526,9 +1526,11 @@ k_tile_nnz(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indic
   const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
   if (row >= n_rows) return;
   int32_t* base = counts + (row / T) * n_cols;
-  for (int64_t e = indptr[row] + lane; e < indptr[row + 1]; e += kWave) {
+  const int64_t eb = indptr[row];
+  for (int64_t e = eb + lane; e < indptr[row + 1]; e += kWave) {
     const int32_t j = indices[e];
-    if (j != row) atomicAdd(base + j, 1);
+    // a dense adjacency holds each (row, j) once: skip self loops and repeats of the previous column
+    if (j != row && (e == eb || indices[e - 1] != j)) atomicAdd(base + j, 1);
   }
 }
 
@@ -1654,12 +1656,18 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
                      const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
                   const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
                   int64_t plan_chunk, void* workspace, void* stream) {
-  if (!indptr || !x || !y || n_rows < 0 || nnz < 0 || F <= 0) return fail(GTA_ERR_ARG, "aggregate: bad arguments");
+  if (n_rows < 0 || nnz < 0 || F <= 0) return fail(GTA_ERR_ARG, "aggregate: bad sizes");
   if (x_mode != GTA_IDX_EDGE && x_mode != GTA_IDX_SRC && x_mode != GTA_IDX_DST)
     return fail(GTA_ERR_ARG, "aggregate: bad x_mode");
-  if (x_mode == GTA_IDX_SRC && !indices) return fail(GTA_ERR_ARG, "aggregate: x_mode SRC needs indices");
   if (F > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "aggregate: F too large");
   if (n_rows == 0) return GTA_OK;
+  // with no edges, indices / edge operands are never read (may be NULL); every row gets 0
+  if (!indptr || !y || (nnz > 0 && !x)) return fail(GTA_ERR_ARG, "aggregate: bad arguments");
+  if (x_mode == GTA_IDX_SRC && !indices && nnz > 0) return fail(GTA_ERR_ARG, "aggregate: x_mode SRC needs indices");
+  if (nnz == 0) {
+    x = y;  // any valid address: no row has an edge to read
+    w = nullptr;
+  }
   int wm = WM_NONE, gsz = 1;
   if (w) {
     if (heads <= 0 || F % heads != 0) return fail(GTA_ERR_ARG, "aggregate: heads must divide F");
@@ -1753,7 +1761,7 @@ int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t blocks) {
 
 int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
                                      int64_t blocks, void* plan, int64_t plan_bytes, void* stream) {
-  if (!indptr || !indices || !plan || n_rows <= 0 || n_cols <= 0 || blocks < 1 || blocks > 63)
+  if (!indptr || !plan || n_rows <= 0 || n_cols <= 0 || blocks < 1 || blocks > 63)
     return fail(GTA_ERR_ARG, "blocked_plan_build: bad arguments");
   if (n_rows > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "blocked_plan_build: > 2^31 rows");
   const int B = static_cast<int>(blocks);
@@ -1784,9 +1792,9 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
                           const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
                           const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
                           int64_t blocks, void* workspace, void* stream) {
-  if (!indptr || !indices || !x || !y || !plan || n_rows < 0 || F <= 0 || blocks < 1 || blocks > 63)
-    return fail(GTA_ERR_ARG, "aggregate_blocked: bad arguments");
+  if (n_rows < 0 || F <= 0 || blocks < 1 || blocks > 63) return fail(GTA_ERR_ARG, "aggregate_blocked: bad sizes");
   if (n_rows == 0) return GTA_OK;
+  if (!indptr || !x || !y || !plan) return fail(GTA_ERR_ARG, "aggregate_blocked: bad arguments");
   int gl = 0, vw = 0;
   for (int c : {4, 2, 1}) {
     if (F == static_cast<int64_t>(kWave) * c && ldx % c == 0 && ldy % c == 0 && aligned(x, 4 * c) && aligned(y, 4 * c)) {
@@ -1890,10 +1898,11 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
                               const float* b_src, int64_t ldb, int64_t heads, int sf, int normalize, float* y,
                               int64_t ldy, float* sums, const void* plan, int64_t blocks, void* workspace,
                               void* stream) {
-  if (!indptr || !indices || !x || !a_dst || !b_src || !y || !plan || !workspace || n_rows < 0 || blocks < 1 ||
-      blocks > 63 || heads <= 0 || lda < heads || ldb < heads)
-    return fail(GTA_ERR_ARG, "gat_aggregate_blocked: bad arguments");
+  if (n_rows < 0 || blocks < 1 || blocks > 63 || heads <= 0 || lda < heads || ldb < heads)
+    return fail(GTA_ERR_ARG, "gat_aggregate_blocked: bad sizes");
   if (n_rows == 0) return GTA_OK;
+  if (!indptr || !x || !a_dst || !b_src || !y || !plan || !workspace)
+    return fail(GTA_ERR_ARG, "gat_aggregate_blocked: bad arguments");
   const int vq = static_cast<int>(F / 16);
   if ((F != 64 && F != 128 && F != 256) || F % heads || (F / heads) % vq || ldx % 4 || !aligned(x, 16) ||
       ldy % (F / 64) || !aligned(y, 4 * (F / 64)))
@@ -1930,12 +1939,13 @@ int gta_gather_add(const int64_t* indptr, int64_t n_rows, int64_t nnz, const flo
 
 int gta_scatter(int dir, const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, const void* x,
                 int64_t ldx, int64_t F, int dtype, void* out, int64_t ldo, void* stream) {
-  if (!indptr || !x || !out || n_rows < 0 || F <= 0) return fail(GTA_ERR_ARG, "scatter: bad arguments");
+  if (n_rows < 0 || nnz < 0 || F <= 0) return fail(GTA_ERR_ARG, "scatter: bad sizes");
   if (dir != GTA_DIR_R && dir != GTA_DIR_C) return fail(GTA_ERR_ARG, "scatter: bad dir");
-  if (dir == GTA_DIR_C && !indices) return fail(GTA_ERR_ARG, "scatter C needs indices");
   const int esz = (dtype == GTA_BF16) ? 2 : (dtype == GTA_F32 ? 4 : 0);
   if (!esz) return fail(GTA_ERR_ARG, "scatter: bad dtype");
   if (n_rows == 0 || nnz == 0) return GTA_OK;
+  if (!indptr || !x || !out) return fail(GTA_ERR_ARG, "scatter: bad arguments");
+  if (dir == GTA_DIR_C && !indices) return fail(GTA_ERR_ARG, "scatter C needs indices");
   const int64_t rowb = F * esz, ldxb = ldx * esz, ldob = ldo * esz;
   int unit = 16;
   while (unit > 2 && (rowb % unit || ldxb % unit || ldob % unit || !aligned(x, unit) || !aligned(out, unit))) unit >>= 1;
@@ -1973,7 +1983,9 @@ static int check_bcast(int64_t Fa, int64_t Fb, bool has_b, int64_t* Fo) {
 int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
                    const float* a, int a_mode, int64_t lda, int64_t Fa, const float* b, int b_mode, int64_t ldb,
                    int64_t Fb, float* out, int64_t ldo, void* stream) {
-  if (!indptr || !a || !out || n_rows < 0 || Fa <= 0) return fail(GTA_ERR_ARG, "apply_edge: bad arguments");
+  if (n_rows < 0 || nnz < 0 || Fa <= 0) return fail(GTA_ERR_ARG, "apply_edge: bad sizes");
+  if (n_rows == 0 || nnz == 0) return GTA_OK;  // no edge: nothing to write (operands may be NULL)
+  if (!indptr || !a || !out) return fail(GTA_ERR_ARG, "apply_edge: bad arguments");
   if ((a_mode == GTA_IDX_SRC || (b && b_mode == GTA_IDX_SRC)) && !indices)
     return fail(GTA_ERR_ARG, "apply_edge: SRC operand needs indices");
   int64_t Fo;
@@ -1989,7 +2001,9 @@ int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indice
 
 int gta_apply_node(int bin, int sf, int64_t n, const float* a, int64_t lda, int64_t Fa, const float* b, int64_t ldb,
                    int64_t Fb, float* out, int64_t ldo, void* stream) {
-  if (!a || !out || n < 0 || Fa <= 0) return fail(GTA_ERR_ARG, "apply_node: bad arguments");
+  if (n < 0 || Fa <= 0) return fail(GTA_ERR_ARG, "apply_node: bad sizes");
+  if (n == 0) return GTA_OK;
+  if (!a || !out) return fail(GTA_ERR_ARG, "apply_node: bad arguments");
   int64_t Fo;
   if (check_bcast(Fa, Fb, b != nullptr, &Fo)) return fail(GTA_ERR_ARG, "apply_node: widths must divide");
   if (n == 0) return GTA_OK;
@@ -2040,7 +2054,9 @@ int gta_edge_softmax(const int64_t* indptr, const int32_t* indices, int64_t n_ro
 
 int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* w,
                   int64_t ldw, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream) {
-  if (!x || !w || !out || M < 0 || K <= 0 || N <= 0) return fail(GTA_ERR_ARG, "update_mm: bad arguments");
+  if (M < 0 || K <= 0 || N <= 0) return fail(GTA_ERR_ARG, "update_mm: bad sizes");
+  if (M == 0) return GTA_OK;
+  if (!x || !w || !out) return fail(GTA_ERR_ARG, "update_mm: bad arguments");
   if (K > INT32_MAX || N > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "update_mm: K/N too large");
   if (M == 0) return GTA_OK;
   if (dtype != GTA_F32 && dtype != GTA_BF16 && dtype != GTA_F32_BF16) return fail(GTA_ERR_ARG, "update_mm: bad dtype");
@@ -2066,7 +2082,9 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
 
 int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                     int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream) {
-  if (!x || !wt || !out || M < 0 || K <= 0 || N <= 0 || ldwt < K) return fail(GTA_ERR_ARG, "update_mm_t: bad arguments");
+  if (M < 0 || K <= 0 || N <= 0 || ldwt < K) return fail(GTA_ERR_ARG, "update_mm_t: bad sizes");
+  if (M == 0) return GTA_OK;
+  if (!x || !wt || !out) return fail(GTA_ERR_ARG, "update_mm_t: bad arguments");
   if (K > INT32_MAX || N > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t: K/N too large");
   if (dtype != GTA_F32 && dtype != GTA_BF16 && dtype != GTA_F32_BF16) return fail(GTA_ERR_ARG, "update_mm_t: bad dtype");
   if (M == 0) return GTA_OK;
@@ -2094,7 +2112,7 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
 
 int gta_tile_nnz(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols, int64_t T,
                  int32_t* counts, void* stream) {
-  if (!indptr || !indices || !counts || n_rows < 0 || n_cols <= 0 || T <= 0)
+  if (!indptr || !counts || n_rows < 0 || n_cols <= 0 || T <= 0)
     return fail(GTA_ERR_ARG, "tile_nnz: bad arguments");
   if (n_rows == 0) return GTA_OK;
   const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));

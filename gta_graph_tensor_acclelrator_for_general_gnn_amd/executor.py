@@ -803,7 +803,7 @@ SPARSITY = {"cora": 0.012, "pubmed": 0.1, "flickr": 0.46, "reddit": 1}  # code/s
 def attach_model(res, stream_records, tile_size_list, graph, model="rw", isSinput=False, dataset=None):
     """Fill res.model_rw (closed form) and, for model == "full", res.model_cycles via the exact
     cost-model restatement (costmodel.py).  Tile nnz come from the GPU (gta_tile_nnz); like the
-    reference's dense adjacency they assume a duplicate-free CSR."""
+    reference's dense adjacency they count a repeated (dst, src) once when rows are column-sorted."""
     from . import costmodel
     if model is None:
         return res

@@ -124,6 +124,8 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
     ldy = _rows(out, "out")
     if out.shape[0] < graph.n_rows or out.shape[1] != F:
         raise ValueError("out must be [N, F]")
+    if graph.n_rows == 0:
+        return out
     if isinstance(plan, int):
         plan = graph.plan(plan)
     pbuf = ws = None

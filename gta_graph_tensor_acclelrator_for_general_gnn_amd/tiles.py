@@ -7,7 +7,8 @@ largest block per T (cal_min_sparsity :53-63) and the tile-size list (gen_size
 ("FinalVersion For Paper/preprocessing_forReditFlickr.py":6-41).  A dense
 232,965^2 matrix is 217 GB, so here the counts come straight from the CSR with
 one integer-atomic histogram kernel (gta_tile_nnz); equal to the dense count for
-a duplicate-free CSR (tests/test_gpu_ops.py pins it to the reference's output).
+a CSR with column-sorted rows, duplicates included (tests/test_gpu_ops.py pins it
+to the reference's output).
 """
 import torch
 

@@ -208,10 +208,11 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
                     int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream);
 
 /* ---- f2 TILE-NNZ metadata ----------------------------------------------
- * counts[t, j] = #{ e : dst(e) in [t*T, (t+1)*T), src(e) == j, dst(e) != j }
+ * counts[t, j] = #{ distinct (dst, j) : dst in [t*T, (t+1)*T), an edge dst <- j, dst != j }
  * for t < ceil(n_rows/T), j < n_cols (int32 [ceil(n_rows/T), n_cols]).
- * Every CSR entry counts, so a duplicate-free CSR gives the dense
- * count_nonzero of the reference; the caller zeroes counts first.
+ * A repeated column counts once when it repeats the previous entry of its row, so a CSR
+ * with sorted rows (duplicates adjacent) gives exactly the dense count_nonzero of the
+ * reference; the caller zeroes counts first.
  * Reference: calculate_sparsity code/preprocessing.py:12-40 (dense
  * count_nonzero per T x 1 block after removing self loops). */
 int gta_tile_nnz(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,

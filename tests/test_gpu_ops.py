@@ -421,3 +421,59 @@ def test_gat_aggregate_blocked_matches_oracle(dev, F, heads, normalize, blocks):
     _check(y, ref, scale, f"gat y F={F} H={heads} norm={normalize}")
     if normalize:
         assert torch.all(y[3] == 0) and torch.all(y[4] == 0)
+
+
+@pytest.mark.parametrize("case", ["no_edges", "no_rows", "one_row", "dup_self"])
+def test_degenerate_graphs_every_op(dev, case):
+    """Empty and ragged extremes through every entry point: a graph without edges, without rows,
+    one row holding every edge, and duplicate edges plus self loops -- results equal the oracle."""
+    rng = np.random.default_rng(5)
+    if case == "no_edges":
+        ip, ix = np.zeros(6, np.int64), np.zeros(0, np.int32)
+    elif case == "no_rows":
+        ip, ix = np.zeros(1, np.int64), np.zeros(0, np.int32)
+    elif case == "one_row":
+        n = 300
+        ip = np.zeros(n + 1, np.int64)
+        ip[n // 2 + 1:] = 9000
+        ix = np.sort(rng.integers(0, n, 9000)).astype(np.int32)
+    else:
+        n = 50
+        deg = rng.integers(0, 40, n)
+        ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+        ix = np.concatenate([np.sort(np.concatenate([[r] * 3, rng.integers(0, 5, max(0, d - 3))]))[:d]
+                             for r, d in enumerate(deg)]).astype(np.int32)
+    n, e = len(ip) - 1, len(ix)
+    ncols = max(n, 1)
+    g = G.Graph(torch.from_numpy(ip).to(dev), torch.from_numpy(ix).to(dev), n_cols=ncols)
+    F, H = 128, 8
+    x = rng.standard_normal((ncols, F)).astype(np.float32)
+    w = rng.random((e, H)).astype(np.float32)
+    xd, wd = torch.from_numpy(x).to(dev), torch.from_numpy(w).to(dev)
+    ref = isa_ref.aggregate(ip, ix, x, "src", w) if n else np.zeros((0, F))
+    scale = isa_ref.aggregate_abs(ip, ix, x, "src", w) if n else np.zeros((0, F))
+    for plan in (None, 64):
+        _check(ops.aggregate(g, xd, "src", wd, plan=plan), ref, scale, f"{case} aggregate plan={plan}")
+    if n:
+        _check(ops.aggregate_blocked(g, xd, wd, blocks=4), ref, scale, f"{case} blocked")
+        a = rng.standard_normal((n, H)).astype(np.float32)
+        b = rng.standard_normal((ncols, H)).astype(np.float32)
+        y, _ = ops.gat_aggregate_blocked(g, xd, torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev), blocks=4)
+        yr, _ = isa_ref.gat_aggregate(ip, ix, x.astype(np.float64), a.astype(np.float64), b.astype(np.float64))
+        assert np.allclose(y.cpu().numpy(), yr, rtol=1e-4, atol=1e-5)
+        al, su = ops.edge_softmax(g, torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev), want_sums=True)
+        ar, sr = isa_ref.edge_softmax(ip, ix, a.astype(np.float64), b.astype(np.float64))
+        assert np.allclose(al.cpu().numpy(), ar, rtol=1e-4, atol=1e-6) and np.allclose(su.cpu().numpy(), sr, rtol=1e-4)
+    xe = torch.from_numpy(rng.standard_normal((e, 16)).astype(np.float32)).to(dev)
+    _check(ops.gather_add(g, xe), isa_ref.gather_add(ip, xe.cpu().numpy()) if n else np.zeros((0, 16)),
+           isa_ref.gather_add(ip, np.abs(xe.cpu().numpy())) if n else np.zeros((0, 16)), f"{case} gather")
+    for d in ("R", "C"):
+        got = ops.scatter(g, xd, d)
+        assert got.shape == (e, F)
+        assert np.array_equal(got.cpu().numpy(), isa_ref.scatter(ip, ix, x, d))
+    out = ops.apply_edge(g, "ADD", "RELU", wd, "edge", xd[:, :H].contiguous(), "src")
+    assert np.allclose(out.cpu().numpy(), isa_ref.apply_edge(ip, ix, "ADD", "RELU", w, "edge", x[:, :H], "src"))
+    assert ops.update_mm(xd[:0], torch.randn(F, 16, device=dev)).shape == (0, 16)
+    if n:
+        counts = ops.tile_nnz(g, 16).cpu().numpy()
+        assert np.array_equal(counts, isa_ref.tile_nnz(ip, ix, ncols, 16))
