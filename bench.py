@@ -9,11 +9,17 @@ fp32.  Inputs are synthetic (seeded lognormal-degree CSR, uniform sources,
 X ~ N(0,1), alpha = softmax over in-edges of N(0,1) logits) and resident in
 HBM before the timed region.
 
---gpus N (launched by torch.distributed.run): edges are partitioned by source
-column ranges; each rank aggregates its shard per destination-row chunk and
-RCCL reduce-scatters the partial Y chunk by chunk, so each rank ends with the
-summed rows of its own node range (distributed.py's layout; --collective
-all_reduce gives every rank all of Y instead).  Total work fixed: "strong".
+--gpus N (launched by torch.distributed.run): the edges are cut into a 2-D grid
+of tiles -- pr row groups (destination rows, nnz-balanced) x pc column groups
+(source columns, nnz-balanced), the reference's row-tile x column blocking
+(code/preprocessing.py:26-38) -- 1x2, 2x2, 4x2 at N = 2, 4, 8.  Each rank
+aggregates its tile in one launch and the pc ranks of a row group sum their
+partial aggregates with one RCCL reduce-scatter, so every rank ends with its
+share of Y's rows.  Measured per-rank compute on one GPU (profiles/
+r01_shard_probe*.json) is why: a 1-D source-column shard keeps every row, and
+per-row work does not shrink with N.  --layout chunked keeps the 1-D shards
+with per-row-chunk collectives (--collective all_reduce | reduce_scatter).
+Total work fixed: "strong".
 
 Printed JSON (rank 0): value = edges/s of the whole job; roofline = the
 aggregate kernel's algorithmic HBM bytes (548 B/edge + 520 B/node, SURVEY.md
@@ -109,11 +115,16 @@ def main():
                     help="blocked: column-blocked aggregate (L2-resident X slices); plan: row-chunked single pass")
     ap.add_argument("--blocks", type=int, default=0,
                     help="column blocks of the blocked aggregate (0 = auto: ~7.5 MB X slices, >= 24 edges/row/block)")
-    ap.add_argument("--n", type=int, default=N_REDDIT)
-    ap.add_argument("--e", type=int, default=E_REDDIT)
+    ap.add_argument("--n", "--graph-nodes", dest="n", type=int, default=N_REDDIT)
+    ap.add_argument("--e", "--graph-edges", dest="e", type=int, default=E_REDDIT)
     ap.add_argument("--collective", choices=["reduce_scatter", "all_reduce"], default="reduce_scatter",
                     help="N>1 exchange: reduce-scatter hands each rank the summed rows of its own node range "
                          "(distributed.py layout, half the bytes); all-reduce gives every rank all of Y")
+    ap.add_argument("--layout", choices=["grid", "chunked"], default="grid",
+                    help="N>1: grid = 2-D edge tiles (row groups x column groups, distributed.GridShard), one "
+                         "aggregate launch per rank, reduce-scatter inside each row group; chunked = 1-D source-"
+                         "column shards over all rows, per-row-chunk collectives overlapped with compute")
+    ap.add_argument("--grid", default="auto", help="PRxPC rank grid for --layout grid (auto: 1x2, 2x2, 4x2 ...)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     args = ap.parse_args()
 
@@ -134,10 +145,31 @@ def main():
     if args.lpe:
         ops.set_debug("agg_lpe", args.lpe)
 
+    verbose = bool(os.environ.get("GTA_BENCH_VERBOSE"))
+
+    def note(msg):
+        if verbose:
+            print(f"[rank {rank}] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
+
+    note("building inputs")
     g, x, alpha = make_inputs(args.n, args.e, dev)
     nnz_total = g.nnz
-    rs = world > 1 and args.collective == "reduce_scatter"
-    if world > 1:
+    note("inputs ready")
+    grid = world > 1 and args.layout == "grid"
+    rs = world > 1 and args.collective == "reduce_scatter" and not grid
+    if grid:
+        pr, pc = distributed.grid_shape(world) if args.grid == "auto" else map(int, args.grid.lower().split("x"))
+        if pr * pc != world:
+            raise SystemExit(f"--grid {pr}x{pc} does not match {world} ranks")
+        shard = distributed.GridShard(g, rank, pr, pc)
+        note(f"grid shard {shard.i},{shard.j}: {shard.graph.nnz} edges")
+        groups = distributed.row_groups(pr, pc)
+        note("row groups ready")
+        gl = shard.graph
+        xl = x[shard.c0:shard.c1].contiguous()
+        wl = alpha[shard.edge_ids].contiguous()
+        n_chunks = 1
+    elif world > 1:
         n_chunks = args.row_chunks or 8
         if rs:
             shard = distributed.DistShard(g, rank, world, chunks=n_chunks)
@@ -151,6 +183,10 @@ def main():
         n_chunks = args.row_chunks or 1
 
     def make_chunks(chunk):
+        if grid:  # one launch over the rank's whole tile
+            c = partition.ChunkedRows.__new__(partition.ChunkedRows)
+            c.graph, c.parts = gl, [(0, gl.n_rows, gl, gl.plan(chunk) if chunk else None)]
+            return c
         if not rs:
             return partition.ChunkedRows(gl, n_chunks=n_chunks, chunk=chunk)
         parts = []  # chunk k = padded rows [k*W*mk, (k+1)*W*mk): one part per rank
@@ -173,8 +209,11 @@ def main():
                 impl = "plan"
         if impl == "plan":
             chunked = make_chunks(args.chunk)
-    y = torch.empty(gl.n_rows if rs else g.n_rows, F, device=dev)
+    y = torch.empty(gl.n_rows if (rs or grid) else g.n_rows, F, device=dev)
     y_own = torch.empty(shard.chunks * shard.mk, F, device=dev) if rs else None  # this rank's reduced rows
+    if grid:
+        y_own = torch.empty(shard.m, F, device=dev)
+        my_group = groups[shard.i]
     stream = torch.cuda.current_stream(dev)
 
     def agg_chunk(gg, xx, ww, out, plan):
@@ -183,6 +222,16 @@ def main():
         return ops.aggregate(gg, xx, "src", ww, out=out, plan=plan)
 
     def step():
+        if grid:
+            agg_chunk(gl, xl, wl, y, chunked.parts[0][3])
+            if pc == 1:
+                y_own.copy_(y[:shard.m])
+            elif backend == "nccl":  # RCCL reduce-scatter among the pc ranks of this row group
+                dist.reduce_scatter_tensor(y_own, y, group=my_group)
+            else:  # gloo (1-GPU rehearsal): no reduce-scatter
+                dist.all_reduce(y, group=my_group)
+                y_own.copy_(y[shard.j * shard.m:(shard.j + 1) * shard.m])
+            return
         if not rs:
             partition.distributed_aggregate(chunked, xl, wl, y, aggregate_fn=agg_chunk)
             return
@@ -198,9 +247,11 @@ def main():
         for wk in works:
             wk.wait()
 
+    note(f"impl {impl}, warmup")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    note("timing")
 
     # kernel-only timing (HIP events on the launch stream) for the roofline
     n_evt = min(args.steps, 10)
@@ -236,7 +287,19 @@ def main():
     y_mine = y.clone()
     if world > 1:
         ref = ops.aggregate(g, x, "src", alpha, plan=args.chunk)
-        if rs:  # reassemble Y from every rank's reduced rows
+        if grid:  # reassemble Y from every rank's reduced rows (row groups may differ in m: pad)
+            mmax = max(-(-(shard.rcuts[i + 1] - shard.rcuts[i]) // pc) for i in range(pr))
+            mine = torch.zeros(mmax, F, device=dev)
+            mine[:shard.m] = y_own
+            parts = [torch.empty_like(mine) for _ in range(world)]
+            dist.all_gather(parts, mine)
+            full = torch.empty_like(ref)
+            for q in range(world):
+                rows = shard.owned_rows(q).to(dev)
+                ok = rows >= 0
+                full[rows[ok]] = parts[q][:rows.numel()][ok]
+            y_mine, what = full, f"{pr}x{pc} grid tiles, reduce-scattered per row group (reassembled) vs 1-GPU"
+        elif rs:  # reassemble Y from every rank's reduced rows
             parts = [torch.empty_like(y_own) for _ in range(world)]
             dist.all_gather(parts, y_own)
             full = torch.empty_like(ref)
@@ -283,9 +346,12 @@ def main():
                 "alpha=per-head softmax over in-edges",
         "config": {"workload": "GAT layer-1 aggregate block [3,11,12] (scatter C -> applyedge MUL -> gather ADD)",
                    "graph": "reddit-shaped", "N": args.n, "E": nnz_total, "F": F, "heads": HEADS,
-                   "parallelism": f"edge-partition by source column x{world}" + (
-                       (" + RCCL reduce-scatter per row chunk (each rank ends with its node range's rows)" if rs
-                        else " + RCCL all-reduce per row chunk") if world > 1 else ""),
+                   "parallelism": (f"2-D edge tiles {pr}x{pc} (row groups x source-column groups), RCCL reduce-scatter "
+                                   f"of the partial aggregates inside each row group" if grid else
+                                   f"edge-partition by source column x{world}" + (
+                                       (" + RCCL reduce-scatter per row chunk (each rank ends with its node "
+                                        "range's rows)" if rs else " + RCCL all-reduce per row chunk")
+                                       if world > 1 else "")),
                    "impl": impl, "blocks": args.blocks if impl == "blocked" else None,
                    "plan_chunk": args.chunk if impl == "plan" else None, "row_chunks": n_chunks},
         "achieved_GBps": nnz_total and alg_bytes(g.n_rows, nnz_total) / (ms_per_step / 1e3) / 1e9,

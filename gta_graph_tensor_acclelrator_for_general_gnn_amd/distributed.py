@@ -161,3 +161,58 @@ def run_stream(opgraph, stream, shard, tensors, semantics=None, group=None, plan
         torch.cuda.synchronize(shard.graph.device)
     res = executor.ExecResult(ex.values, outputs, time.perf_counter() - t0, ex.alg_bytes, ex.launches)
     return res, ex
+
+
+def grid_shape(world):
+    """Default 2-D rank grid (row groups pr x column groups pc) for the aggregate benchmark: the
+    edge tiles of the reference's (row tile x column) blocking, code/preprocessing.py:26-38.
+    pc = 2 keeps a real partial-aggregate reduction at every p > 1 while each rank's row count,
+    and with it its per-row work and its share of the exchange, falls as 1/pr."""
+    if world <= 2:
+        return 1, world
+    return world // 2, 2
+
+
+class GridShard:
+    """Rank r = i*pc + j of a pr x pc grid owns the edges whose destination lies in row block i
+    (nnz-balanced row cuts) and whose source lies in column block j (nnz-balanced column cuts),
+    as a CSR over row block i's rows with local column ids.  The pc ranks of row group i sum their
+    partial aggregates with one reduce-scatter: rank (i, j) ends with rows
+    R_i + j*m .. R_i + (j+1)*m of the block (m = ceil(n_i / pc); the CSR is padded to pc*m rows)."""
+
+    def __init__(self, graph, rank, pr, pc):
+        self.pr, self.pc, self.rank = pr, pc, rank
+        self.i, self.j = divmod(rank, pc)
+        dev = graph.device
+        ip = graph.indptr
+        targets = torch.arange(1, pr, device=dev, dtype=torch.float64) * (graph.nnz / pr)
+        inner = torch.searchsorted(ip[1:].to(torch.float64), targets) + 1
+        self.rcuts = [0] + [int(v) for v in inner.cpu()] + [graph.n_rows]
+        self.ccuts = [int(c) for c in partition.column_cuts(graph, pc)]
+        r0, r1 = self.rcuts[self.i], self.rcuts[self.i + 1]
+        c0, c1 = self.ccuts[self.j], self.ccuts[self.j + 1]
+        self.r0, self.r1, self.c0, self.c1 = r0, r1, c0, c1
+        self.m = -(-(r1 - r0) // pc)
+        e0, e1 = int(ip[r0]), int(ip[r1])
+        src = graph.indices[e0:e1]
+        keep = (src >= c0) & (src < c1)
+        deg = ip[r0 + 1:r1 + 1] - ip[r0:r1]
+        rows = torch.repeat_interleave(torch.arange(r1 - r0, device=dev), deg)[keep]
+        counts = torch.bincount(rows, minlength=pc * self.m)
+        indptr = torch.zeros(pc * self.m + 1, dtype=torch.int64, device=dev)
+        indptr[1:] = torch.cumsum(counts, 0)
+        self.graph = Graph(indptr, (src[keep].long() - c0).to(torch.int32), n_cols=c1 - c0)
+        self.edge_ids = torch.nonzero(keep, as_tuple=False).flatten() + e0
+
+    def owned_rows(self, rank):
+        """Global row ids of `rank`'s reduce-scatter output ([m] rows; -1 = padding)."""
+        i, j = divmod(rank, self.pc)
+        r0, r1 = self.rcuts[i], self.rcuts[i + 1]
+        m = -(-(r1 - r0) // self.pc)
+        t = torch.arange(m) + r0 + j * m
+        return torch.where(t < r1, t, torch.full_like(t, -1))
+
+
+def row_groups(pr, pc):
+    """torch.distributed groups of the pc ranks of each row (every rank must create all of them)."""
+    return [dist.new_group(list(range(i * pc, (i + 1) * pc))) for i in range(pr)]
