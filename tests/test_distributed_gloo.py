@@ -137,3 +137,55 @@ def test_chunk_major_shard_layout(world, chunks):
         np.testing.assert_array_equal(own, np.arange(s.c0, s.c1))
         total += len(eids)
     assert total == g.nnz
+
+
+def _grid_worker(rank, world, pr, pc, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, graph as G
+        from oracle import isa_ref
+        g = G.synthetic(600, 12000, seed=8)
+        gen = torch.Generator().manual_seed(3)
+        x = torch.randn(600, 16, generator=gen)
+        w = torch.rand(g.nnz, 4, generator=gen)
+        s = distributed.GridShard(g, rank, pr, pc)
+        groups = distributed.row_groups(pr, pc)
+        sip, six = s.graph.numpy()
+        y = torch.from_numpy(isa_ref.aggregate(sip, six, x[s.c0:s.c1].numpy(), "src",
+                                               w[s.edge_ids].numpy()).astype(np.float32))
+        dist.all_reduce(y, group=groups[s.i])  # the bench's gloo stand-in for the reduce-scatter
+        own = y[s.j * s.m:(s.j + 1) * s.m].contiguous()
+        mmax = max(-(-(s.rcuts[i + 1] - s.rcuts[i]) // pc) for i in range(pr))
+        mine = torch.zeros(mmax, 16)
+        mine[:s.m] = own
+        parts = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(parts, mine)
+        if rank == 0:
+            full = np.zeros((600, 16))
+            for r in range(world):
+                rows = s.owned_rows(r).numpy()
+                ok = rows >= 0
+                full[rows[ok]] = parts[r][:len(rows)][ok].numpy()
+            ip, ix = g.numpy()
+            ref = isa_ref.aggregate(ip, ix, x.numpy(), "src", w.numpy())
+            q.put(float(np.abs(full - ref).max() / np.abs(ref).max()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("pr,pc", [(2, 2), (1, 2), (3, 1)])
+def test_grid_tiles_reduce_scatter_gloo(pr, pc):
+    """bench.py's 2-D layout: row-group partial sums, reassembled from every rank's owned rows,
+    equal the single-device aggregate."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    world = pr * pc
+    procs = [ctx.Process(target=_grid_worker, args=(r, world, pr, pc, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(180)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert q.get(timeout=10) < 1e-5
