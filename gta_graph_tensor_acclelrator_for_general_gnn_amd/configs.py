@@ -7,6 +7,9 @@
                both MLP GEMMs in bf16 on MFMA (fp32 accumulation)
   gat8-reddit  GAT layer 1 on Reddit, 8 heads, F=602: not a BASELINE config; the full layer
                around the metric's aggregate (edge-softmax, GEMMs, aggregate, ELU)
+  sgc/dgn/pna-flickr, gat8-flickr-trans
+               the other genGraphOP networks (and GAT's reordered form) at Flickr scale: not
+               BASELINE configs; they show every network's stream runs at size
 (config 0 -- V2/GAT_Cora.yaml through the V2 lowering -- is legacy.py: create_list restated
 byte-exactly (tests/test_legacy_v2.py) and its stream executed on libgta (test_gpu_executor.py).)
 """
@@ -20,6 +23,10 @@ CONFIGS = {
     "gat8-reddit": dict(network="GAT", dataset="reddit", feature=602, layers=(1,), heads=8),
     "sage-reddit": dict(network="GraphSAGE", dataset="reddit", feature=602, layers=(1,)),
     "gin-products": dict(network="GIN", dataset="products", feature=100, layers=(1,), bf16=True),
+    "gat8-flickr-trans": dict(network="GAT", dataset="flickr", feature=500, layers=(1,), heads=8, reorder=True),
+    "sgc-flickr": dict(network="SGC", dataset="flickr", feature=500, layers=(1,)),
+    "dgn-flickr": dict(network="DGN", dataset="flickr", feature=500, layers=(1,)),
+    "pna-flickr": dict(network="PNA", dataset="flickr", feature=500, layers=(1,)),
 }
 
 
@@ -31,7 +38,8 @@ def build(name, device, seed=0, graph=None):
     meta = None
     for i, L in enumerate(c["layers"]):
         feat = c["feature"] if L == 1 else [0, c["feature"], 128, 64, 16][L]
-        lay = pipeline.Layer(c["network"], L, g, feat, heads=c.get("heads", 16), metadata=meta)
+        lay = pipeline.Layer(c["network"], L, g, feat, reorder=c.get("reorder", False), heads=c.get("heads", 16),
+                             metadata=meta)
         meta = meta or lay.metadata
         layers.append(lay)
     dtype_w = torch.bfloat16 if c.get("bf16") else torch.float32

@@ -709,7 +709,9 @@ struct AttArgs {
   float* sslabs;   // [B, n_rows, H] per-item partial sums of v
 };
 
-template <int VW, int U, bool WEIGHTED, int NT = 0, bool ATT = false>  // NT bit 0: non-temporal index/weight loads, bit 1: slab stores
+template <int VW, int U, bool WEIGHTED, int NT = 0, bool ATT = false, int SFC = -1>
+// NT bit 0: non-temporal index/weight loads, bit 1: slab stores; SFC >= 0: the ATT special function
+// fixed at compile time (-1: att.sf at run time)
 __global__ void __launch_bounds__(kBlock)
 k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items, const float* __restrict__ x,
            int64_t ldx, const float* __restrict__ w, int64_t ldw, int lph, float* __restrict__ slabs,
@@ -752,7 +754,8 @@ k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items,
 #pragma unroll
           for (int q = 0; q < NQ; ++q) xv[u][q] = p[q];
           if (ATT) {
-            wu[u] = sf_apply(att.sf, arow + att.b[static_cast<int64_t>(src) * att.ldb + head]);
+            const float sv = arow + att.b[static_cast<int64_t>(src) * att.ldb + head];
+            wu[u] = (SFC >= 0) ? sf_apply(SFC, sv) : sf_apply(att.sf, sv);
             ssum += wu[u];
           } else if (WEIGHTED) {
             const float* wp = w + (eb + c + s + u) * ldw + head;
@@ -1918,9 +1921,14 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
   const int64_t items = n_rows * B;
   const dim3 g4(static_cast<unsigned>((items + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock))), blk(kBlock);
   const SegItem* it = static_cast<const SegItem*>(v.items);
-  if (vq == 4) k_agg_seg4<4, 4, false, 0, true><<<g4, blk, 0, s>>>(indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, it, att);
-  else if (vq == 8) k_agg_seg4<8, 8, false, 0, true><<<g4, blk, 0, s>>>(indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, it, att);
-  else k_agg_seg4<16, 2, false, 0, true><<<g4, blk, 0, s>>>(indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, it, att);
+  const bool elr = sf == GTA_SF_EXP_LEAKY_RELU;  // GAT's score function, specialised
+#define GTA_ATT(VW_, U_)                                                                                          \
+  if (elr) k_agg_seg4<VW_, U_, false, 0, true, GTA_SF_EXP_LEAKY_RELU><<<g4, blk, 0, s>>>(                        \
+      indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, it, att);                                            \
+  else k_agg_seg4<VW_, U_, false, 0, true><<<g4, blk, 0, s>>>(indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, \
+                                                             it, att)
+  if (vq == 4) { GTA_ATT(4, 4); } else if (vq == 8) { GTA_ATT(8, 8); } else { GTA_ATT(16, 2); }
+#undef GTA_ATT
   GTA_LAUNCHED("k_agg_seg4<att>");
   const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
   const int H = static_cast<int>(heads);

@@ -144,6 +144,13 @@ class Executor:
         #   to fp32 rounding, the gather's own value computed only if something asks for it
         self.mm_first = True
         self.reorder = self._match_mm_first()
+        #   node_mm: an applyedge MM of a scatter runs on the node tensor, (x W)[r(e)] == x[r(e)] W
+        #   (bitwise: the same dot product per row), and stays a virtual scatter of x W
+        #   mm_pushdown: MM(scatter a (+) scatter b) == (a W)[r(e)] (+) (b W)[r'(e)] (DGN op 2 -> 3),
+        #   to fp32 rounding; the [E, F_in] sum is never built
+        self.node_mm = True
+        self.mm_pushdown = True
+        self.pushdown = self._match_pushdown()
 
     # ---------------------------------------------------------------- inputs
     def _ext(self, op, slot):
@@ -286,6 +293,46 @@ class Executor:
             found[G.idx] = M.idx
         return found
 
+    def _match_pushdown(self):
+        """{applyedge ADD of two scatters: its only consumer, a single-input applyedge MM}."""
+        found = {}
+        for op in self.g.ops:
+            if op.type != "applyedge" or op.comp != "ADD" or len(self.g.inputs[op.idx]) != 2:
+                continue
+            srcs = [x.op for x in self.g.inputs[op.idx] if x.kind == "op"]
+            if len(srcs) != 2 or any(self.g.ops[i].type != "scatter" for i in srcs):
+                continue
+            cons = self.consumers[op.idx]
+            if len(cons) != 1:
+                continue
+            m = self.g.ops[cons[0]]
+            if m.type == "applyedge" and m.comp == "MM" and len(self.g.inputs[m.idx]) == 1 \
+                    and self.sem.bin_of(op) == "ADD":
+                found[op.idx] = m.idx
+        return found
+
+    def _node_mm(self, op, v, post_sf=None):
+        """applyedge MM of a virtual scatter: the GEMM runs over the node rows, the result stays virtual."""
+        W = self.tensors[f"w:{op.idx}"]
+        x, W = self._mm_dtypes(v.t, W)
+        if W.shape[0] != x.shape[1]:
+            raise ValueError(f"op {op.idx}: weight rows {W.shape[0]} != feature width {x.shape[1]}")
+        xw = ops.update_mm(x, W, sf=post_sf)
+        self._count(x.shape[0] * (x.shape[1] * x.element_size() + W.shape[1] * 4) + W.numel() * W.element_size())
+        return Scat(xw, v.mode)
+
+    def _pushdown_mm(self, op, add_idx, post_sf=None):
+        """MM(scatter a + scatter b) as (a W)[r_a(e)] + (b W)[r_b(e)]."""
+        if post_sf is not None:
+            return None  # the SF acts on the sum: keep the literal order
+        a, b = [self._source(self.g.ops[add_idx], k) for k in range(2)]
+        if not (isinstance(a, Scat) and isinstance(b, Scat)):
+            return None
+        sa, sb = self._node_mm(op, a), self._node_mm(op, b)
+        out = ops.apply_edge(self.graph, "ADD", None, sa.t, sa.mode, sb.t, sb.mode)
+        self._count(self.graph.nnz * out.shape[1] * 4 * 3)
+        return EdgeT(out)
+
     def _gather_value(self, op):
         v = self._eval_gather(op)
         return NodeT(self.dist.reduce_rows(v.t)) if self.dist is not None else v
@@ -414,9 +461,27 @@ class Executor:
         return b
 
     def _eval_applyedge(self, op, fused=False, post_sf=None):
-        ins = self._inputs(op)
         E = self.graph.nnz
+        pushed = (op.comp == "MM" and self.mm_pushdown and self.g.inputs[op.idx]
+                  and self.g.inputs[op.idx][0].kind == "op"
+                  and self.pushdown.get(self.g.inputs[op.idx][0].op) == op.idx)
+        ins = [None] if pushed else self._inputs(op)
+        if pushed:
+            raw = self.values.get(self.g.inputs[op.idx][0].op)
+            if not (isinstance(raw, Lazy) and raw.v is None):
+                ins = self._inputs(op)
         if op.comp == "MM":
+            src = self.g.inputs[op.idx][0]
+            raw = self.values.get(src.op) if src.kind == "op" else None
+            if self.mm_pushdown and src.kind == "op" and self.pushdown.get(src.op) == op.idx \
+                    and isinstance(raw, Lazy) and raw.v is None:
+                v = self._pushdown_mm(op, src.op, post_sf)
+                if v is not None:
+                    return v
+            if ins[0] is None:
+                ins = self._inputs(op)
+            if self.node_mm and isinstance(ins[0], Scat):
+                return self._node_mm(op, ins[0], post_sf)
             return EdgeT(self._edge_mm(op, ins[0], post_sf))
         if op.comp == "SF":
             a, am, _ = self._edge_operand(ins[0])
@@ -480,6 +545,11 @@ class Executor:
             p = self.g.ops[v.op]
             pins = self._inputs(p)
             if p.comp == "MM":
+                if self.node_mm and isinstance(pins[0], Scat):  # gather(x[r(e)] W) = SpMM of x W
+                    sw = self._node_mm(p, pins[0])
+                    y = self._spmm(sw.t, sw.mode, None)
+                    self._count(E * (4 + sw.t.shape[1] * 4) + n * (8 + sw.t.shape[1] * 4))
+                    return NodeT(y)
                 xe = self._edge_mm(p, pins[0])
                 y = ops.gather_add(self.graph, xe)
                 self._count(E * xe.shape[1] * 4 + n * xe.shape[1] * 4)
@@ -613,6 +683,8 @@ class Executor:
             v = self._eval_softmax(op, self.softmax[op.idx])
             if v is not None:
                 return v
+        if self.mm_pushdown and op.idx in self.pushdown:
+            return Lazy(lambda: self._eval_applyedge(op))  # its MM consumer computes through the sum
         if self.fuse_attention and op.idx in self.attn and fused_into.get(op.idx) is None:
             return Lazy(lambda: self._eval_applyedge(op))  # its gather consumer runs the fused kernel
         if op.type == "applyedge":

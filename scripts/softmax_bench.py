@@ -50,6 +50,16 @@ def main():
             print(key, json.dumps(res[key]), flush=True)
     ops.set_debug("esm_lane", 1)
     ops.set_debug("esm_keep", 4)
+    if H == 8:  # the fused attention aggregate against softmax + alpha-weighted aggregate (same graph)
+        xf = torch.randn(g.n_rows, 128, device=dev)
+        for B in (12, 16, 20):
+            ms = timed(lambda: ops.gat_aggregate_blocked(g, xf, a, b, blocks=B))
+            res[f"att_fused_blk{B}"] = {"ms": ms}
+            print(f"att_fused_blk{B}", json.dumps(res[f"att_fused_blk{B}"]), flush=True)
+        alpha, _ = ops.edge_softmax(g, a, b)
+        ms = timed(lambda: ops.aggregate_blocked(g, xf, alpha, blocks=16))
+        res["alpha_weighted_blk16"] = {"ms": ms}
+        print("alpha_weighted_blk16", json.dumps(res["alpha_weighted_blk16"]), flush=True)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", f"softmax_bench_{dataset}_{H}.json"), "w") as f:
         json.dump({"N": g.n_rows, "E": g.nnz, "H": H, "alg_bytes": alg, "variants": res}, f, indent=1)

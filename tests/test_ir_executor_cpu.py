@@ -197,3 +197,25 @@ def test_chrome_trace_cpu(golden_dir, manifest, monkeypatch, tmp_path):
     assert json.load(open(path)) == ev
     agg = executor.aggregate_trace(ev)
     assert sum(c for c, _, _ in agg.values()) == len(ev)
+
+
+@pytest.mark.parametrize("network", ["DGN", "PNA"])
+def test_node_mm_and_pushdown_cpu(golden_dir, manifest, monkeypatch, network):
+    """Edge GEMMs of scattered node rows run over the nodes ((x W)[r(e)]), and DGN's MM of a sum of
+    two scatters is pushed through the sum: fewer algorithmic bytes, every op still matches the oracle."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    rec = [s for s in _streams(manifest) if s["network"] == network and not s["reorder"]][0]
+    sem = Semantics.for_network(network, False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    gc, ip, ix = _cora_graph(golden_dir)
+    tensors = workloads.make_tensors(og, gc, network, seed=2)
+    ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
+    nbytes = {}
+    for on in (True, False):
+        ex = executor.Executor(og, st, gc, tensors, sem)
+        ex.node_mm = ex.mm_pushdown = on
+        ex.run()
+        nbytes[on] = ex.alg_bytes
+        compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
+    assert nbytes[True] < nbytes[False]
