@@ -1383,7 +1383,10 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
   __shared__ __attribute__((aligned(16))) WT Bt[BN][KP];
   const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
   const int g = lane >> 4, r16 = lane & 15;
-  const int n0 = blockIdx.y * BN;
+  // column blocks of one row group sit in adjacent blocks (blockIdx.x = group * ncb + cb; the grid
+  // is a multiple of ncb), so the second column block's x rows are L2 hits
+  const int ncb = (N + BN - 1) / BN;
+  const int n0 = static_cast<int>(blockIdx.x % ncb) * BN;
   constexpr int AV = BF ? 8 : 4;  // A values per lane per fragment
   const bool avec = (ldx % AV == 0) && aligned(x, sizeof(TA) * AV);
   const bool wvec = (ldwt % WV == 0) && aligned(wt, 16);
@@ -1418,7 +1421,7 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
     stage(0);
     __syncthreads();
   }
-  for (int64_t grp = blockIdx.x; grp < n_groups; grp += gridDim.x) {
+  for (int64_t grp = blockIdx.x / ncb; grp < n_groups; grp += gridDim.x / ncb) {
     const int64_t mw = grp * 128 + wv * 32;
     const TA* ap[2];
     bool aok[2];
@@ -2100,9 +2103,9 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   const int64_t groups = (M + 127) / 128;
   const int64_t per_cu = g_mm_blocks_per_cu > 0 ? g_mm_blocks_per_cu : 8;
   const int kc = (dtype == GTA_F32) ? (nt >= 8 ? 64 : 128) : (nt >= 8 ? 128 : 256);  // k_mm_rows KC
-  const int64_t cap = (K <= kc) ? 256 * per_cu : groups;  // W staged once: persistent row-group loop
-  const dim3 gr(static_cast<unsigned>(std::min<int64_t>(groups, cap)),
-                static_cast<unsigned>((N + 16 * nt - 1) / (16 * nt)));
+  const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
+  const int64_t cap = (K <= kc) ? std::max<int64_t>(1, 256 * per_cu / ncb) : groups;  // W staged once: persistent
+  const dim3 gr(static_cast<unsigned>(std::min<int64_t>(groups, cap) * ncb));
 #define GTA_MMR(TA_, WT_, NT_)                                                                                \
   k_mm_rows<TA_, WT_, NT_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const TA_*>(x), ldx, row_idx, M,  \
                                                                static_cast<int>(K), static_cast<const WT_*>(wt), \

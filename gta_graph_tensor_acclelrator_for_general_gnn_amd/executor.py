@@ -150,6 +150,10 @@ class Executor:
         #   to fp32 rounding; the [E, F_in] sum is never built
         self.node_mm = True
         self.mm_pushdown = True
+        #   sibling_mm: applynode MMs that multiply the same node tensor run as ONE GEMM over the
+        #   concatenated weights (x read once; e.g. GraphSAGE's x W3 and x W4, GAT's scores W1, W2)
+        self.sibling_mm = True
+        self._wcat = {}
         self.pushdown = self._match_pushdown()
 
     # ---------------------------------------------------------------- inputs
@@ -333,6 +337,63 @@ class Executor:
         self._count(self.graph.nnz * out.shape[1] * 4 * 3)
         return EdgeT(out)
 
+    def _pending_siblings(self, x, main_idx, W):
+        """Unevaluated applynode MM ops whose input is the node tensor x itself, with weights of
+        W's dtype and K and no SF epilogue of their own."""
+        if not self.sibling_mm:
+            return []
+        sib = []
+        for op in self.g.ops:
+            if op.idx == main_idx or op.idx in self.values or op.type != "applynode" or op.comp != "MM":
+                continue
+            ins = self.g.inputs[op.idx]
+            if len(ins) != 1:
+                continue
+            src = ins[0]
+            if src.kind == "op":
+                v = self.values.get(src.op)
+                if not (isinstance(v, NodeT) and v.t is x):
+                    continue
+            elif src.kind == "x":
+                if self._ext(op, 0) is not None or self.tensors.get("x") is not x:
+                    continue
+            else:
+                continue
+            Ws = self.tensors.get(f"w:{op.idx}")
+            if Ws is None or Ws.dtype != W.dtype or Ws.shape[0] != W.shape[0] or self._sf_child_any(op):
+                continue
+            sib.append(op)
+        return sib
+
+    def _sf_child_any(self, op):
+        cons = self.consumers[op.idx]
+        return self.fuse_sf and len(cons) == 1 and self.g.ops[cons[0]].comp == "SF" \
+            and self.g.ops[cons[0]].type == op.type
+
+    def _node_gemm(self, x, main_idx, W, post_sf=None):
+        """x W for op main_idx; sibling MMs of the same x ride along in the same GEMM (their
+        values are column views of the output).  Returns the main op's [rows, N] result."""
+        sibs = [] if post_sf is not None else self._pending_siblings(x, main_idx, W)
+        x2, W2 = self._mm_dtypes(x, W)
+        if not sibs:
+            out = ops.update_mm(x2, W2, sf=post_sf)
+            self._count(x.shape[0] * (x.shape[1] * x.element_size() + W.shape[1] * 4) + W.numel() * W.element_size())
+            return out
+        key = (main_idx,) + tuple(o.idx for o in sibs)
+        Wc = self._wcat.get(key)
+        if Wc is None:
+            Wc = torch.cat([W] + [self.tensors[f"w:{o.idx}"] for o in sibs], dim=1).contiguous()
+            self._wcat[key] = Wc
+        x2, Wc2 = self._mm_dtypes(x, Wc)
+        out = ops.update_mm(x2, Wc2)
+        self._count(x.shape[0] * (x.shape[1] * x.element_size() + Wc.shape[1] * 4) + Wc.numel() * Wc.element_size())
+        off = W.shape[1]
+        for o in sibs:
+            n_o = self.tensors[f"w:{o.idx}"].shape[1]
+            self.values[o.idx] = NodeT(out[:, off:off + n_o])
+            off += n_o
+        return out[:, :W.shape[1]]
+
     def _gather_value(self, op):
         v = self._eval_gather(op)
         return NodeT(self.dist.reduce_rows(v.t)) if self.dist is not None else v
@@ -367,9 +428,7 @@ class Executor:
         W = self.tensors[f"w:{M.idx}"]
         if W.shape[0] != x.shape[1]:
             return None
-        x, W = self._mm_dtypes(x, W)
-        xw = ops.update_mm(x, W)
-        self._count(x.shape[0] * (x.shape[1] * x.element_size() + W.shape[1] * 4) + W.numel() * W.element_size())
+        xw = self._node_gemm(x, M.idx, W).contiguous()
         n, E, F = self.graph.n_rows, self.graph.nnz, xw.shape[1]
         y = self._spmm(xw, "src", w)
         self._count(E * (4 + (4 if w is not None else 0) + 4 * F) + n * (8 + 4 * F))
@@ -624,10 +683,7 @@ class Executor:
         if op.comp == "MM":
             W = self.tensors[f"w:{op.idx}"]
             x = self._node(ins[0])
-            x, W = self._mm_dtypes(x, W)
-            y = ops.update_mm(x, W, sf=post_sf)
-            self._count(n * (x.shape[1] * x.element_size() + W.shape[1] * 4) + W.numel() * W.element_size())
-            return NodeT(y)
+            return NodeT(self._node_gemm(x, op.idx, W, post_sf))
         if op.comp == "SF":
             a = self._node(ins[0])
             y = ops.apply_node(None, self.sem.sf_of(op), a)
