@@ -169,10 +169,11 @@ def comp_types(op_records):
 
 
 def typed_records(op_records):
+    """Op records with COMP_TYPE: kept where the graph has it (genGraphOP's), inferred otherwise."""
     recs = []
     for r, c in zip(op_records, comp_types(op_records)):
         r = dict(r)
-        r["COMP_TYPE"] = c
+        r.setdefault("COMP_TYPE", c)
         recs.append(r)
     return recs
 
@@ -207,8 +208,10 @@ SEMANTICS = {  # the build's choices for the V2 graphs (cf. semantics.py)
 }
 
 
-def execute_v2(op_records, stream_records, graph, tensors, network="GAT", op_list=None, plan_chunk=512):
-    """Run a V2 stream (lower_v2 output) on the HIP executor -> (ExecResult, Executor)."""
-    sem = SEMANTICS.get(network, Semantics())
+def execute_v2(op_records, stream_records, graph, tensors, network="GAT", op_list=None, plan_chunk=512,
+               reorder=False):
+    """Run a V2 stream (lower_v2 output) on the HIP executor -> (ExecResult, Executor).  network names
+    the V2 graphs ("GAT" = V2/GAT_Cora.yaml, "simpletest") or any genGraphOP network."""
+    sem = SEMANTICS.get(network) or Semantics.for_network(network, reorder)
     g = ir.OpGraph(typed_records(op_records), sem.inputs)
     return executor.run_stream(g, LegacyStream(stream_records, op_list), graph, tensors, sem, plan_chunk)

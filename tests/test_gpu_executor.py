@@ -187,3 +187,23 @@ def test_execute_chrome_trace_on_gpu(golden_dir, manifest, cora, dev, tmp_path, 
     ev = json.load(open("trace/chrome_timeline.json"))
     assert ev == res.trace and len(ev) >= 1
     assert all(e["ph"] == "X" and e["dur"] >= 0 for e in ev) and sum(e["dur"] for e in ev) > 0
+
+
+def test_gcn_cora_2layer_fused_template_on_gpu(golden_dir, cora, dev):
+    """BASELINE config 2 through the fused_template (V2 create_list) lowering, both layers chained on
+    libgta, vs the fp64 oracle."""
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import frontend, legacy
+    ip, ix = cora
+    gd, gc = G.from_numpy(ip, ix, device=dev), G.from_numpy(ip, ix)
+    x_c = None
+    for layer, fin in ((1, 1433), (2, 128)):
+        ops_ = frontend.gen_ops("GCN", layer, 2708, 10556, 1433, False, 16)
+        recs = legacy.lower_v2("cora", ops_, [[o["OP_NO"]] for o in ops_], [64] * len(ops_), 2708)
+        og = ir.OpGraph(legacy.typed_records(ops_))
+        tc = workloads.make_tensors(og, gc, "GCN", seed=layer)
+        if x_c is not None:
+            tc["x"] = x_c
+        res, ex = legacy.execute_v2(ops_, recs, gd, {k: v.to(dev) for k, v in tc.items()}, "GCN")
+        ref = execute_ref(og, Semantics.for_network("GCN"), ip, ix, {k: v.double().numpy() for k, v in tc.items()})
+        compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)), rtol=2e-4)
+        x_c = res.outputs[sorted(res.outputs)[-1]].cpu()

@@ -80,3 +80,20 @@ def test_execute_v2_stream_cpu(golden_dir, monkeypatch, k):
     monkeypatch.setattr(executor, "ops", fake_ops)
     res = run_v2(golden_dir, _v2(golden_dir)[k])
     assert res.launches > 0 and all(torch.isfinite(t).all() for t in res.outputs.values())
+
+
+@pytest.mark.parametrize("layer", [1, 2])
+def test_gcn_cora_through_fused_template_cpu(golden_dir, monkeypatch, layer):
+    """BASELINE config 2's 'fused_template' route: genGraphOP's GCN layer lowered by the V2 create_list
+    (one block per op) and executed, equal to the op-by-op oracle."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    ops_ = frontend.gen_ops("GCN", layer, 2708, 10556, 1433, False, 16)
+    recs = legacy.lower_v2("cora", ops_, [[o["OP_NO"]] for o in ops_], [64] * len(ops_), 2708)
+    z = __import__("numpy").load(os.path.join(golden_dir, "cora_graph.npz"))
+    gc = G.from_numpy(z["indptr"], z["indices"])
+    og = ir.OpGraph(legacy.typed_records(ops_))
+    tensors = workloads.make_tensors(og, gc, "GCN", seed=layer)
+    res, ex = legacy.execute_v2(ops_, recs, gc, tensors, "GCN")
+    ref = execute_ref(og, legacy.Semantics.for_network("GCN"), z["indptr"], z["indices"],
+                      {k: v.double().numpy() for k, v in tensors.items()})
+    compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)), rtol=1e-4)
