@@ -1019,6 +1019,92 @@ k_apply_edge(int bin, int sf, const int64_t* __restrict__ indptr, const int32_t*
   }
 }
 
+// Row-sweep forms of K3 (the generic kernel above divides per element and re-reads
+// the index per element).  A wave owns a destination row and walks its edges:
+//  * k_apply_edge_cols: lanes cover the output columns, VW per lane (float4/float2
+//    when rows are aligned and any head broadcast keeps VW columns in one head),
+//    4 edges unrolled so their row gathers are in flight together;
+//  * k_apply_edge_pack: Fo <= 32 (a power of two): 64/Fo edges per wave instruction,
+//    lane = (edge slot, column).
+template <int VW>
+__device__ __forceinline__ void ld_vec(const float* p, float* v, int ga, int c) {  // VW output columns from c
+  if (ga == 1) {
+    if (VW == 4) { const float4 t = *reinterpret_cast<const float4*>(p + c); v[0] = t.x; v[1] = t.y; v[2] = t.z; v[3] = t.w; }
+    else if (VW == 2) { const float2 t = *reinterpret_cast<const float2*>(p + c); v[0] = t.x; v[1] = t.y; }
+    else v[0] = p[c];
+  } else {  // VW consecutive columns share one head (ga % VW == 0)
+    const float t = p[c / ga];
+#pragma unroll
+    for (int q = 0; q < VW; ++q) v[q] = t;
+  }
+}
+
+template <int VW>
+__global__ void __launch_bounds__(kBlock)
+k_apply_edge_cols(int bin, int sf, const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+                  int64_t n_rows, const float* __restrict__ a, int a_mode, int64_t lda, int ga,
+                  const float* __restrict__ b, int b_mode, int64_t ldb, int gb, float* __restrict__ out,
+                  int64_t ldo, int Fo) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  const int64_t eb = indptr[row], ee = indptr[row + 1];
+  for (int c = lane * VW; c < Fo; c += kWave * VW) {
+    int64_t e = eb;
+    for (; e + 4 <= ee; e += 4) {
+      float va[4][VW], vb[4][VW];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t ra = edge_row(a_mode, e + u, row, indices);
+        ld_vec<VW>(a + ra * lda, va[u], ga, c);
+        if (b != nullptr) {
+          const int64_t rb = (ldb == 0) ? 0 : edge_row(b_mode, e + u, row, indices);
+          ld_vec<VW>(b + rb * ldb, vb[u], gb, c);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        float o[VW];
+#pragma unroll
+        for (int q = 0; q < VW; ++q) o[q] = sf_apply(sf, b != nullptr ? bin_apply(bin, va[u][q], vb[u][q]) : va[u][q]);
+        float* op = out + (e + u) * ldo + c;
+        if (VW == 4) *reinterpret_cast<float4*>(op) = make_float4(o[0], o[1], o[2], o[3]);
+        else if (VW == 2) *reinterpret_cast<float2*>(op) = make_float2(o[0], o[1]);
+        else op[0] = o[0];
+      }
+    }
+    for (; e < ee; ++e) {
+      float va[VW], vb[VW];
+      ld_vec<VW>(a + edge_row(a_mode, e, row, indices) * lda, va, ga, c);
+      if (b != nullptr) ld_vec<VW>(b + ((ldb == 0) ? 0 : edge_row(b_mode, e, row, indices)) * ldb, vb, gb, c);
+      float* op = out + e * ldo + c;
+#pragma unroll
+      for (int q = 0; q < VW; ++q) op[q] = sf_apply(sf, b != nullptr ? bin_apply(bin, va[q], vb[q]) : va[q]);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_apply_edge_pack(int bin, int sf, const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
+                  int64_t n_rows, const float* __restrict__ a, int a_mode, int64_t lda, int ga,
+                  const float* __restrict__ b, int b_mode, int64_t ldb, int gb, float* __restrict__ out,
+                  int64_t ldo, int Fo) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  const int64_t eb = indptr[row], ee = indptr[row + 1];
+  const int epi = kWave / Fo, k = lane / Fo, c = lane - k * Fo;
+  const int ca = c / ga, cb = c / gb;
+  for (int64_t e0 = eb; e0 < ee; e0 += epi) {
+    const int64_t e = e0 + k;
+    if (e < ee) {
+      float v = a[edge_row(a_mode, e, row, indices) * lda + ca];
+      if (b != nullptr) v = bin_apply(bin, v, b[((ldb == 0) ? 0 : edge_row(b_mode, e, row, indices)) * ldb + cb]);
+      out[e * ldo + c] = sf_apply(sf, v);
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kBlock)
 k_apply_node(int bin, int sf, int64_t n, const float* __restrict__ a, int64_t lda, int Fa,
              const float* __restrict__ b, int64_t ldb, int Fb, float* __restrict__ out, int64_t ldo, int Fo) {
@@ -1602,6 +1688,7 @@ int g_seg_quarter = 1;     // quarter-wave (4 items per wave) form of the blocke
 int g_seg_nt = 0;          // non-temporal bits of the quarter-wave form (F = 128, U = 8)
 int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
 int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
+int g_apply_edge_form = 1;  // 1: row-sweep K3 kernels (cols / pack); 0: the generic per-element kernel
 int g_esm_lane = 1;        // edge-per-lane edge-softmax when H in {4,8,16} and rows are 16-B aligned
 int g_esm_keep = 4;        // chunks of 64 edges held in VGPRs by the edge-per-lane form (2 or 4)
 
@@ -1627,6 +1714,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "seg_u") { g_seg_u = static_cast<int>(value); return 0; }
   if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
   if (k == "mm_blocks_per_cu") { g_mm_blocks_per_cu = value; return 0; }
+  if (k == "apply_edge_form") { g_apply_edge_form = static_cast<int>(value); return 0; }
   if (k == "esm_lane") { g_esm_lane = static_cast<int>(value); return 0; }
   if (k == "esm_keep") { g_esm_keep = static_cast<int>(value); return 0; }
   return fail(GTA_ERR_ARG, "gta_debug_set: unknown key " + k);
@@ -2003,9 +2091,31 @@ int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indice
   if (check_bcast(Fa, Fb, b != nullptr, &Fo)) return fail(GTA_ERR_ARG, "apply_edge: widths must divide");
   if (n_rows == 0 || nnz == 0) return GTA_OK;
   const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
-  k_apply_edge<<<grid, dim3(kBlock), 0, S(stream)>>>(bin, sf, indptr, indices, n_rows, a, a_mode, lda,
-                                                     static_cast<int>(Fa), b, b_mode, ldb, static_cast<int>(Fb), out,
-                                                     ldo, static_cast<int>(Fo));
+  const int fo = static_cast<int>(Fo), ga = static_cast<int>(Fo / Fa), gb = b ? static_cast<int>(Fo / Fb) : 1;
+  if (g_apply_edge_form == 0) {
+    k_apply_edge<<<grid, dim3(kBlock), 0, S(stream)>>>(bin, sf, indptr, indices, n_rows, a, a_mode, lda,
+                                                       static_cast<int>(Fa), b, b_mode, ldb, static_cast<int>(Fb),
+                                                       out, ldo, fo);
+  } else if (fo <= 32 && (fo & (fo - 1)) == 0) {
+    k_apply_edge_pack<<<grid, dim3(kBlock), 0, S(stream)>>>(bin, sf, indptr, indices, n_rows, a, a_mode, lda, ga,
+                                                            b, b_mode, ldb, gb, out, ldo, fo);
+  } else {
+    auto vec_ok = [&](int vw) {
+      if (fo % vw || ldo % vw || !aligned(out, 4 * vw)) return false;
+      if (ga == 1 ? (lda % vw || !aligned(a, 4 * vw)) : (ga % vw != 0)) return false;
+      if (b && (gb == 1 ? (ldb % vw || !aligned(b, 4 * vw)) : (gb % vw != 0))) return false;
+      return true;
+    };
+    if (vec_ok(4) && fo >= 4 * kWave)
+      k_apply_edge_cols<4><<<grid, dim3(kBlock), 0, S(stream)>>>(bin, sf, indptr, indices, n_rows, a, a_mode, lda, ga,
+                                                                 b, b_mode, ldb, gb, out, ldo, fo);
+    else if (vec_ok(2) && fo >= 2 * kWave)
+      k_apply_edge_cols<2><<<grid, dim3(kBlock), 0, S(stream)>>>(bin, sf, indptr, indices, n_rows, a, a_mode, lda, ga,
+                                                                 b, b_mode, ldb, gb, out, ldo, fo);
+    else
+      k_apply_edge_cols<1><<<grid, dim3(kBlock), 0, S(stream)>>>(bin, sf, indptr, indices, n_rows, a, a_mode, lda, ga,
+                                                                 b, b_mode, ldb, gb, out, ldo, fo);
+  }
   GTA_LAUNCHED("k_apply_edge");
   return GTA_OK;
 }

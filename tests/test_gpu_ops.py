@@ -477,3 +477,26 @@ def test_degenerate_graphs_every_op(dev, case):
     if n:
         counts = ops.tile_nnz(g, 16).cpu().numpy()
         assert np.array_equal(counts, isa_ref.tile_nnz(ip, ix, ncols, 16))
+
+
+@pytest.mark.parametrize("Fa,Fb", [(128, 128), (128, 8), (8, 128), (602, 602), (100, 4), (16, 16), (8, 1), (1, 1),
+                                   (256, 16), (48, 48), (3, 3)])
+@pytest.mark.parametrize("modes", [("src", "dst"), ("edge", "src"), ("dst", "edge"), ("edge", "row")])
+def test_apply_edge_forms_agree(dev, Fa, Fb, modes):
+    """Row-sweep K3 kernels (vector columns, packed small widths) == the generic per-element kernel,
+    bitwise (same arithmetic per element), incl. head broadcast, odd widths and a broadcast b row."""
+    g, ip, ix = _graph(300, 6000, seed=Fa + Fb, empty_rows=4, heavy_row=900, dev=dev)
+    rng = np.random.default_rng(Fa * 7 + Fb)
+    rows = {"src": g.n_rows, "dst": g.n_rows, "edge": g.nnz, "row": 1}
+    a = torch.from_numpy(rng.standard_normal((rows[modes[0]], Fa)).astype(np.float32)).to(dev)
+    b = torch.from_numpy(rng.standard_normal((rows[modes[1]], Fb)).astype(np.float32)).to(dev)
+    bmode = "edge" if modes[1] == "row" else modes[1]
+    outs = []
+    for form in (0, 1):
+        ops.set_debug("apply_edge_form", form)
+        try:
+            outs.append(ops.apply_edge(g, "MUL", "LEAKY_RELU", a, modes[0], b, bmode,
+                                       b_broadcast_row=modes[1] == "row"))
+        finally:
+            ops.set_debug("apply_edge_form", 1)
+    assert torch.equal(outs[0], outs[1])
