@@ -224,7 +224,7 @@ class Executor:
 
     def _materialize_deferred(self, d):
         op = self.g.ops[d.op]
-        v = self._eval_applyedge(op, fused=False)
+        v = self._eval_applyedge(op)
         self.values[d.op] = v
         return v
 
@@ -240,8 +240,8 @@ class Executor:
           trans    (ops 6,8,9):      V and G from one launch (V's other consumer aggregates it)"""
         ops_, ins, cons = self.g.ops, self.g.inputs, self.consumers
 
-        def only(i):
-            return len(cons[i]) == 1 and cons[i][0]
+        def only(i):  # the single consumer of op i, or None
+            return cons[i][0] if len(cons[i]) == 1 else None
 
         found = {}
         for A in ops_:
@@ -254,7 +254,7 @@ class Executor:
             if orders != ["C", "R"] or self.sem.bin_of(A) != "ADD":
                 continue
             v = only(A.idx)
-            if v is False or ops_[v].type != "applyedge" or ops_[v].comp != "SF":
+            if v is None or ops_[v].type != "applyedge" or ops_[v].comp != "SF":
                 continue
             gs = [c for c in cons[v] if ops_[c].type == "gather" and ops_[c].order == "R"]
             if len(gs) != 1:
@@ -262,9 +262,9 @@ class Executor:
             G = gs[0]
             pat = {"A": A.idx, "V": v, "G": G, "D": None}
             S = only(G)
-            if S is not False and ops_[S].type == "scatter" and ops_[S].order == "R":
+            if S is not None and ops_[S].type == "scatter" and ops_[S].order == "R":
                 D = only(S)
-                if D is not False and set(cons[v]) == {G, D} and ops_[D].type == "applyedge":
+                if D is not None and set(cons[v]) == {G, D} and ops_[D].type == "applyedge":
                     dins = [x.op if x.kind == "op" else None for x in ins[D]]
                     b = self.sem.bin_of(ops_[D])
                     if (b == "DIV" and dins == [v, S]) or (b == "RDIV" and dins == [S, v]):
@@ -516,10 +516,9 @@ class Executor:
 
     # ---------------------------------------------------------------- eval
     def _binary(self, op):
-        b = self.sem.bin_of(op)
-        return b
+        return self.sem.bin_of(op)
 
-    def _eval_applyedge(self, op, fused=False, post_sf=None):
+    def _eval_applyedge(self, op, post_sf=None):
         E = self.graph.nnz
         pushed = (op.comp == "MM" and self.mm_pushdown and self.g.inputs[op.idx]
                   and self.g.inputs[op.idx][0].kind == "op"
@@ -562,7 +561,7 @@ class Executor:
             if bin_ in ("ADD", "MUL"):
                 a, am, b, bm, arow, brow = b, bm, a, am, False, True
             else:
-                a = self._to_edge_tensor(("row", a)) if False else a.expand(E, a.shape[1]).contiguous()
+                a = a.expand(E, a.shape[1]).contiguous()  # a broadcast row on the left of DIV/SUB
                 am, arow = "edge", False
         out = ops.apply_edge(self.graph, bin_, post_sf, a, am, b, bm, b_broadcast_row=brow)
         self._count(E * out.shape[1] * 4 * 3)
