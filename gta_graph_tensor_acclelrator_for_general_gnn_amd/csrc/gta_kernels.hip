@@ -1456,8 +1456,8 @@ k_mm_bf16(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
 //          contracts k = k0+4g+j (B read with the same k map).
 //   bf16:  v_mfma_f32_16x16x32_bf16, lane (r, g) holds x[r][k0+8g .. +7] (fp32 X is
 //          rounded to bf16 in registers, round to nearest even).
-template <typename TA, typename WT, int NT>
-__global__ void __launch_bounds__(kBlock)
+template <typename TA, typename WT, int NT, bool PF = false>  // PF: prefetch the next A fragment
+__global__ void __launch_bounds__(kBlock, PF ? 4 : 1)
 k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const WT* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo) {
   constexpr bool BF = sizeof(WT) == 2;
@@ -1563,10 +1563,20 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
           }
         }
       };
+      float avn[2][AV];
+      if (PF) load_a(0, avn);
 #pragma unroll 1
       for (int ks = 0; ks < kend; ks += KS) {
         float av[2][AV];
-        load_a(ks, av);
+        if (PF) {
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int q = 0; q < AV; ++q) av[i][q] = avn[i][q];
+          if (ks + KS < kend) load_a(ks + KS, avn);
+        } else {
+          load_a(ks, av);
+        }
         if constexpr (BF) {
           bf16x8 a8[2];
 #pragma unroll
@@ -1687,6 +1697,7 @@ int64_t g_seg_waves = 0;  // persistent waves of the column-blocked kernel (0 = 
 int g_seg_quarter = 1;     // quarter-wave (4 items per wave) form of the blocked aggregate
 int g_seg_nt = 0;          // non-temporal bits of the quarter-wave form (F = 128, U = 8)
 int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
+int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
 int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
 int g_apply_edge_form = 1;  // 1: row-sweep K3 kernels (cols / pack); 0: the generic per-element kernel
 int g_esm_lane = 1;        // edge-per-lane edge-softmax when H in {4,8,16} and rows are 16-B aligned
@@ -1713,6 +1724,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "seg_nt") { g_seg_nt = static_cast<int>(value); return 0; }
   if (k == "seg_u") { g_seg_u = static_cast<int>(value); return 0; }
   if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
+  if (k == "mm_prefetch") { g_mm_prefetch = static_cast<int>(value); return 0; }
   if (k == "mm_blocks_per_cu") { g_mm_blocks_per_cu = value; return 0; }
   if (k == "apply_edge_form") { g_apply_edge_form = static_cast<int>(value); return 0; }
   if (k == "esm_lane") { g_esm_lane = static_cast<int>(value); return 0; }
@@ -2216,10 +2228,16 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
   const int64_t cap = (K <= kc) ? std::max<int64_t>(1, 256 * per_cu / ncb) : groups;  // W staged once: persistent
   const dim3 gr(static_cast<unsigned>(std::min<int64_t>(groups, cap) * ncb));
+  // prefetch the next A fragment: measured 1.2x on fp32 (K = 602) and bf16 K = 128, slower with a
+  // K tail on the mixed path (profiles/r01_mm_bench.json); g_mm_prefetch 2 = always, 0 = never
+  const bool pf = g_mm_prefetch == 2 || (g_mm_prefetch == 1 && (dtype == GTA_F32 || K % 32 == 0));
 #define GTA_MMR(TA_, WT_, NT_)                                                                                \
-  k_mm_rows<TA_, WT_, NT_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const TA_*>(x), ldx, row_idx, M,  \
-                                                               static_cast<int>(K), static_cast<const WT_*>(wt), \
-                                                               ldwt, static_cast<int>(N), sf, out, ldo)
+  if (pf) k_mm_rows<TA_, WT_, NT_, true><<<gr, dim3(kBlock), 0, S(stream)>>>(                        \
+      static_cast<const TA_*>(x), ldx, row_idx, M, static_cast<int>(K), static_cast<const WT_*>(wt), ldwt,        \
+      static_cast<int>(N), sf, out, ldo);                                                                         \
+  else k_mm_rows<TA_, WT_, NT_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const TA_*>(x), ldx, row_idx, M, \
+                                                                    static_cast<int>(K), static_cast<const WT_*>(wt), \
+                                                                    ldwt, static_cast<int>(N), sf, out, ldo)
 #define GTA_MMR_NT(TA_, WT_) \
   if (nt == 1) GTA_MMR(TA_, WT_, 1); else if (nt == 2) GTA_MMR(TA_, WT_, 2); else if (nt == 4) GTA_MMR(TA_, WT_, 4); else GTA_MMR(TA_, WT_, 8)
   if (dtype == GTA_F32) { GTA_MMR_NT(float, float); }

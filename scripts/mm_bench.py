@@ -48,6 +48,11 @@ def main():
                     ms = timed(lambda: ops.update_mm(x, w))
                     res[f"{name}:form1:bpc{bpc}"] = {"ms": ms}
                 ops.set_debug("mm_blocks_per_cu", 0)
+                for pf in (0, 2):
+                    ops.set_debug("mm_prefetch", pf)
+                    ms = timed(lambda: ops.update_mm(x, w))
+                    res[f"{name}:form1:bpcpf{pf}"] = {"ms": ms}
+                ops.set_debug("mm_prefetch", 1)
             ms = timed(lambda: ops.update_mm(x, w))
             outs[form] = ops.update_mm(x, w)
             nbytes = M * K * x.element_size() + M * N * 4 + K * N * w.element_size()
