@@ -500,3 +500,27 @@ def test_apply_edge_forms_agree(dev, Fa, Fb, modes):
         finally:
             ops.set_debug("apply_edge_form", 1)
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("pf", [0, 2])
+@pytest.mark.parametrize("M,K,N,dt", [(40000, 602, 128, "f32"), (40000, 100, 128, "mixed"), (40000, 128, 64, "bf16"),
+                                      (33000, 37, 200, "f32")])
+def test_update_mm_prefetch_forms(dev, pf, M, K, N, dt):
+    """The row GEMM with and without A-fragment prefetch: same result to the fp32 bound."""
+    rng = np.random.default_rng(K + N + pf)
+    x = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32))
+    w = torch.from_numpy((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32))
+    if dt == "bf16":
+        x, w = x.to(torch.bfloat16), w.to(torch.bfloat16)
+    elif dt == "mixed":
+        w = w.to(torch.bfloat16)
+    ops.set_debug("mm_prefetch", pf)
+    try:
+        out = ops.update_mm(x.to(dev), w.to(dev))
+    finally:
+        ops.set_debug("mm_prefetch", 1)
+    xr = x.float().numpy().astype(np.float64)
+    if dt != "f32":
+        xr = torch.from_numpy(xr).to(torch.bfloat16).double().numpy()
+    wf = w.float().numpy().astype(np.float64)
+    _check(out, xr @ wf, np.abs(xr) @ np.abs(wf), f"update_mm pf={pf} {dt}")
