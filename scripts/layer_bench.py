@@ -11,7 +11,7 @@ sys.path.insert(0, ROOT)
 from gta_graph_tensor_acclelrator_for_general_gnn_amd import configs, executor  # noqa: E402
 
 
-def main(names=None, reps=5, trace=False):
+def main(names=None, reps=5, trace=False, graphed=False):
     dev = torch.device("cuda:0")
     out = {}
     for name in (names or list(configs.CONFIGS)):
@@ -32,6 +32,25 @@ def main(names=None, reps=5, trace=False):
             if r:
                 times.append(time.perf_counter() - t1)
         ms = 1e3 * sorted(times)[len(times) // 2]
+        graphed_ms = None
+        if graphed:  # the same forward replayed as HIP graphs (one per layer)
+            runs, prev = [], None
+            for lay, t in zip(layers, tensors):
+                if prev is not None:
+                    t["x"] = prev  # layer k reads layer k-1's (static) graph output
+                runs.append(executor.GraphedRun(lay.opgraph, lay.stream, g, t, lay.sem))
+                prev = runs[-1].outputs[sorted(runs[-1].outputs)[-1]]
+            gt = []
+            for r in range(reps + 1):
+                torch.cuda.synchronize()
+                t1 = time.perf_counter()
+                for gr in runs:
+                    gr.replay()
+                torch.cuda.synchronize()
+                if r:
+                    gt.append(time.perf_counter() - t1)
+            graphed_ms = 1e3 * sorted(gt)[len(gt) // 2]
+            del runs
         if trace:  # one more forward with per-op HIP-event tracing (Chrome JSON)
             x = None
             events = []
@@ -44,7 +63,7 @@ def main(names=None, reps=5, trace=False):
             executor.save_chrome_trace(events, os.path.join(ROOT, "gpurun_out", f"trace_{name}.json"))
         out[name] = {"N": g.n_rows, "E": g.nnz, "layers": [l.layer for l in layers],
                      "op_array": [l.op_array for l in layers], "tile_size_list": [l.tile_size_list for l in layers],
-                     "ms_per_forward": ms, "edges_per_s": g.nnz * len(layers) / (ms / 1e3), "build_s": build_s}
+                     "ms_per_forward": ms, "ms_per_forward_hipgraph": graphed_ms, "edges_per_s": g.nnz * len(layers) / (ms / 1e3), "build_s": build_s}
         print(name, json.dumps(out[name]), flush=True)
         del layers, g, tensors
         torch.cuda.empty_cache()
@@ -54,5 +73,5 @@ def main(names=None, reps=5, trace=False):
 
 
 if __name__ == "__main__":
-    argv = [a for a in sys.argv[1:] if a != "--trace"]
-    main(argv or None, trace="--trace" in sys.argv[1:])
+    argv = [a for a in sys.argv[1:] if a not in ("--trace", "--hipgraph")]
+    main(argv or None, trace="--trace" in sys.argv[1:], graphed="--hipgraph" in sys.argv[1:])
