@@ -684,6 +684,20 @@ k_agg_seg2d(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
 // group the chunk's 16 source indices arrive in one coalesced load and are
 // broadcast lane by lane with ds_swizzle (pattern fixed per unrolled step); lanes
 // of a finished item are masked off and issue no loads.
+template <int G>
+__device__ __forceinline__ int bcastG(int v, int k) {  // lane k of each G-lane group (G = 16 or 32), k < G
+  static_assert(G == 16 || G == 32, "group of 16 or 32 lanes");
+  switch (k) {
+#define GTA_BG(K_) case K_: return __builtin_amdgcn_ds_swizzle(v, (0x1F & ~(G - 1)) | (((K_) % G) << 5));
+    GTA_BG(0) GTA_BG(1) GTA_BG(2) GTA_BG(3) GTA_BG(4) GTA_BG(5) GTA_BG(6) GTA_BG(7)
+    GTA_BG(8) GTA_BG(9) GTA_BG(10) GTA_BG(11) GTA_BG(12) GTA_BG(13) GTA_BG(14) GTA_BG(15)
+    GTA_BG(16) GTA_BG(17) GTA_BG(18) GTA_BG(19) GTA_BG(20) GTA_BG(21) GTA_BG(22) GTA_BG(23)
+    GTA_BG(24) GTA_BG(25) GTA_BG(26) GTA_BG(27) GTA_BG(28) GTA_BG(29) GTA_BG(30) GTA_BG(31)
+#undef GTA_BG
+  }
+  return v;
+}
+
 __device__ __forceinline__ int bcast16(int v, int k) {  // lane (l & 0x30) | k, k in [0, 16)
   switch (k) {
 #define GTA_B16(K_) case K_: return __builtin_amdgcn_ds_swizzle(v, 0x10 | ((K_) << 5));
@@ -709,23 +723,26 @@ struct AttArgs {
   float* sslabs;   // [B, n_rows, H] per-item partial sums of v
 };
 
-template <int VW, int U, bool WEIGHTED, int NT = 0, bool ATT = false, int SFC = -1>
+template <int VW, int U, bool WEIGHTED, int NT = 0, bool ATT = false, int SFC = -1, int G = 16>
 // NT bit 0: non-temporal index/weight loads, bit 1: slab stores; SFC >= 0: the ATT special function
-// fixed at compile time (-1: att.sf at run time)
+// fixed at compile time (-1: att.sf at run time); G = lanes per item (16: four items per wave,
+// 32: two items per wave -- one 512-B row per half-wave instruction at F = 128)
 __global__ void __launch_bounds__(kBlock)
 k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items, const float* __restrict__ x,
            int64_t ldx, const float* __restrict__ w, int64_t ldw, int lph, float* __restrict__ slabs,
            const SegItem* __restrict__ items, AttArgs att = AttArgs{}) {
-  constexpr int F = 16 * VW;
+  constexpr int F = G * VW;
+  constexpr int IPW = kWave / G;  // items per wave
   constexpr int NQ = VW / 4;
   const int lane = threadIdx.x & (kWave - 1);
-  const int l16 = lane & 15;
-  const int64_t k = (static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform()) * 4 + (lane >> 4);
+  const int l16 = lane & (G - 1);
+  const int64_t k = (static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform()) * IPW + lane / G;
   SegItem it{0, 0, 0};
   if (k < n_items) it = items[k];
   const int len = it.len;
-  int mx = max(len, __shfl_xor(len, 16));
-  mx = max(mx, __shfl_xor(mx, 32));
+  int mx = len;
+#pragma unroll
+  for (int off = G; off < kWave; off <<= 1) mx = max(mx, __shfl_xor(mx, off));
   const int maxlen = __builtin_amdgcn_readfirstlane(mx);
   if (maxlen == 0) return;
   const int64_t eb = it.beg;
@@ -738,16 +755,16 @@ k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items,
   if (ATT && len > 0) arow = att.a[static_cast<int64_t>(it.row) * att.lda + head];
   auto ldi = [&](int64_t e) { return (NT & 1) ? __builtin_nontemporal_load(indices + e) : indices[e]; };
   int idxv = (l16 < len) ? ldi(eb + l16) : 0;
-  for (int c = 0; c < maxlen; c += 16) {
-    const int idxn = (c + 16 + l16 < len) ? ldi(eb + c + 16 + l16) : 0;
+  for (int c = 0; c < maxlen; c += G) {
+    const int idxn = (c + G + l16 < len) ? ldi(eb + c + G + l16) : 0;
 #pragma unroll
-    for (int s = 0; s < 16; s += U) {
+    for (int s = 0; s < G; s += U) {
       if (c + s >= maxlen) break;
       float4 xv[U][NQ];
       float wu[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int src = bcast16(idxv, s + u);
+        const int src = bcastG<G>(idxv, s + u);
         const bool ok = c + s + u < len;
         if (ok) {
           const float4* p = reinterpret_cast<const float4*>(x + static_cast<int64_t>(src) * ldx + col);
@@ -1695,6 +1712,7 @@ int g_agg_nt = 0;     // non-temporal index/weight loads in the SpMM form
 int g_agg_lean = 1;   // k_agg_lean for F = 64*VW SpMM shapes
 int64_t g_seg_waves = 0;  // persistent waves of the column-blocked kernel (0 = 8 per SIMD)
 int g_seg_quarter = 1;     // quarter-wave (4 items per wave) form of the blocked aggregate
+int g_seg_lanes = 32;      // lanes per item of that form at F = 128: 32 (2 items/wave, measured 3 % faster) or 16
 int g_seg_nt = 0;          // non-temporal bits of the quarter-wave form (F = 128, U = 8)
 int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
 int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
@@ -1723,6 +1741,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "seg_waves") { g_seg_waves = value; return 0; }
   if (k == "seg_nt") { g_seg_nt = static_cast<int>(value); return 0; }
   if (k == "seg_u") { g_seg_u = static_cast<int>(value); return 0; }
+  if (k == "seg_lanes") { g_seg_lanes = static_cast<int>(value); return 0; }
   if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
   if (k == "mm_prefetch") { g_mm_prefetch = static_cast<int>(value); return 0; }
   if (k == "mm_blocks_per_cu") { g_mm_blocks_per_cu = value; return 0; }
@@ -1940,7 +1959,19 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
                                                             static_cast<const SegItem*>(v.items));               \
   else k_agg_seg4<VW_, U_, false, NT_><<<g4, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, lph, slabs,  \
                                                            static_cast<const SegItem*>(v.items))
-      if (vq == 4) { GTA_SEG4(4, 4); }
+      if (vq == 8 && g_seg_lanes == 32) {  // half-wave items: 32 lanes x float4
+        const int lph32 = w ? static_cast<int>((F / heads) / 4) : 0;
+        const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
+        const SegItem* its = static_cast<const SegItem*>(v.items);
+        if (w && lph32 >= 1 && 32 % lph32 == 0 && (F / heads) % 4 == 0)
+          k_agg_seg4<4, 8, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, lph32,
+                                                                       slabs, its);
+        else if (!w)
+          k_agg_seg4<4, 8, false, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, 0,
+                                                                        slabs, its);
+        else
+          return fail(GTA_ERR_UNSUPPORTED, "aggregate_blocked: half-wave head layout");
+      } else if (vq == 4) { GTA_SEG4(4, 4); }
       else if (vq == 8) {
         if (g_seg_u == 2) { GTA_SEG4(8, 2); } else if (g_seg_u == 4) { GTA_SEG4(8, 4); }
         else if (g_seg_nt == 1) { GTA_SEG4NT(8, 8, 1); } else if (g_seg_nt == 2) { GTA_SEG4NT(8, 8, 2); }
@@ -2030,7 +2061,14 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
       indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, it, att);                                            \
   else k_agg_seg4<VW_, U_, false, 0, true><<<g4, blk, 0, s>>>(indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, \
                                                              it, att)
-  if (vq == 4) { GTA_ATT(4, 4); } else if (vq == 8) { GTA_ATT(8, 8); } else { GTA_ATT(16, 2); }
+  const int lph32 = static_cast<int>((F / heads) / 4);
+  if (F == 128 && g_seg_lanes == 32 && (F / heads) % 4 == 0 && lph32 >= 1 && 32 % lph32 == 0) {
+    const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
+    if (elr) k_agg_seg4<4, 8, false, 0, true, GTA_SF_EXP_LEAKY_RELU, 32><<<g2h, blk, 0, s>>>(
+        indices, n_rows, items, x, ldx, nullptr, 0, lph32, slabs, it, att);
+    else k_agg_seg4<4, 8, false, 0, true, -1, 32><<<g2h, blk, 0, s>>>(indices, n_rows, items, x, ldx, nullptr, 0,
+                                                                      lph32, slabs, it, att);
+  } else if (vq == 4) { GTA_ATT(4, 4); } else if (vq == 8) { GTA_ATT(8, 8); } else { GTA_ATT(16, 2); }
 #undef GTA_ATT
   GTA_LAUNCHED("k_agg_seg4<att>");
   const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));

@@ -32,7 +32,11 @@ def main():
     g, x, alpha = bench.make_inputs(args.n, args.e, dev)
     if args.slices > 1:
         from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G
-        g = G.Graph(g.indptr, torch.remainder(g.indices, args.n // args.slices).to(torch.int32).contiguous())
+        cols = torch.remainder(g.indices.long(), args.n // args.slices)
+        rows = g.row_of_edge().long()
+        order = torch.sort(rows * args.n + cols).indices  # keep columns sorted within rows (blocked plans)
+        g = G.Graph(g.indptr, cols[order].to(torch.int32).contiguous())
+        alpha = alpha[order].contiguous()
     y = torch.empty(g.n_rows, bench.F, device=dev)
     variants = []
     for v in args.variants.split(","):
@@ -43,6 +47,8 @@ def main():
             quarter = 0 if "q0" in parts[1:] else 1  # q0: one item per wave (k_agg_seg2d)
             us = [int(p_[1:]) for p_ in parts[1:] if p_.startswith("u")]
             quarter = quarter * (us[0] if us else 8)  # u<U>: edges per step of the quarter-wave form
+            lanes = 32 if "h" in parts[1:] else 16  # h: half-wave items (32 lanes each)
+            wv = wv + 10000000 * (lanes // 16 - 1)
             nts = [int(p_[2:]) for p_ in parts[1:] if p_.startswith("nt")]
             wv = wv + 1000 * (nts[0] if nts else 0)  # nt<bits>: non-temporal loads (1) / slab stores (2)
             variants.append((v, -int(parts[0][3:]), quarter, wv, single))
@@ -61,6 +67,8 @@ def main():
     for r in range(args.rounds):
         for name, lpe, chunk, nt, lean in variants:
             if lpe < 0:
+                ops.set_debug("seg_lanes", 32 if nt >= 10000000 else 16)
+                nt = nt % 10000000
                 ops.set_debug("seg_waves", nt % 1000)
                 ops.set_debug("seg_nt", nt // 1000)
                 ops.set_debug("seg_quarter", 1 if chunk else 0)

@@ -319,7 +319,8 @@ def test_edge_softmax_other_sf_and_errors(dev):
         ops.edge_softmax(g, a, b[:, :4].contiguous())
 
 
-@pytest.mark.parametrize("knobs", [{"seg_quarter": 0}, {"seg_u": 2}, {"seg_u": 4}, {"seg_nt": 3}])
+@pytest.mark.parametrize("knobs", [{"seg_quarter": 0}, {"seg_u": 2}, {"seg_u": 4}, {"seg_nt": 3}, {"seg_lanes": 16},
+                                   {"seg_lanes": 16, "seg_u": 4}])
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 0), (64, 4), (256, 16), (128, 1)])
 def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     """Every form of the blocked kernel (one item per wave, quarter-wave with 2/4/8 edges per
@@ -331,7 +332,7 @@ def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
     w = torch.from_numpy(rng.random((g.nnz, heads)).astype(np.float32)).to(dev) if heads else None
     y0 = ops.aggregate_blocked(g, x, w, blocks=8)
-    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 0}
+    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 0, "seg_lanes": 32}
     try:
         for k, v in knobs.items():
             ops.set_debug(k, v)
@@ -347,7 +348,7 @@ def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     xn, wn = x.cpu().numpy(), None if w is None else w.cpu().numpy()
     _check(y, isa_ref.aggregate(ip, ix, xn, "src", wn), isa_ref.aggregate_abs(ip, ix, xn, "src", wn), f"{knobs}")
     if "seg_quarter" not in knobs:
-        assert torch.equal(y, y0)  # same per-item edge order in every quarter-wave form
+        assert torch.equal(y, y0)  # same per-item edge order in every quarter/half-wave form
 
 
 @pytest.mark.parametrize("form", ["rows", "tile"])
@@ -393,7 +394,8 @@ def test_update_mm_weight_cache_never_stale(dev):
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 16), (128, 1), (64, 4), (64, 16), (256, 8), (256, 16)])
 @pytest.mark.parametrize("normalize", [True, False])
 @pytest.mark.parametrize("blocks", [1, 5, 16])
-def test_gat_aggregate_blocked_matches_oracle(dev, F, heads, normalize, blocks):
+@pytest.mark.parametrize("lanes", [32, 16])
+def test_gat_aggregate_blocked_matches_oracle(dev, F, heads, normalize, blocks, lanes):
     """Fused GAT attention aggregate vs the oracle's op-by-op composition (edge softmax, alpha * x,
     gather); empty rows give 0 (normalize) and a 3000-edge row spans every block."""
     n, e = 800, 20000
@@ -407,9 +409,13 @@ def test_gat_aggregate_blocked_matches_oracle(dev, F, heads, normalize, blocks):
     x = rng.standard_normal((n, F)).astype(np.float32)
     a = rng.standard_normal((n, heads)).astype(np.float32)
     b = rng.standard_normal((n, heads)).astype(np.float32)
-    y, sums = ops.gat_aggregate_blocked(g, torch.from_numpy(x).to(dev), torch.from_numpy(a).to(dev),
-                                        torch.from_numpy(b).to(dev), normalize=normalize, want_sums=True,
-                                        blocks=blocks)
+    ops.set_debug("seg_lanes", lanes)
+    try:
+        y, sums = ops.gat_aggregate_blocked(g, torch.from_numpy(x).to(dev), torch.from_numpy(a).to(dev),
+                                            torch.from_numpy(b).to(dev), normalize=normalize, want_sums=True,
+                                            blocks=blocks)
+    finally:
+        ops.set_debug("seg_lanes", 32)
     ref, rsum = isa_ref.gat_aggregate(ip, ix, x.astype(np.float64), a.astype(np.float64), b.astype(np.float64),
                                       "EXP_LEAKY_RELU", normalize)
     _check(sums, rsum, rsum, f"gat sums F={F} H={heads}")
