@@ -1963,9 +1963,17 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
         const int lph32 = w ? static_cast<int>((F / heads) / 4) : 0;
         const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
         const SegItem* its = static_cast<const SegItem*>(v.items);
-        if (w && lph32 >= 1 && 32 % lph32 == 0 && (F / heads) % 4 == 0)
-          k_agg_seg4<4, 8, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, lph32,
-                                                                       slabs, its);
+        if (w && lph32 >= 1 && 32 % lph32 == 0 && (F / heads) % 4 == 0) {
+          if (g_seg_u == 4)
+            k_agg_seg4<4, 4, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
+                                                                         lph32, slabs, its);
+          else if (g_seg_u == 16)
+            k_agg_seg4<4, 16, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
+                                                                          lph32, slabs, its);
+          else
+            k_agg_seg4<4, 8, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
+                                                                         lph32, slabs, its);
+        }
         else if (!w)
           k_agg_seg4<4, 8, false, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, 0,
                                                                         slabs, its);
