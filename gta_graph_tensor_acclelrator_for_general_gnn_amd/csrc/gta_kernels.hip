@@ -1713,7 +1713,7 @@ int g_agg_lean = 1;   // k_agg_lean for F = 64*VW SpMM shapes
 int64_t g_seg_waves = 0;  // persistent waves of the column-blocked kernel (0 = 8 per SIMD)
 int g_seg_quarter = 1;     // quarter-wave (4 items per wave) form of the blocked aggregate
 int g_seg_lanes = 32;      // lanes per item of that form at F = 128: 32 (2 items/wave, measured 3 % faster) or 16
-int g_seg_nt = 0;          // non-temporal bits of the quarter-wave form (F = 128, U = 8)
+int g_seg_nt = 2;          // non-temporal bits of the multi-item forms at F = 128, U = 8: 2 = slab stores (-1 %)
 int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
 int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
 int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
@@ -1970,6 +1970,12 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
           else if (g_seg_u == 16)
             k_agg_seg4<4, 16, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
                                                                           lph32, slabs, its);
+          else if (g_seg_nt == 1)
+            k_agg_seg4<4, 8, true, 1, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
+                                                                         lph32, slabs, its);
+          else if (g_seg_nt == 2)
+            k_agg_seg4<4, 8, true, 2, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
+                                                                         lph32, slabs, its);
           else
             k_agg_seg4<4, 8, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
                                                                          lph32, slabs, its);

@@ -332,7 +332,7 @@ def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
     w = torch.from_numpy(rng.random((g.nnz, heads)).astype(np.float32)).to(dev) if heads else None
     y0 = ops.aggregate_blocked(g, x, w, blocks=8)
-    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 0, "seg_lanes": 32}
+    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 2, "seg_lanes": 32}
     try:
         for k, v in knobs.items():
             ops.set_debug(k, v)
