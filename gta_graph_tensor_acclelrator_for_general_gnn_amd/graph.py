@@ -7,7 +7,7 @@ in CSR order.  The reference holds adjacency only as a dense .npy
 (code/preprocessing.py:14) or a CSR .npz it never uses (code/simulator.py:63-73);
 this CSR is the device-resident form of the same matrix (rows = dst, cols = src).
 
-Synthetic shapes: Cora N=2708/E=10556, Flickr 89250/899756,
+Synthetic shapes: Cora N=2708/E=10556, CiteSeer 3327/9228, PubMed 19717/88648, Flickr 89250/899756,
 Reddit 232965/114615892, ogbn-products 2449029/123718280.  Degrees are
 lognormal (sigma 1) scaled to the exact edge count; sources are uniform
 (or "locality": near the destination id).
@@ -16,8 +16,10 @@ import math
 
 import torch
 
-SHAPES = {
+SHAPES = {  # node counts as the reference hard-codes them (code/compiler.py:491-498, interpreter.py:808-815)
     "cora": (2708, 10556),
+    "citeseer": (3327, 9228),    # V2/GAT_Cora.yaml's dimensions (feature_number 3327, output_number 9228)
+    "pubmed": (19717, 88648),
     "flickr": (89250, 899756),
     "reddit": (232965, 114615892),
     "products": (2449029, 123718280),

@@ -1,4 +1,5 @@
 import numpy as np
+import pytest
 import torch
 
 from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G
@@ -41,3 +42,14 @@ def test_norm_weights():
     assert w.shape == (1000,) and torch.all(w > 0)
     s = G.mean_weights(g)
     assert s.shape == (100,)
+
+
+@pytest.mark.parametrize("name", ["cora", "citeseer", "pubmed", "flickr"])
+def test_dataset_shapes(name):
+    """Every dataset the reference names has a synthetic CSR of its shape (node counts as
+    code/compiler.py:491-498 hard-codes them)."""
+    g = G.dataset_graph(name, seed=1)
+    n, e = G.SHAPES[name]
+    assert g.n_rows == n and g.nnz == e
+    ip, ix = g.numpy()
+    assert ip[0] == 0 and ip[-1] == e and (np.diff(ip) >= 0).all() and ix.min() >= 0 and ix.max() < n
