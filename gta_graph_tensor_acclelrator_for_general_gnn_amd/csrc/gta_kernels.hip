@@ -607,24 +607,23 @@ k_agg_seg(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indice
   }
 }
 
-// Single-launch column-blocked form: item k = (b = k / n_rows, row = perm[k % n_rows]),
-// b-major, so the waves in flight at any moment gather from one or two X slices.
-// Each non-empty (b, row) segment writes its partial to slab b; k_seg_reduce sums
-// the non-empty slabs of each row in block order (deterministic, no atomics).
+// Single-launch column-blocked form: one wave per plan item (a bounded part of one
+// (block, row) segment), items block-major, so the waves in flight at any moment
+// gather from one or two X slices.  Item k writes its partial to slab row k;
+// k_seg_reduce sums each row's slab rows in (block, part) order (deterministic, no
+// atomics).
 template <int VW, int GL>
 __global__ void __launch_bounds__(kBlock)
-k_agg_seg2d(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
+k_agg_seg2d(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p,
             const float* __restrict__ x, int64_t ldx, const float* __restrict__ w, int64_t ldw,
-            float* __restrict__ slabs, SegView sv, const SegItem* __restrict__ items) {
+            float* __restrict__ slabs, const SegItem* __restrict__ items) {
   constexpr int U = (GL > 8) ? GL : 8;
   constexpr int NWL = (GL > 0) ? U / GL : 0;
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t k = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
-  if (k >= n_rows * sv.B) return;
-  const int b = static_cast<int>(k / n_rows);
+  if (k >= *n_items_p) return;
   const SegItem it = items[k];
   if (it.len == 0) return;
-  const int64_t row = it.row;
   const int64_t eb = it.beg, ee = it.beg + it.len;
   const int col = lane * VW;
   const int head = (GL > 0) ? lane / GL : 0;
@@ -674,7 +673,7 @@ k_agg_seg2d(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
   Vec<VW> o;
 #pragma unroll
   for (int q = 0; q < VW; ++q) o.v[q] = acc[q];
-  o.store(slabs + (static_cast<int64_t>(b) * n_rows + row) * (kWave * VW) + col);
+  o.store(slabs + k * (kWave * VW) + col);
 }
 
 // Quarter-wave form of k_agg_seg2d: a wave runs FOUR consecutive (block, row) items,
@@ -711,7 +710,7 @@ __device__ __forceinline__ int bcast16(int v, int k) {  // lane (l & 0x30) | k, 
 // ATT (fused GAT attention, GAT ops 6-12 minus the final SF): the edge weight is
 // not read but computed, v = sf(a[row, h] + b[src, h]) from the two score tables
 // (b gathered like x, from the same column block), and the item's per-head sum of
-// v goes to a second slab; k_seg_reduce_att divides.  No [E, H] tensor is
+// v follows its partials in the slab row; k_seg_reduce_att divides.  No [E, H] tensor is
 // written or read.
 struct AttArgs {
   const float* a;  // [n_rows, H] destination-side scores (lda)
@@ -719,8 +718,7 @@ struct AttArgs {
   const float* b;  // [n_cols, H] source-side scores (ldb)
   int64_t ldb;
   int sf;
-  int H;
-  float* sslabs;   // [B, n_rows, H] per-item partial sums of v
+  int H;           // the item's per-head sums of v follow its F partials in the slab row (stride F + H padded to 4)
 };
 
 template <int VW, int U, bool WEIGHTED, int NT = 0, bool ATT = false, int SFC = -1, int G = 16>
@@ -728,7 +726,7 @@ template <int VW, int U, bool WEIGHTED, int NT = 0, bool ATT = false, int SFC = 
 // fixed at compile time (-1: att.sf at run time); G = lanes per item (16: four items per wave,
 // 32: two items per wave -- one 512-B row per half-wave instruction at F = 128)
 __global__ void __launch_bounds__(kBlock)
-k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items, const float* __restrict__ x,
+k_agg_seg4(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
            int64_t ldx, const float* __restrict__ w, int64_t ldw, int lph, float* __restrict__ slabs,
            const SegItem* __restrict__ items, AttArgs att = AttArgs{}) {
   constexpr int F = G * VW;
@@ -737,6 +735,7 @@ k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items,
   const int lane = threadIdx.x & (kWave - 1);
   const int l16 = lane & (G - 1);
   const int64_t k = (static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform()) * IPW + lane / G;
+  const int64_t n_items = *n_items_p;
   SegItem it{0, 0, 0};
   if (k < n_items) it = items[k];
   const int len = it.len;
@@ -798,37 +797,68 @@ k_agg_seg4(const int32_t* __restrict__ indices, int64_t n_rows, int64_t n_items,
     idxv = idxn;
   }
   if (len > 0) {
-    const int b = static_cast<int>(k / n_rows);
-    float* o = slabs + (static_cast<int64_t>(b) * n_rows + it.row) * F + col;
+    const int64_t lds = ATT ? F + ((att.H + 3) & ~3) : F;  // sums padded to 16 B
+    float* o = slabs + k * lds + col;
 #pragma unroll
     for (int q = 0; q < VW; ++q) {
       if (NT & 2) __builtin_nontemporal_store(acc[q], o + q);
       else o[q] = acc[q];
     }
-    if (ATT && l16 % lph == 0) att.sslabs[(static_cast<int64_t>(b) * n_rows + it.row) * att.H + head] = ssum;
+    if (ATT && l16 % lph == 0) slabs[k * lds + F + head] = ssum;
+  }
+}
+
+// The row's slab rows (item ids row_items[row_ptr[row] .. row_ptr[row+1]), in
+// (block, part) order) summed in that order; ids arrive 64 at a time with one
+// coalesced load and are broadcast by readlane, 4 slab loads in flight.
+struct RowItems {
+  const int64_t* row_ptr;
+  const int32_t* row_items;
+};
+
+template <int VW, typename Fn>
+__device__ __forceinline__ void for_row_items(RowItems ri, int64_t row, int lane, Fn&& fn) {
+  const int64_t j0 = ri.row_ptr[row], j1 = ri.row_ptr[row + 1];
+  for (int64_t j = j0; j < j1; j += kWave) {
+    const int n = static_cast<int>(min<int64_t>(kWave, j1 - j));
+    const int ids = (lane < n) ? ri.row_items[j + lane] : 0;
+    int t = 0;
+    for (; t + 4 <= n; t += 4) {
+      const int64_t i0 = __builtin_amdgcn_readlane(ids, t), i1 = __builtin_amdgcn_readlane(ids, t + 1);
+      const int64_t i2 = __builtin_amdgcn_readlane(ids, t + 2), i3 = __builtin_amdgcn_readlane(ids, t + 3);
+      fn(i0, i1, i2, i3, 4);
+    }
+    for (; t < n; ++t) {
+      const int64_t i0 = __builtin_amdgcn_readlane(ids, t);
+      fn(i0, i0, i0, i0, 1);
+    }
   }
 }
 
 template <int VW>
 __global__ void __launch_bounds__(kBlock)
 k_seg_reduce(int64_t n_rows, const float* __restrict__ slabs, const float* __restrict__ row_scale,
-             float* __restrict__ y, int64_t ldy, int accumulate, SegView sv) {
+             float* __restrict__ y, int64_t ldy, int accumulate, RowItems ri) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
   if (row >= n_rows) return;
-  const int32_t* sg = sv.seg + row * (sv.B + 1);
   const int col = lane * VW;
   constexpr int F = kWave * VW;
   float acc[VW];
 #pragma unroll
   for (int q = 0; q < VW; ++q) acc[q] = 0.f;
-  for (int b = 0; b < sv.B; ++b) {
-    if (sg[b] == sg[b + 1]) continue;
-    Vec<VW> p;
-    p.load(slabs + (static_cast<int64_t>(b) * n_rows + row) * F + col);
+  for_row_items<VW>(ri, row, lane, [&](int64_t i0, int64_t i1, int64_t i2, int64_t i3, int m) {
+    Vec<VW> p[4];
+    p[0].load(slabs + i0 * F + col);
+    if (m == 4) {
+      p[1].load(slabs + i1 * F + col);
+      p[2].load(slabs + i2 * F + col);
+      p[3].load(slabs + i3 * F + col);
+    }
+    for (int u = 0; u < m; ++u)
 #pragma unroll
-    for (int q = 0; q < VW; ++q) acc[q] += p.v[q];
-  }
+      for (int q = 0; q < VW; ++q) acc[q] += p[u].v[q];
+  });
   const float scale = row_scale ? row_scale[row] : 1.f;
   float* yp = y + row * ldy + col;
   Vec<VW> o;
@@ -843,36 +873,38 @@ k_seg_reduce(int64_t n_rows, const float* __restrict__ slabs, const float* __res
   o.store(yp);
 }
 
-// Ordered reduce of the attention form: y[row, c] = sum_b acc_b / sum_b s_b[head(c)]
+// Ordered reduce of the attention form: y[row, c] = sum_k acc_k / sum_k s_k[head(c)]
 // (normalize; rows without edges get 0), or the numerator alone; sums[row, h] =
-// sum_b s_b[h] when requested.  Same block order as k_seg_reduce.
+// sum_k s_k[h] when requested.  Slab rows hold F partials then H sums (stride F + H rounded up to 4);
+// same item order as k_seg_reduce.
 template <int VW>
 __global__ void __launch_bounds__(kBlock)
-k_seg_reduce_att(int64_t n_rows, const float* __restrict__ slabs, const float* __restrict__ sslabs, int H,
-                 int normalize, float* __restrict__ y, int64_t ldy, float* __restrict__ sums, SegView sv) {
+k_seg_reduce_att(int64_t n_rows, const float* __restrict__ slabs, int H, int normalize, float* __restrict__ y,
+                 int64_t ldy, float* __restrict__ sums, RowItems ri) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
   if (row >= n_rows) return;
-  const int32_t* sg = sv.seg + row * (sv.B + 1);
   const int col = lane * VW;
   constexpr int F = kWave * VW;
+  const int64_t lds = F + ((H + 3) & ~3);
   const int head = col / (F / H);
   float acc[VW];
 #pragma unroll
   for (int q = 0; q < VW; ++q) acc[q] = 0.f;
   float sh = 0.f, sl = 0.f;  // this lane's head sum; lane < H: head `lane`'s sum (for `sums`)
-  bool any = false;
-  for (int b = 0; b < sv.B; ++b) {
-    if (sg[b] == sg[b + 1]) continue;
-    any = true;
-    Vec<VW> p;
-    p.load(slabs + (static_cast<int64_t>(b) * n_rows + row) * F + col);
+  const bool any = ri.row_ptr[row + 1] > ri.row_ptr[row];
+  for_row_items<VW>(ri, row, lane, [&](int64_t i0, int64_t i1, int64_t i2, int64_t i3, int m) {
+    const int64_t id[4] = {i0, i1, i2, i3};
+    for (int u = 0; u < m; ++u) {
+      Vec<VW> p;
+      p.load(slabs + id[u] * lds + col);
 #pragma unroll
-    for (int q = 0; q < VW; ++q) acc[q] += p.v[q];
-    const float* ss = sslabs + (static_cast<int64_t>(b) * n_rows + row) * H;
-    sh += ss[head];
-    if (lane < H) sl += ss[lane];
-  }
+      for (int q = 0; q < VW; ++q) acc[q] += p.v[q];
+      const float* ss = slabs + id[u] * lds + F;
+      sh += ss[head];
+      if (lane < H) sl += ss[lane];
+    }
+  });
   Vec<VW> o;
 #pragma unroll
   for (int q = 0; q < VW; ++q) o.v[q] = normalize ? (any ? acc[q] / sh : 0.f) : acc[q];
@@ -880,46 +912,78 @@ k_seg_reduce_att(int64_t n_rows, const float* __restrict__ slabs, const float* _
   if (sums != nullptr && lane < H) sums[row * H + lane] = sl;
 }
 
-// ---- column-blocked plan: segment table + heavy-first row order -----------
-// layout: int64 hdr[8] {B, bsize, n_rows, unsorted_flag}, int32 perm[n_rows],
-//         int32 seg[n_rows*(B+1)], int32 bucket[64] (count, offset)
+// ---- column-blocked plan: segment table, heavy-first row order, bounded items ----
+// A (block, row) segment of len edges becomes ceil(len / item_edges) items of
+// near-equal length (empty segments none), so no single item's gather chain
+// outlasts the rest of the launch (a Reddit row holds up to ~2.4e4 edges).  Item k
+// writes slab row k; row_items lists each row's items in (block, part) order, the
+// fixed order of the ordered reduce.
+// layout (host-computable offsets first, then the item arrays):
+//   int64 hdr[8] {B, bsize, n_rows, unsorted_flag, n_items, item_edges, max_items, row_items byte offset}
+//   int32 perm[n_rows]             rows, heaviest degree bucket first
+//   int32 seg[n_rows*(B+1)]        per-row segment offsets
+//   int32 bucket[64]               (count, offset) per degree bucket
+//   int64 row_ptr[n_rows+1]        exclusive scan of items per row
+//   int32 cnt[n_rows*B]            items per (block, perm position), scanned in place to item offsets
+//   SegItem items[max_items]       block-major
+//   int32 row_items[max_items]     item ids of each row, (block, part) order
 struct BlockedView {
   int64_t* hdr;
   int32_t* perm;
   int32_t* seg;
   int32_t* bucket;
-  void* items;  // SegItem[B * n_rows], block-major, heaviest row first within a block
+  int64_t* row_ptr;
+  int32_t* cnt;
+  SegItem* items;
+  int32_t* row_items;
 };
 
-BlockedView blocked_view(void* base, int64_t n_rows, int B) {
+inline int64_t blocked_max_items(int64_t n_rows, int64_t nnz, int B, int64_t item_edges) {
+  return std::min<int64_t>(n_rows * B, nnz) + nnz / item_edges;
+}
+
+inline int64_t blocked_fixed_bytes(int64_t n_rows, int B) {
+  return round16(64) + round16(n_rows * 4) + round16(n_rows * (B + 1) * 4) + round16(64 * 4) +
+         round16((n_rows + 1) * 8) + round16(n_rows * B * 4);
+}
+
+BlockedView blocked_view(void* base, int64_t n_rows, int B, int64_t max_items) {
   char* p = static_cast<char*>(base);
   BlockedView v;
   v.hdr = reinterpret_cast<int64_t*>(p); p += round16(8 * 8);
   v.perm = reinterpret_cast<int32_t*>(p); p += round16(n_rows * 4);
   v.seg = reinterpret_cast<int32_t*>(p); p += round16(n_rows * (B + 1) * 4);
   v.bucket = reinterpret_cast<int32_t*>(p); p += round16(64 * 4);
-  v.items = reinterpret_cast<void*>(p);
+  v.row_ptr = reinterpret_cast<int64_t*>(p); p += round16((n_rows + 1) * 8);
+  v.cnt = reinterpret_cast<int32_t*>(p); p += round16(n_rows * B * 4);
+  v.items = reinterpret_cast<SegItem*>(p); p += round16(max_items * 16);
+  v.row_items = reinterpret_cast<int32_t*>(p);
   return v;
 }
 
-int64_t blocked_bytes(int64_t n_rows, int B) {
-  return round16(64) + round16(n_rows * 4) + round16(n_rows * (B + 1) * 4) + round16(64 * 4) +
-         round16(n_rows * B * 16);
+int64_t blocked_bytes(int64_t n_rows, int B, int64_t max_items) {
+  return blocked_fixed_bytes(n_rows, B) + round16(max_items * 16) + round16(max_items * 4);
 }
 
 __device__ __forceinline__ int deg_bucket(int64_t d) {  // 31 = heaviest ... 0 = empty/1
   return d <= 1 ? 0 : min(31, 63 - __clzll(static_cast<unsigned long long>(d)));
 }
 
+__host__ __device__ __forceinline__ int64_t n_parts(int64_t len, int64_t item_edges) {
+  return (len + item_edges - 1) / item_edges;
+}
+
 // one wave per row: lane b (0..B) binary-searches the first edge with col >= b*bsize;
-// all lanes also verify the row's columns are sorted (the segments need it)
+// all lanes also verify the row's columns are sorted (the segments need it).  Also
+// writes the row's item count (sum over blocks of n_parts) into row_ptr[row].
 __global__ void __launch_bounds__(kBlock)
 k_blocked_seg(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows, int B,
-              int64_t bsize, BlockedView v) {
+              int64_t bsize, int64_t item_edges, BlockedView v) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
   if (row >= n_rows) return;
   const int64_t rb = indptr[row], re = indptr[row + 1];
+  int64_t pos = 0;  // lane b < B+1: offset of block b
   for (int b = lane; b <= B; b += kWave) {
     const int64_t key = static_cast<int64_t>(b) * bsize;
     int64_t lo = rb, hi = re;
@@ -927,8 +991,15 @@ k_blocked_seg(const int64_t* __restrict__ indptr, const int32_t* __restrict__ in
       const int64_t mid = (lo + hi) >> 1;
       if (static_cast<int64_t>(indices[mid]) < key) lo = mid + 1; else hi = mid;
     }
-    v.seg[row * (B + 1) + b] = static_cast<int32_t>((b == B ? re : lo) - rb);
+    pos = (b == B ? re : lo) - rb;
+    v.seg[row * (B + 1) + b] = static_cast<int32_t>(pos);
   }
+  // B <= 63: lane b holds offset b; lane b's segment is [pos_b, pos_{b+1})
+  const int64_t nxt = __shfl_down(pos, 1);
+  int64_t parts = (lane < B) ? n_parts(nxt - pos, item_edges) : 0;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) parts += __shfl_xor(parts, off);
+  if (lane == 0) v.row_ptr[row] = parts;
   bool bad = false;
   for (int64_t e = rb + lane; e + 1 < re; e += kWave) bad |= indices[e] > indices[e + 1];
   if (__any(bad) && lane == 0) atomicOr(reinterpret_cast<unsigned long long*>(&v.hdr[3]), 1ull);
@@ -945,25 +1016,79 @@ __global__ void k_blocked_scan(BlockedView v) {  // heaviest bucket first
   }
 }
 
-__global__ void k_blocked_items(const int64_t* __restrict__ indptr, int64_t n_rows, int B, BlockedView v) {
-  const int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
-  if (k >= n_rows * B) return;
-  const int b = static_cast<int>(k / n_rows);
-  const int32_t row = v.perm[k - static_cast<int64_t>(b) * n_rows];
-  const int32_t* sg = v.seg + static_cast<int64_t>(row) * (B + 1);
-  SegItem it;
-  it.beg = indptr[row] + sg[b];
-  it.row = row;
-  it.len = sg[b + 1] - sg[b];
-  static_cast<SegItem*>(v.items)[k] = it;
-}
-
 __global__ void k_blocked_perm(const int64_t* __restrict__ indptr, int64_t n_rows, BlockedView v) {
   const int64_t r = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (r >= n_rows) return;
   const int k = deg_bucket(indptr[r + 1] - indptr[r]);
   const int pos = atomicAdd(&v.bucket[32 + k], 1);  // order inside a bucket is free: results don't depend on it
   v.perm[pos] = static_cast<int32_t>(r);
+}
+
+// cnt[k] = items of (block b = k / n_rows, row perm[k % n_rows])
+__global__ void k_blocked_cnt(int64_t n_rows, int B, int64_t item_edges, BlockedView v) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= n_rows * B) return;
+  const int b = static_cast<int>(k / n_rows);
+  const int32_t row = v.perm[k - static_cast<int64_t>(b) * n_rows];
+  const int32_t* sg = v.seg + static_cast<int64_t>(row) * (B + 1);
+  v.cnt[k] = static_cast<int32_t>(n_parts(sg[b + 1] - sg[b], item_edges));
+}
+
+// single-workgroup in-place exclusive scan (plan build only); out[n] = total when
+// TOTAL_AT_END, and *total = the sum when total != nullptr
+template <typename T>
+__global__ void __launch_bounds__(1024) k_scan_excl(T* __restrict__ a, int64_t n, int total_at_end,
+                                                    int64_t* __restrict__ total) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t per = (n + 1023) / 1024;
+  const int64_t b = min<int64_t>(n, t * per), e = min<int64_t>(n, b + per);
+  int64_t s = 0;
+  for (int64_t i = b; i < e; ++i) s += a[i];
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    const int64_t x = (t >= off) ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  int64_t run = (t == 0) ? 0 : part[t - 1];
+  for (int64_t i = b; i < e; ++i) {
+    const int64_t x = a[i];
+    a[i] = static_cast<T>(run);
+    run += x;
+  }
+  if (t == 1023) {
+    if (total_at_end) a[n] = static_cast<T>(part[1023]);
+    if (total) *total = part[1023];
+  }
+}
+
+// items of (block b, perm position i): near-equal parts of the segment, item ids
+// cnt[k] .. cnt[k] + parts - 1; each is also listed under its row, after the row's
+// items of blocks < b
+__global__ void k_blocked_items(const int64_t* __restrict__ indptr, int64_t n_rows, int B, int64_t item_edges,
+                                BlockedView v) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (k >= n_rows * B) return;
+  const int b = static_cast<int>(k / n_rows);
+  const int32_t row = v.perm[k - static_cast<int64_t>(b) * n_rows];
+  const int32_t* sg = v.seg + static_cast<int64_t>(row) * (B + 1);
+  const int64_t len = sg[b + 1] - sg[b];
+  if (len == 0) return;
+  int64_t before = 0;  // the row's items in blocks < b
+  for (int q = 0; q < b; ++q) before += n_parts(sg[q + 1] - sg[q], item_edges);
+  const int64_t parts = n_parts(len, item_edges), part = (len + parts - 1) / parts;
+  const int64_t id0 = v.cnt[k], slot0 = v.row_ptr[row] + before, beg = indptr[row] + sg[b];
+  for (int64_t j = 0; j < parts; ++j) {
+    SegItem it;
+    it.beg = beg + j * part;
+    it.row = row;
+    it.len = static_cast<int32_t>(max<int64_t>(0, min<int64_t>(part, len - j * part)));
+    v.items[id0 + j] = it;
+    v.row_items[slot0 + j] = static_cast<int32_t>(id0 + j);
+  }
 }
 
 // sum the chunk partials of split rows, in chunk order
@@ -1879,45 +2004,63 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
   return GTA_OK;
 }
 
-int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t blocks) {
-  if (n_rows < 0 || blocks < 1 || blocks > 63) return fail(GTA_ERR_ARG, "blocked_plan_bytes: need 1 <= blocks <= 63");
-  return blocked_bytes(n_rows, static_cast<int>(blocks));
+int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t item_edges) {
+  if (n_rows < 0 || nnz < 0 || blocks < 1 || blocks > 63 || item_edges < 1)
+    return fail(GTA_ERR_ARG, "blocked_plan_bytes: need n_rows, nnz >= 0, 1 <= blocks <= 63, item_edges >= 1");
+  const int B = static_cast<int>(blocks);
+  return blocked_bytes(n_rows, B, blocked_max_items(n_rows, nnz, B, item_edges));
 }
 
 int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
-                                     int64_t blocks, void* plan, int64_t plan_bytes, void* stream) {
-  if (!indptr || !plan || n_rows <= 0 || n_cols <= 0 || blocks < 1 || blocks > 63)
+                                     int64_t nnz, int64_t blocks, int64_t item_edges, void* plan, int64_t plan_bytes,
+                                     void* stream) {
+  if (!indptr || !plan || n_rows <= 0 || n_cols <= 0 || nnz < 0 || blocks < 1 || blocks > 63 || item_edges < 1)
     return fail(GTA_ERR_ARG, "blocked_plan_build: bad arguments");
+  if (nnz > 0 && !indices) return fail(GTA_ERR_ARG, "blocked_plan_build: indices needed");
   if (n_rows > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "blocked_plan_build: > 2^31 rows");
   const int B = static_cast<int>(blocks);
-  if (plan_bytes < blocked_bytes(n_rows, B)) return fail(GTA_ERR_ARG, "blocked_plan_build: plan buffer too small");
-  BlockedView v = blocked_view(plan, n_rows, B);
+  const int64_t mi = blocked_max_items(n_rows, nnz, B, item_edges);
+  if (mi > INT32_MAX || n_rows * B > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "blocked_plan_build: > 2^31 items");
+  if (plan_bytes < blocked_bytes(n_rows, B, mi)) return fail(GTA_ERR_ARG, "blocked_plan_build: plan buffer too small");
+  BlockedView v = blocked_view(plan, n_rows, B, mi);
   hipStream_t s = S(stream);
   const int64_t bsize = (n_cols + B - 1) / B;
-  GTA_HIP(hipMemsetAsync(v.hdr, 0, 64, s));
+  const int64_t hdr[8] = {B, bsize, n_rows, 0, 0, item_edges, mi,
+                          reinterpret_cast<char*>(v.row_items) - static_cast<char*>(plan)};
+  GTA_HIP(hipMemcpyAsync(v.hdr, hdr, sizeof(hdr), hipMemcpyHostToDevice, s));
   GTA_HIP(hipMemsetAsync(v.bucket, 0, 64 * 4, s));
   k_blocked_seg<<<dim3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0, s>>>(
-      indptr, indices, n_rows, B, bsize, v);
+      indptr, indices, n_rows, B, bsize, item_edges, v);
   GTA_LAUNCHED("k_blocked_seg");
   k_blocked_scan<<<1, 64, 0, s>>>(v);
   GTA_LAUNCHED("k_blocked_scan");
   k_blocked_perm<<<dim3(static_cast<unsigned>((n_rows + 255) / 256)), dim3(256), 0, s>>>(indptr, n_rows, v);
   GTA_LAUNCHED("k_blocked_perm");
-  k_blocked_items<<<dim3(static_cast<unsigned>((n_rows * B + 255) / 256)), dim3(256), 0, s>>>(indptr, n_rows, B, v);
+  k_scan_excl<int64_t><<<1, 1024, 0, s>>>(v.row_ptr, n_rows, 1, nullptr);  // items per row -> row_ptr
+  GTA_LAUNCHED("k_scan_excl");
+  const dim3 gk(static_cast<unsigned>((n_rows * B + 255) / 256));
+  k_blocked_cnt<<<gk, dim3(256), 0, s>>>(n_rows, B, item_edges, v);
+  GTA_LAUNCHED("k_blocked_cnt");
+  k_scan_excl<int32_t><<<1, 1024, 0, s>>>(v.cnt, n_rows * B, 0, &v.hdr[4]);  // -> first item id, n_items
+  GTA_LAUNCHED("k_scan_excl");
+  k_blocked_items<<<gk, dim3(256), 0, s>>>(indptr, n_rows, B, item_edges, v);
   GTA_LAUNCHED("k_blocked_items");
   return GTA_OK;
 }
 
-int64_t gta_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t blocks, int64_t F) {
-  if (n_rows < 0 || blocks < 1 || F <= 0) return fail(GTA_ERR_ARG, "blocked_workspace_bytes: bad sizes");
-  return n_rows * blocks * F * static_cast<int64_t>(sizeof(float));
+int64_t gta_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t F,
+                                              int64_t item_edges) {
+  if (n_rows < 0 || nnz < 0 || blocks < 1 || blocks > 63 || F <= 0 || item_edges < 1)
+    return fail(GTA_ERR_ARG, "blocked_workspace_bytes: bad sizes");
+  return blocked_max_items(n_rows, nnz, static_cast<int>(blocks), item_edges) * F * static_cast<int64_t>(sizeof(float));
 }
 
-int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
+int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols, int64_t nnz,
                           const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
                           const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
-                          int64_t blocks, void* workspace, void* stream) {
-  if (n_rows < 0 || F <= 0 || blocks < 1 || blocks > 63) return fail(GTA_ERR_ARG, "aggregate_blocked: bad sizes");
+                          int64_t blocks, int64_t item_edges, void* workspace, void* stream) {
+  if (n_rows < 0 || nnz < 0 || F <= 0 || blocks < 1 || blocks > 63 || item_edges < 1)
+    return fail(GTA_ERR_ARG, "aggregate_blocked: bad sizes");
   if (n_rows == 0) return GTA_OK;
   if (!indptr || !x || !y || !plan) return fail(GTA_ERR_ARG, "aggregate_blocked: bad arguments");
   int gl = 0, vw = 0;
@@ -1936,52 +2079,52 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
   }
   const char* gl_msg = "aggregate_blocked: (F/heads)/VW must be 4, 8 or 16 (or quarter-wave lanes per head 1..16)";
   const int B = static_cast<int>(blocks);
-  BlockedView v = blocked_view(const_cast<void*>(plan), n_rows, B);
+  const int64_t mi = blocked_max_items(n_rows, nnz, B, item_edges);
+  BlockedView v = blocked_view(const_cast<void*>(plan), n_rows, B, mi);
   hipStream_t s = S(stream);
-  if (workspace) {  // single launch into per-block slabs + ordered reduce
-    SegView sv{v.perm, v.seg, B, 0};
+  if (workspace) {  // single launch into per-item slab rows + ordered reduce
+    const RowItems ri{v.row_ptr, v.row_items};
     float* slabs = static_cast<float*>(workspace);
-    const int64_t items = n_rows * B;
+    const int64_t items = mi;  // grid bound; the kernels stop at the plan's n_items
+    const int64_t* nit = &v.hdr[4];
+    const SegItem* its = v.items;
     const dim3 g2(static_cast<unsigned>((items + kWavesPerBlock - 1) / kWavesPerBlock)), blk2(kBlock);
     const int vq = static_cast<int>(F / 16);
     const int lph = w ? static_cast<int>((F / heads) / vq) : 0;
     const bool quarter = g_seg_quarter && (vq == 4 || vq == 8 || vq == 16) && ldx % 4 == 0 && aligned(x, 16) &&
                          (!w || ((F / heads) % vq == 0 && lph >= 1 && 16 % lph == 0));
-    if (quarter) {
+    if (items == 0) {
+      // no edges: no items; the reduce below writes the (empty) rows
+    } else if (quarter) {
       const dim3 g4(static_cast<unsigned>((items + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock)));
 #define GTA_SEG4(VW_, U_)                                                                                   \
-  if (w) k_agg_seg4<VW_, U_, true><<<g4, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, lph, slabs, \
-                                                       static_cast<const SegItem*>(v.items));               \
-  else k_agg_seg4<VW_, U_, false><<<g4, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, lph, slabs,  \
-                                                      static_cast<const SegItem*>(v.items))
+  if (w) k_agg_seg4<VW_, U_, true><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its);     \
+  else k_agg_seg4<VW_, U_, false><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its)
 #define GTA_SEG4NT(VW_, U_, NT_)                                                                             \
-  if (w) k_agg_seg4<VW_, U_, true, NT_><<<g4, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, lph, slabs, \
-                                                            static_cast<const SegItem*>(v.items));               \
-  else k_agg_seg4<VW_, U_, false, NT_><<<g4, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, lph, slabs,  \
-                                                           static_cast<const SegItem*>(v.items))
+  if (w) k_agg_seg4<VW_, U_, true, NT_><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its); \
+  else k_agg_seg4<VW_, U_, false, NT_><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its)
       if (vq == 8 && g_seg_lanes == 32) {  // half-wave items: 32 lanes x float4
         const int lph32 = w ? static_cast<int>((F / heads) / 4) : 0;
         const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
-        const SegItem* its = static_cast<const SegItem*>(v.items);
         if (w && lph32 >= 1 && 32 % lph32 == 0 && (F / heads) % 4 == 0) {
           if (g_seg_u == 4)
-            k_agg_seg4<4, 4, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
+            k_agg_seg4<4, 4, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                          lph32, slabs, its);
           else if (g_seg_u == 16)
-            k_agg_seg4<4, 16, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
+            k_agg_seg4<4, 16, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                           lph32, slabs, its);
           else if (g_seg_nt == 1)
-            k_agg_seg4<4, 8, true, 1, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
+            k_agg_seg4<4, 8, true, 1, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                          lph32, slabs, its);
           else if (g_seg_nt == 2)
-            k_agg_seg4<4, 8, true, 2, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
+            k_agg_seg4<4, 8, true, 2, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                          lph32, slabs, its);
           else
-            k_agg_seg4<4, 8, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw,
+            k_agg_seg4<4, 8, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                          lph32, slabs, its);
         }
         else if (!w)
-          k_agg_seg4<4, 8, false, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, n_rows, items, x, ldx, w, ldw, 0,
+          k_agg_seg4<4, 8, false, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, 0,
                                                                         slabs, its);
         else
           return fail(GTA_ERR_UNSUPPORTED, "aggregate_blocked: half-wave head layout");
@@ -1998,8 +2141,7 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     } else {
       if (!gl_ok) return fail(GTA_ERR_UNSUPPORTED, gl_msg);
 #define GTA_SEG2D(VW_, GL_) \
-  k_agg_seg2d<VW_, GL_><<<g2, blk2, 0, s>>>(indptr, indices, n_rows, x, ldx, w, ldw, slabs, sv, \
-                                            static_cast<const SegItem*>(v.items))
+  k_agg_seg2d<VW_, GL_><<<g2, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, slabs, its)
     if (vw == 2) {
       if (gl == 0) GTA_SEG2D(2, 0); else if (gl == 4) GTA_SEG2D(2, 4); else if (gl == 8) GTA_SEG2D(2, 8); else GTA_SEG2D(2, 16);
     } else if (vw == 4) {
@@ -2011,9 +2153,9 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     GTA_LAUNCHED("k_agg_seg2d");
     }
     const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
-    if (vw == 2) k_seg_reduce<2><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, sv);
-    else if (vw == 4) k_seg_reduce<4><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, sv);
-    else k_seg_reduce<1><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, sv);
+    if (vw == 2) k_seg_reduce<2><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, ri);
+    else if (vw == 4) k_seg_reduce<4><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, ri);
+    else k_seg_reduce<1><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, ri);
     GTA_LAUNCHED("k_seg_reduce");
     return GTA_OK;
   }
@@ -2039,20 +2181,24 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
   return GTA_OK;
 }
 
-int64_t gta_gat_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t blocks, int64_t F, int64_t heads) {
-  if (n_rows < 0 || blocks < 1 || F <= 0 || heads <= 0) return fail(GTA_ERR_ARG, "gat_workspace_bytes: bad sizes");
-  return n_rows * blocks * (F + heads) * static_cast<int64_t>(sizeof(float));
+int64_t gta_gat_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t F,
+                                                  int64_t heads, int64_t item_edges) {
+  if (n_rows < 0 || nnz < 0 || blocks < 1 || blocks > 63 || F <= 0 || heads <= 0 || item_edges < 1)
+    return fail(GTA_ERR_ARG, "gat_workspace_bytes: bad sizes");
+  return blocked_max_items(n_rows, nnz, static_cast<int>(blocks), item_edges) * (F + ((heads + 3) & ~3)) *
+         static_cast<int64_t>(sizeof(float));
 }
 
 int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
-                              const float* x, int64_t ldx, int64_t F, const float* a_dst, int64_t lda,
+                              int64_t nnz, const float* x, int64_t ldx, int64_t F, const float* a_dst, int64_t lda,
                               const float* b_src, int64_t ldb, int64_t heads, int sf, int normalize, float* y,
-                              int64_t ldy, float* sums, const void* plan, int64_t blocks, void* workspace,
-                              void* stream) {
-  if (n_rows < 0 || blocks < 1 || blocks > 63 || heads <= 0 || lda < heads || ldb < heads)
+                              int64_t ldy, float* sums, const void* plan, int64_t blocks, int64_t item_edges,
+                              void* workspace, void* stream) {
+  if (n_rows < 0 || nnz < 0 || blocks < 1 || blocks > 63 || heads <= 0 || lda < heads || ldb < heads ||
+      item_edges < 1)
     return fail(GTA_ERR_ARG, "gat_aggregate_blocked: bad sizes");
   if (n_rows == 0) return GTA_OK;
-  if (!indptr || !x || !a_dst || !b_src || !y || !plan || !workspace)
+  if (!indptr || !x || !a_dst || !b_src || !y || !plan || (!workspace && nnz > 0))
     return fail(GTA_ERR_ARG, "gat_aggregate_blocked: bad arguments");
   const int vq = static_cast<int>(F / 16);
   if ((F != 64 && F != 128 && F != 256) || F % heads || (F / heads) % vq || ldx % 4 || !aligned(x, 16) ||
@@ -2061,35 +2207,39 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
   const int lph = static_cast<int>((F / heads) / vq);
   if (lph < 1 || 16 % lph) return fail(GTA_ERR_UNSUPPORTED, "gat_aggregate_blocked: lanes per head must divide 16");
   const int B = static_cast<int>(blocks);
-  BlockedView v = blocked_view(const_cast<void*>(plan), n_rows, B);
-  SegView sv{v.perm, v.seg, B, 0};
+  const int64_t mi = blocked_max_items(n_rows, nnz, B, item_edges);
+  BlockedView v = blocked_view(const_cast<void*>(plan), n_rows, B, mi);
+  const RowItems ri{v.row_ptr, v.row_items};
   hipStream_t s = S(stream);
   float* slabs = static_cast<float*>(workspace);
-  AttArgs att{a_dst, lda, b_src, ldb, sf, static_cast<int>(heads), slabs + n_rows * B * F};
-  const int64_t items = n_rows * B;
+  AttArgs att{a_dst, lda, b_src, ldb, sf, static_cast<int>(heads)};
+  const int64_t items = mi;
+  const int64_t* nit = &v.hdr[4];
   const dim3 g4(static_cast<unsigned>((items + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock))), blk(kBlock);
-  const SegItem* it = static_cast<const SegItem*>(v.items);
+  const SegItem* it = v.items;
+  if (items > 0) {  // no edges: no items, the reduce alone writes the empty rows
   const bool elr = sf == GTA_SF_EXP_LEAKY_RELU;  // GAT's score function, specialised
 #define GTA_ATT(VW_, U_)                                                                                          \
   if (elr) k_agg_seg4<VW_, U_, false, 0, true, GTA_SF_EXP_LEAKY_RELU><<<g4, blk, 0, s>>>(                        \
-      indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, it, att);                                            \
-  else k_agg_seg4<VW_, U_, false, 0, true><<<g4, blk, 0, s>>>(indices, n_rows, items, x, ldx, nullptr, 0, lph, slabs, \
+      indices, nit, x, ldx, nullptr, 0, lph, slabs, it, att);                                            \
+  else k_agg_seg4<VW_, U_, false, 0, true><<<g4, blk, 0, s>>>(indices, nit, x, ldx, nullptr, 0, lph, slabs, \
                                                              it, att)
   const int lph32 = static_cast<int>((F / heads) / 4);
   if (F == 128 && g_seg_lanes == 32 && (F / heads) % 4 == 0 && lph32 >= 1 && 32 % lph32 == 0) {
     const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
     if (elr) k_agg_seg4<4, 8, false, 0, true, GTA_SF_EXP_LEAKY_RELU, 32><<<g2h, blk, 0, s>>>(
-        indices, n_rows, items, x, ldx, nullptr, 0, lph32, slabs, it, att);
-    else k_agg_seg4<4, 8, false, 0, true, -1, 32><<<g2h, blk, 0, s>>>(indices, n_rows, items, x, ldx, nullptr, 0,
+        indices, nit, x, ldx, nullptr, 0, lph32, slabs, it, att);
+    else k_agg_seg4<4, 8, false, 0, true, -1, 32><<<g2h, blk, 0, s>>>(indices, nit, x, ldx, nullptr, 0,
                                                                       lph32, slabs, it, att);
   } else if (vq == 4) { GTA_ATT(4, 4); } else if (vq == 8) { GTA_ATT(8, 8); } else { GTA_ATT(16, 2); }
 #undef GTA_ATT
   GTA_LAUNCHED("k_agg_seg4<att>");
+  }
   const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
   const int H = static_cast<int>(heads);
-  if (F == 64) k_seg_reduce_att<1><<<g3, blk, 0, s>>>(n_rows, slabs, att.sslabs, H, normalize, y, ldy, sums, sv);
-  else if (F == 128) k_seg_reduce_att<2><<<g3, blk, 0, s>>>(n_rows, slabs, att.sslabs, H, normalize, y, ldy, sums, sv);
-  else k_seg_reduce_att<4><<<g3, blk, 0, s>>>(n_rows, slabs, att.sslabs, H, normalize, y, ldy, sums, sv);
+  if (F == 64) k_seg_reduce_att<1><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri);
+  else if (F == 128) k_seg_reduce_att<2><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri);
+  else k_seg_reduce_att<4><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri);
   GTA_LAUNCHED("k_seg_reduce_att");
   return GTA_OK;
 }

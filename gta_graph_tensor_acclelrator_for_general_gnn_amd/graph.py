@@ -69,12 +69,13 @@ class Graph:
             self._plans[chunk] = ops.AggregatePlan(self, chunk)
         return self._plans[chunk]
 
-    def blocked_plan(self, blocks=32):
-        """Cached column-blocked plan (segment table over `blocks` source-column blocks)."""
-        key = ("blocked", blocks)
+    def blocked_plan(self, blocks=32, item_edges=None):
+        """Cached column-blocked plan (segment table over `blocks` source-column blocks, work items
+        of <= item_edges edges; None = ops.BlockedPlan.ITEM_EDGES)."""
+        from . import ops
+        key = ("blocked", blocks, int(item_edges or ops.BlockedPlan.ITEM_EDGES))
         if key not in self._plans:
-            from . import ops
-            self._plans[key] = ops.BlockedPlan(self, blocks)
+            self._plans[key] = ops.BlockedPlan(self, blocks, key[2])
         return self._plans[key]
 
     def numpy(self):

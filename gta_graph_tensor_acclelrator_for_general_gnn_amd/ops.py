@@ -141,34 +141,45 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
 
 
 class BlockedPlan:
-    """Column-blocked aggregate plan: per-row segment table over B source-column blocks
-    + heaviest-first row order (gta_aggregate_blocked_plan_build)."""
+    """Column-blocked aggregate plan (gta_aggregate_blocked_plan_build): per-row segment table over
+    B source-column blocks, heaviest-first row order, and the work items -- every (block, row)
+    segment cut into parts of <= item_edges edges -- with each row's item list for the ordered
+    reduce."""
 
-    def __init__(self, graph, blocks=32):
+    ITEM_EDGES = 256  # default part length (bench sweep: profiles/r01_agg_sweep_items.json)
+
+    def __init__(self, graph, blocks=32, item_edges=None):
         _need_gpu(graph.indptr)
         L = _L()
         self.graph, self.blocks = graph, int(blocks)
-        nb = check(L.gta_aggregate_blocked_plan_bytes(graph.n_rows, self.blocks), "blocked_plan_bytes")
+        self.item_edges = int(item_edges or BlockedPlan.ITEM_EDGES)
+        nb = check(L.gta_aggregate_blocked_plan_bytes(graph.n_rows, graph.nnz, self.blocks, self.item_edges),
+                   "blocked_plan_bytes")
         self.buf = torch.empty(int(nb), dtype=torch.uint8, device=graph.device)
         check(L.gta_aggregate_blocked_plan_build(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols,
-                                                 self.blocks, _ptr(self.buf), int(nb), _stream(graph.device)),
+                                                 graph.nnz, self.blocks, self.item_edges, _ptr(self.buf), int(nb),
+                                                 _stream(graph.device)),
               "blocked_plan_build")
-        self.sorted = int(self.buf[24:32].view(torch.int64).item()) == 0
+        hdr = self.buf[:64].view(torch.int64).cpu()
+        self.sorted = int(hdr[3]) == 0
+        self.n_items = int(hdr[4])
         self._ws = {}
 
     def workspace(self, F):
-        """Per-block partial slabs for the single-launch form ([B, N, F] fp32)."""
+        """Per-item partial rows for the single-launch form ([items, F] fp32)."""
         if F not in self._ws:
-            nb = check(_L().gta_aggregate_blocked_workspace_bytes(self.graph.n_rows, self.blocks, F),
+            nb = check(_L().gta_aggregate_blocked_workspace_bytes(self.graph.n_rows, self.graph.nnz, self.blocks, F,
+                                                                  self.item_edges),
                        "blocked_workspace_bytes")
             self._ws[F] = torch.empty(int(nb), dtype=torch.uint8, device=self.graph.device)
         return self._ws[F]
 
     def workspace_att(self, F, heads):
-        """Slabs of the fused attention aggregate ([B, N, F] partials + [B, N, heads] sums)."""
+        """Partial rows of the fused attention aggregate ([items, F + heads padded to 4])."""
         key = ("att", F, heads)
         if key not in self._ws:
-            nb = check(_L().gta_gat_aggregate_blocked_workspace_bytes(self.graph.n_rows, self.blocks, F, heads),
+            nb = check(_L().gta_gat_aggregate_blocked_workspace_bytes(self.graph.n_rows, self.graph.nnz, self.blocks,
+                                                                      F, heads, self.item_edges),
                        "gat_workspace_bytes")
             self._ws[key] = torch.empty(int(nb), dtype=torch.uint8, device=self.graph.device)
         return self._ws[key]
@@ -236,9 +247,10 @@ def aggregate_blocked(graph, x, w=None, row_scale=None, out=None, accumulate=Fal
         out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=x.device)
     ldy = _rows(out, "out")
     ws = plan.workspace(F) if single_launch else None
-    check(_L().gta_aggregate_blocked(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols, _ptr(x), ldx,
-                                     F, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy, int(bool(accumulate)),
-                                     _ptr(plan.buf), plan.blocks, _ptr(ws), _stream(x.device)), "aggregate_blocked")
+    check(_L().gta_aggregate_blocked(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols, graph.nnz,
+                                     _ptr(x), ldx, F, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy,
+                                     int(bool(accumulate)), _ptr(plan.buf), plan.blocks, plan.item_edges, _ptr(ws),
+                                     _stream(x.device)), "aggregate_blocked")
     return out
 
 
@@ -272,9 +284,10 @@ def gat_aggregate_blocked(graph, x, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize
         raise ValueError("gat_aggregate_blocked: sums must be a contiguous [N, heads] tensor")
     ws = plan.workspace_att(F, H)
     check(_L().gta_gat_aggregate_blocked(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols,
-                                         _ptr(x), _rows(x, "x"), F, _ptr(a_dst), _rows(a_dst, "a_dst"), _ptr(b_src),
+                                         graph.nnz, _ptr(x), _rows(x, "x"), F, _ptr(a_dst), _rows(a_dst, "a_dst"), _ptr(b_src),
                                          _rows(b_src, "b_src"), H, _sf(sf), 1 if normalize else 0, _ptr(out),
-                                         _rows(out, "out"), _ptr(sums), _ptr(plan.buf), plan.blocks, _ptr(ws),
+                                         _rows(out, "out"), _ptr(sums), _ptr(plan.buf), plan.blocks, plan.item_edges,
+                                         _ptr(ws),
                                          _stream(x.device)), "gat_aggregate_blocked")
     return out, sums
 

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 1
+#define GTA_ABI_VERSION 2  /* 2: blocked plans of bounded items (nnz, item_edges) */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -118,18 +118,26 @@ int64_t gta_aggregate_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t chunk
  * column axis outermost.  Needs each CSR row's columns sorted (the plan build
  * flags unsorted rows in plan header word 3) and F = 64*VW (64/128/256) with
  * (F/heads)/VW in {4, 8, 16}.  Deterministic (fixed block order, no atomics);
- * row_scale is applied per block.  1 <= blocks <= 63. */
-int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t blocks);
+ * row_scale is applied per block.  1 <= blocks <= 63.
+ * The plan cuts every (block, row) segment into ceil(len / item_edges) work
+ * items of near-equal length (the reference's tile split of a long row,
+ * Tile_Times per row tile, code/interpreter.py:244-259): a heavy row's gathers
+ * then spread over several waves instead of one long chain at the launch tail.
+ * plan, workspace and launch must use the same (nnz, blocks, item_edges). */
+int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t item_edges);
 int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
-                                     int64_t blocks, void* plan, int64_t plan_bytes, void* stream);
+                                     int64_t nnz, int64_t blocks, int64_t item_edges, void* plan,
+                                     int64_t plan_bytes, void* stream);
 /* workspace: NULL = B dependent launches accumulating into y; otherwise >=
- * gta_aggregate_blocked_workspace_bytes: one launch over (block, row) items in
- * block-major order writing per-block partial slabs, then an ordered reduce. */
-int64_t gta_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t blocks, int64_t F);
-int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
+ * gta_aggregate_blocked_workspace_bytes: one launch over the plan's items in
+ * block-major order, item k writing partial row k, then an ordered reduce
+ * summing each row's items in (block, part) order. */
+int64_t gta_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t F,
+                                              int64_t item_edges);
+int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols, int64_t nnz,
                           const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
                           const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
-                          int64_t blocks, void* workspace, void* stream);
+                          int64_t blocks, int64_t item_edges, void* workspace, void* stream);
 
 /* ---- K6' fused GAT attention aggregate (GAT ops 6-12 without the final SF) ----
  * v(e, h) = sf( a_dst[dst(e), h] + b_src[src(e), h] )
@@ -142,12 +150,13 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
  * ever written.  workspace >= gta_gat_aggregate_blocked_workspace_bytes.  F in {64, 128,
  * 256}, x rows 16-B aligned, (F/heads) a multiple of F/16.
  * Reference: GAT op graph vTCAD/GraphOP/genGraphOP.py:51-64; template/GAT_op.png. */
-int64_t gta_gat_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t blocks, int64_t F, int64_t heads);
+int64_t gta_gat_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t F,
+                                                  int64_t heads, int64_t item_edges);
 int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
-                              const float* x, int64_t ldx, int64_t F, const float* a_dst, int64_t lda,
+                              int64_t nnz, const float* x, int64_t ldx, int64_t F, const float* a_dst, int64_t lda,
                               const float* b_src, int64_t ldb, int64_t heads, int sf, int normalize, float* y,
-                              int64_t ldy, float* sums, const void* plan, int64_t blocks, void* workspace,
-                              void* stream);
+                              int64_t ldy, float* sums, const void* plan, int64_t blocks, int64_t item_edges,
+                              void* workspace, void* stream);
 
 /* ---- K2 GATHER ADD (edge -> node) ---------------------------------------
  * y[i, :] (+)= sum_{e in row i} xe[e, :]    == gta_aggregate(x_mode=EDGE, w=NULL)

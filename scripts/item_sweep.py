@@ -1,0 +1,93 @@
+"""Interleaved sweep of the blocked aggregate's item length (BlockedPlan item_edges) on the
+Reddit-shaped metric workload and on single rank tiles of 2-D grids (rank (0, 0)'s tile timed
+alone on one GPU, as bench.py --gpus N would run it).  All variants of one shape run in one
+process, round-robin; prints median kernel ms per variant, writes gpurun_out/item_sweep.json.
+
+  python scripts/item_sweep.py --grids 1x1,2x2,4x2,8x1 --items 64,128,256,512,0 --blocks 0
+  (item 0 = unbounded: one item per (block, row) segment; blocks 0 = auto per tile)
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+import bench  # noqa: E402
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, ops  # noqa: E402
+
+UNBOUNDED = 1 << 30
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--grids", default="1x1")
+    ap.add_argument("--items", default="64,128,256,512,0")
+    ap.add_argument("--blocks", default="0", help="comma list; 0 = bench's auto choice for the tile")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--n", type=int, default=bench.N_REDDIT)
+    ap.add_argument("--e", type=int, default=bench.E_REDDIT)
+    args = ap.parse_args()
+    dev = torch.device("cuda:0")
+    t0 = time.time()
+    g, x, alpha = bench.make_inputs(args.n, args.e, dev)
+    print(f"inputs {time.time() - t0:.1f} s", flush=True)
+    out = {}
+    for grid in args.grids.split(","):
+        pr, pc = map(int, grid.lower().split("x"))
+        if pr * pc == 1:
+            gg, xl, wl = g, x, alpha
+        else:
+            s = distributed.GridShard(g, 0, pr, pc)
+            gg, xl, wl = s.graph, x[s.c0:s.c1].contiguous(), alpha[s.edge_ids].contiguous()
+        y = torch.empty(gg.n_rows, bench.F, device=dev)
+        variants = []
+        for b in args.blocks.split(","):
+            B = int(b) or bench.auto_blocks(gg, bench.F)
+            for it in args.items.split(","):
+                ie = int(it) or UNBOUNDED
+                plan = gg.blocked_plan(B, ie)
+                variants.append((f"{grid}:B{B}:i{it}", B, plan))
+        times = {v[0]: [] for v in variants}
+        ref = None
+        for r in range(args.rounds):
+            for name, B, plan in variants:
+                def run():
+                    ops.aggregate_blocked(gg, xl, wl, out=y, plan=plan, blocks=B)
+                run()
+                a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(args.reps):
+                    run()
+                e.record()
+                torch.cuda.synchronize()
+                times[name].append(a.elapsed_time(e) / args.reps)
+                if r == 0:
+                    if ref is None:
+                        ref = y.clone()
+                    else:
+                        d = (y - ref).abs().max().item()
+                        assert d < 1e-3, f"variant {name} differs from the first by {d}"
+        ab = bench.alg_bytes(gg.n_rows, gg.nnz)
+        for name, B, plan in variants:
+            med = float(np.median(times[name]))
+            out[name] = {"rows": gg.n_rows, "edges": gg.nnz, "items": plan.n_items, "median_ms": med,
+                         "min_ms": float(np.min(times[name])), "alg_GBps": ab / (med / 1e3) / 1e9,
+                         "edges_per_s": gg.nnz / (med / 1e3)}
+            print(f"{name:18s} items {plan.n_items:9d}  median {med:7.3f} ms  min {out[name]['min_ms']:7.3f}  "
+                  f"{out[name]['alg_GBps']:7.0f} GB/s alg  {out[name]['edges_per_s'] / 1e9:6.2f} Gedges/s", flush=True)
+        del gg, xl, wl, y, variants
+        torch.cuda.empty_cache()
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "item_sweep.json"), "w") as f:
+        json.dump(out, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()

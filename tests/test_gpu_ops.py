@@ -250,6 +250,48 @@ def test_aggregate_blocked_matches_oracle(dev, F, heads, blocks, single):
     assert torch.equal(y, y2)
 
 
+@pytest.mark.parametrize("item_edges", [1, 7, 64, 256, 1 << 30])
+@pytest.mark.parametrize("blocks", [1, 5, 16])
+def test_blocked_plan_items(dev, item_edges, blocks):
+    """Bounded work items: every non-empty (block, row) segment becomes ceil(len / item_edges) items
+    (empty segments none); the aggregate and the attention form still match the oracle, and any
+    item length gives the same y to fp32 rounding (sum order changes only at part boundaries)."""
+    n, e, F, H = 600, 15000, 128, 8
+    g0 = G.synthetic(n, e, seed=11, device="cpu")
+    ip, ix = g0.numpy()
+    deg = np.diff(ip).copy()
+    deg[3], deg[4] = 4000, 700                                      # heavy rows: many parts per segment
+    deg[[10, 11]] = 0
+    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    rng = np.random.default_rng(item_edges % 1000 + blocks)
+    ix = np.concatenate([np.sort(rng.integers(0, n, d)) for d in deg]).astype(np.int32)
+    g = G.from_numpy(ip, ix, device=dev)
+    plan = g.blocked_plan(blocks, item_edges)
+    bsize = -(-n // blocks)
+    want = 0
+    for r in range(n):
+        seg = np.bincount(ix[ip[r]:ip[r + 1]] // bsize, minlength=blocks)
+        want += int(np.sum(-(-seg // item_edges)))
+    assert plan.n_items == want
+    x = rng.standard_normal((n, F)).astype(np.float32)
+    w = rng.random((len(ix), H)).astype(np.float32)
+    xd, wd = torch.from_numpy(x).to(dev), torch.from_numpy(w).to(dev)
+    y = ops.aggregate_blocked(g, xd, wd, plan=plan, blocks=blocks)
+    _check(y, isa_ref.aggregate(ip, ix, x, "src", w), isa_ref.aggregate_abs(ip, ix, x, "src", w),
+           f"blocked items={item_edges} B={blocks}")
+    assert torch.equal(y, ops.aggregate_blocked(g, xd, wd, plan=plan, blocks=blocks))
+    a = rng.standard_normal((n, H)).astype(np.float64)
+    b = rng.standard_normal((n, H)).astype(np.float64)
+    ya, sa = ops.gat_aggregate_blocked(g, xd, torch.from_numpy(a).float().to(dev), torch.from_numpy(b).float().to(dev),
+                                       want_sums=True, plan=plan, blocks=blocks)
+    ref, rsum = isa_ref.gat_aggregate(ip, ix, x.astype(np.float64), a, b, "EXP_LEAKY_RELU", True)
+    _check(sa, rsum, rsum, f"att sums items={item_edges}")
+    v, _ = isa_ref.edge_softmax(ip, ix, a, b, "EXP_LEAKY_RELU", False)
+    scale = isa_ref.aggregate(ip, ix, np.abs(x.astype(np.float64)), "src", v)
+    scale = scale / np.repeat(np.where(rsum > 0, rsum, 1.0), F // H, axis=1) * 4
+    _check(ya, ref, scale, f"att y items={item_edges}")
+
+
 def test_aggregate_blocked_accumulate_rowscale(dev):
     n, e, F = 500, 9000, 128
     g = G.synthetic(n, e, seed=3, device=dev)
