@@ -65,6 +65,11 @@ def make_inputs(n, e, device, seed=0):
     return g, x, alpha
 
 
+def grid_chunks(pc):
+    """Row chunks per rank tile: the reduce-scatter of chunk k overlaps chunk k+1's aggregate."""
+    return 1 if pc == 1 else 2
+
+
 def auto_blocks(graph, f):
     return ops.BlockedPlan.auto_blocks(graph, f)
 
@@ -161,14 +166,14 @@ def main():
         pr, pc = distributed.grid_shape(world) if args.grid == "auto" else map(int, args.grid.lower().split("x"))
         if pr * pc != world:
             raise SystemExit(f"--grid {pr}x{pc} does not match {world} ranks")
-        shard = distributed.GridShard(g, rank, pr, pc)
-        note(f"grid shard {shard.i},{shard.j}: {shard.graph.nnz} edges")
+        n_chunks = args.row_chunks or grid_chunks(pc)
+        shard = distributed.GridShard(g, rank, pr, pc, chunks=n_chunks)
+        note(f"grid shard {shard.i},{shard.j}: {shard.graph.nnz} edges, {n_chunks} row chunks")
         groups = distributed.row_groups(pr, pc)
         note("row groups ready")
         gl = shard.graph
         xl = x[shard.c0:shard.c1].contiguous()
         wl = alpha[shard.edge_ids].contiguous()
-        n_chunks = 1
     elif world > 1:
         n_chunks = args.row_chunks or 8
         if rs:
@@ -183,9 +188,13 @@ def main():
         n_chunks = args.row_chunks or 1
 
     def make_chunks(chunk):
-        if grid:  # one launch over the rank's whole tile
+        if grid:  # one launch per row chunk of the rank's tile (one launch over the tile at 1 chunk)
             c = partition.ChunkedRows.__new__(partition.ChunkedRows)
-            c.graph, c.parts = gl, [(0, gl.n_rows, gl, gl.plan(chunk) if chunk else None)]
+            c.graph, c.parts = gl, []
+            for k in range(shard.chunks):
+                r0, r1 = shard.chunk_rows(k)
+                gg = gl if shard.chunks == 1 else partition.sub_rows(gl, r0, r1)
+                c.parts.append((r0, r1, gg, gg.plan(chunk) if chunk else None))
             return c
         if not rs:
             return partition.ChunkedRows(gl, n_chunks=n_chunks, chunk=chunk)
@@ -212,7 +221,7 @@ def main():
     y = torch.empty(gl.n_rows if (rs or grid) else g.n_rows, F, device=dev)
     y_own = torch.empty(shard.chunks * shard.mk, F, device=dev) if rs else None  # this rank's reduced rows
     if grid:
-        y_own = torch.empty(shard.m, F, device=dev)
+        y_own = torch.empty(shard.out_rows(), F, device=dev)
         my_group = groups[shard.i]
     stream = torch.cuda.current_stream(dev)
 
@@ -222,15 +231,20 @@ def main():
         return ops.aggregate(gg, xx, "src", ww, out=out, plan=plan)
 
     def step():
-        if grid:
-            agg_chunk(gl, xl, wl, y, chunked.parts[0][3])
-            if pc == 1:
-                y_own.copy_(y[:shard.m])
-            elif backend == "nccl":  # RCCL reduce-scatter among the pc ranks of this row group
-                dist.reduce_scatter_tensor(y_own, y, group=my_group)
-            else:  # gloo (1-GPU rehearsal): no reduce-scatter
-                dist.all_reduce(y, group=my_group)
-                y_own.copy_(y[shard.j * shard.m:(shard.j + 1) * shard.m])
+        if grid:  # chunk k's reduce-scatter runs while chunk k+1 aggregates
+            mk, works = shard.mk, []
+            for k, (r0, r1, gg, plan) in enumerate(chunked.parts):
+                agg_chunk(gg, xl, wl, y[r0:r1], plan)
+                own = y_own[k * mk:(k + 1) * mk]
+                if pc == 1:
+                    own.copy_(y[r0:r1])
+                elif backend == "nccl":  # RCCL reduce-scatter among the pc ranks of this row group
+                    works.append(dist.reduce_scatter_tensor(own, y[r0:r1], group=my_group, async_op=True))
+                else:  # gloo (1-GPU rehearsal): no reduce-scatter
+                    dist.all_reduce(y[r0:r1], group=my_group)
+                    own.copy_(y[r0 + shard.j * mk:r0 + (shard.j + 1) * mk])
+            for wk in works:
+                wk.wait()
             return
         if not rs:
             partition.distributed_aggregate(chunked, xl, wl, y, aggregate_fn=agg_chunk)
@@ -288,9 +302,9 @@ def main():
     if world > 1:
         ref = ops.aggregate(g, x, "src", alpha, plan=args.chunk)
         if grid:  # reassemble Y from every rank's reduced rows (row groups may differ in m: pad)
-            mmax = max(-(-(shard.rcuts[i + 1] - shard.rcuts[i]) // pc) for i in range(pr))
+            mmax = max(len(shard.owned_rows(q)) for q in range(world))
             mine = torch.zeros(mmax, F, device=dev)
-            mine[:shard.m] = y_own
+            mine[:y_own.shape[0]] = y_own
             parts = [torch.empty_like(mine) for _ in range(world)]
             dist.all_gather(parts, mine)
             full = torch.empty_like(ref)

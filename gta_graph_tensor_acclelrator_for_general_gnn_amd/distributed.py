@@ -178,9 +178,15 @@ class GridShard:
     (nnz-balanced row cuts) and whose source lies in column block j (nnz-balanced column cuts),
     as a CSR over row block i's rows with local column ids.  The pc ranks of row group i sum their
     partial aggregates with one reduce-scatter: rank (i, j) ends with rows
-    R_i + j*m .. R_i + (j+1)*m of the block (m = ceil(n_i / pc); the CSR is padded to pc*m rows)."""
+    R_i + j*m .. R_i + (j+1)*m of the block (m = ceil(n_i / pc); the CSR is padded to pc*m rows).
 
-    def __init__(self, graph, rank, pr, pc):
+    chunks = C > 1 lays the padded rows out chunk-major so the exchange can overlap the compute:
+    row R_i + j*m + c*mk + v (mk = ceil(m / C)) sits at padded row c*pc*mk + j*mk + v, so chunk c
+    is the contiguous [pc*mk] range holding one mk-row part per rank of the group -- one
+    reduce-scatter per chunk, issued while chunk c+1 aggregates.  Rank j's output is then
+    [C*mk] rows, part c at c*mk (owned_rows gives their global ids)."""
+
+    def __init__(self, graph, rank, pr, pc, chunks=1):
         self.pr, self.pc, self.rank = pr, pc, rank
         self.i, self.j = divmod(rank, pc)
         dev = graph.device
@@ -193,24 +199,47 @@ class GridShard:
         c0, c1 = self.ccuts[self.j], self.ccuts[self.j + 1]
         self.r0, self.r1, self.c0, self.c1 = r0, r1, c0, c1
         self.m = -(-(r1 - r0) // pc)
+        self.chunks = max(1, int(chunks))
+        self.mk = -(-self.m // self.chunks)
         e0, e1 = int(ip[r0]), int(ip[r1])
         src = graph.indices[e0:e1]
         keep = (src >= c0) & (src < c1)
         deg = ip[r0 + 1:r1 + 1] - ip[r0:r1]
         rows = torch.repeat_interleave(torch.arange(r1 - r0, device=dev), deg)[keep]
-        counts = torch.bincount(rows, minlength=pc * self.m)
-        indptr = torch.zeros(pc * self.m + 1, dtype=torch.int64, device=dev)
-        indptr[1:] = torch.cumsum(counts, 0)
-        self.graph = Graph(indptr, (src[keep].long() - c0).to(torch.int32), n_cols=c1 - c0)
+        local_src = (src[keep].long() - c0).to(torch.int32)
         self.edge_ids = torch.nonzero(keep, as_tuple=False).flatten() + e0
+        if self.chunks > 1:  # chunk-major padded rows; a stable sort keeps each row's edge order
+            jj, u = rows // self.m, rows % self.m
+            rows = (u // self.mk) * (pc * self.mk) + jj * self.mk + u % self.mk
+            order = torch.sort(rows, stable=True).indices
+            rows, local_src, self.edge_ids = rows[order], local_src[order], self.edge_ids[order]
+        n_pad = self.chunks * pc * self.mk
+        counts = torch.bincount(rows, minlength=n_pad)
+        indptr = torch.zeros(n_pad + 1, dtype=torch.int64, device=dev)
+        indptr[1:] = torch.cumsum(counts, 0)
+        self.graph = Graph(indptr, local_src, n_cols=c1 - c0)
+
+    def chunk_rows(self, c):
+        """Padded row range [a, b) of chunk c: the input of its reduce-scatter."""
+        w = self.pc * self.mk
+        return c * w, (c + 1) * w
+
+    def out_rows(self):
+        """Rows of this rank's reduce-scatter output (chunks * mk; = m when chunks == 1)."""
+        return self.m if self.chunks == 1 else self.chunks * self.mk
 
     def owned_rows(self, rank):
-        """Global row ids of `rank`'s reduce-scatter output ([m] rows; -1 = padding)."""
+        """Global row ids of `rank`'s reduce-scatter output ([out_rows] rows; -1 = padding)."""
         i, j = divmod(rank, self.pc)
         r0, r1 = self.rcuts[i], self.rcuts[i + 1]
         m = -(-(r1 - r0) // self.pc)
-        t = torch.arange(m) + r0 + j * m
-        return torch.where(t < r1, t, torch.full_like(t, -1))
+        if self.chunks == 1:
+            t = torch.arange(m) + r0 + j * m
+            return torch.where(t < r1, t, torch.full_like(t, -1))
+        mk = -(-m // self.chunks)
+        u = torch.arange(self.chunks * mk)  # c*mk + v
+        t = r0 + j * m + u
+        return torch.where((u < m) & (t < r1), t, torch.full_like(t, -1))
 
 
 def row_groups(pr, pc):

@@ -19,7 +19,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 import bench  # noqa: E402
-from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, ops  # noqa: E402
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, ops, partition  # noqa: E402
 
 UNBOUNDED = 1 << 30
 
@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--grids", default="1x1")
     ap.add_argument("--items", default="64,128,256,512,0")
     ap.add_argument("--blocks", default="0", help="comma list; 0 = bench's auto choice for the tile")
+    ap.add_argument("--chunks", default="1", help="comma list of row chunks per tile (one launch per chunk, "
+                                                   "chunk-major padded rows as bench.py --row-chunks)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--n", type=int, default=bench.N_REDDIT)
@@ -41,25 +43,29 @@ def main():
     out = {}
     for grid in args.grids.split(","):
         pr, pc = map(int, grid.lower().split("x"))
-        if pr * pc == 1:
-            gg, xl, wl = g, x, alpha
-        else:
-            s = distributed.GridShard(g, 0, pr, pc)
-            gg, xl, wl = s.graph, x[s.c0:s.c1].contiguous(), alpha[s.edge_ids].contiguous()
-        y = torch.empty(gg.n_rows, bench.F, device=dev)
         variants = []
-        for b in args.blocks.split(","):
-            B = int(b) or bench.auto_blocks(gg, bench.F)
-            for it in args.items.split(","):
-                ie = int(it) or UNBOUNDED
-                plan = gg.blocked_plan(B, ie)
-                variants.append((f"{grid}:B{B}:i{it}", B, plan))
+        for ch in map(int, args.chunks.split(",")):
+            if pr * pc == 1 and ch == 1:
+                gg, xl, wl, parts = g, x, alpha, [(0, g.n_rows)]
+            else:
+                s = distributed.GridShard(g, 0, pr, pc, chunks=ch)
+                gg, xl, wl = s.graph, x[s.c0:s.c1].contiguous(), alpha[s.edge_ids].contiguous()
+                parts = [s.chunk_rows(c) for c in range(s.chunks)]
+            subs = [gg if len(parts) == 1 else partition.sub_rows(gg, a, b) for a, b in parts]
+            y = torch.empty(gg.n_rows, bench.F, device=dev)
+            for b in args.blocks.split(","):
+                B = int(b) or bench.auto_blocks(gg, bench.F)
+                for it in args.items.split(","):
+                    ie = int(it) or UNBOUNDED
+                    plans = [sg.blocked_plan(B, ie) for sg in subs]
+                    variants.append((f"{grid}:c{ch}:B{B}:i{it}", B, plans, subs, parts, gg, xl, wl, y))
         times = {v[0]: [] for v in variants}
-        ref = None
+        ref = {}
         for r in range(args.rounds):
-            for name, B, plan in variants:
+            for name, B, plans, subs, parts, gg, xl, wl, y in variants:
                 def run():
-                    ops.aggregate_blocked(gg, xl, wl, out=y, plan=plan, blocks=B)
+                    for (a, b), sg, plan in zip(parts, subs, plans):
+                        ops.aggregate_blocked(sg, xl, wl, out=y[a:b], plan=plan, blocks=B)
                 run()
                 a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 a.record()
@@ -68,21 +74,23 @@ def main():
                 e.record()
                 torch.cuda.synchronize()
                 times[name].append(a.elapsed_time(e) / args.reps)
-                if r == 0:
-                    if ref is None:
-                        ref = y.clone()
+                if r == 0:  # same sums per layout (chunked layouts differ only in padded row order)
+                    key = len(parts)
+                    if key not in ref:
+                        ref[key] = y.clone()
                     else:
-                        d = (y - ref).abs().max().item()
+                        d = (y - ref[key]).abs().max().item()
                         assert d < 1e-3, f"variant {name} differs from the first by {d}"
-        ab = bench.alg_bytes(gg.n_rows, gg.nnz)
-        for name, B, plan in variants:
+        for name, B, plans, subs, parts, gg, xl, wl, y in variants:
+            ab = bench.alg_bytes(gg.n_rows, gg.nnz)
             med = float(np.median(times[name]))
-            out[name] = {"rows": gg.n_rows, "edges": gg.nnz, "items": plan.n_items, "median_ms": med,
-                         "min_ms": float(np.min(times[name])), "alg_GBps": ab / (med / 1e3) / 1e9,
-                         "edges_per_s": gg.nnz / (med / 1e3)}
-            print(f"{name:18s} items {plan.n_items:9d}  median {med:7.3f} ms  min {out[name]['min_ms']:7.3f}  "
+            n_items = sum(p.n_items for p in plans)
+            out[name] = {"rows": gg.n_rows, "edges": gg.nnz, "items": n_items, "launches": len(plans),
+                         "median_ms": med, "min_ms": float(np.min(times[name])),
+                         "alg_GBps": ab / (med / 1e3) / 1e9, "edges_per_s": gg.nnz / (med / 1e3)}
+            print(f"{name:22s} items {n_items:9d}  median {med:7.3f} ms  min {out[name]['min_ms']:7.3f}  "
                   f"{out[name]['alg_GBps']:7.0f} GB/s alg  {out[name]['edges_per_s'] / 1e9:6.2f} Gedges/s", flush=True)
-        del gg, xl, wl, y, variants
+        del variants
         torch.cuda.empty_cache()
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "item_sweep.json"), "w") as f:

@@ -139,7 +139,7 @@ def test_chunk_major_shard_layout(world, chunks):
     assert total == g.nnz
 
 
-def _grid_worker(rank, world, pr, pc, port, q):
+def _grid_worker(rank, world, pr, pc, port, q, chunks=1):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -149,16 +149,22 @@ def _grid_worker(rank, world, pr, pc, port, q):
         gen = torch.Generator().manual_seed(3)
         x = torch.randn(600, 16, generator=gen)
         w = torch.rand(g.nnz, 4, generator=gen)
-        s = distributed.GridShard(g, rank, pr, pc)
+        s = distributed.GridShard(g, rank, pr, pc, chunks=chunks)
         groups = distributed.row_groups(pr, pc)
         sip, six = s.graph.numpy()
         y = torch.from_numpy(isa_ref.aggregate(sip, six, x[s.c0:s.c1].numpy(), "src",
                                                w[s.edge_ids].numpy()).astype(np.float32))
-        dist.all_reduce(y, group=groups[s.i])  # the bench's gloo stand-in for the reduce-scatter
-        own = y[s.j * s.m:(s.j + 1) * s.m].contiguous()
-        mmax = max(-(-(s.rcuts[i + 1] - s.rcuts[i]) // pc) for i in range(pr))
+        own = []
+        for c in range(s.chunks):  # one reduce-scatter per chunk (gloo stand-in: all-reduce + slice)
+            a, b = s.chunk_rows(c)
+            yc = y[a:b].contiguous()
+            dist.all_reduce(yc, group=groups[s.i])
+            own.append(yc[s.j * s.mk:(s.j + 1) * s.mk])
+        own = torch.cat(own)
+        assert own.shape[0] == s.out_rows()
+        mmax = max(len(s.owned_rows(r)) for r in range(world))
         mine = torch.zeros(mmax, 16)
-        mine[:s.m] = own
+        mine[:own.shape[0]] = own
         parts = [torch.empty_like(mine) for _ in range(world)]
         dist.all_gather(parts, mine)
         if rank == 0:
@@ -174,15 +180,16 @@ def _grid_worker(rank, world, pr, pc, port, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("pr,pc", [(2, 2), (1, 2), (3, 1)])
-def test_grid_tiles_reduce_scatter_gloo(pr, pc):
-    """bench.py's 2-D layout: row-group partial sums, reassembled from every rank's owned rows,
-    equal the single-device aggregate."""
+@pytest.mark.parametrize("pr,pc,chunks", [(2, 2, 1), (1, 2, 1), (3, 1, 1), (2, 2, 3), (1, 2, 2)])
+def test_grid_tiles_reduce_scatter_gloo(pr, pc, chunks):
+    """bench.py's 2-D layout: row-group partial sums (one reduce-scatter, or one per chunk of the
+    chunk-major padded rows), reassembled from every rank's owned rows, equal the single-device
+    aggregate."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
     world = pr * pc
-    procs = [ctx.Process(target=_grid_worker, args=(r, world, pr, pc, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=_grid_worker, args=(r, world, pr, pc, port, q, chunks)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
