@@ -34,7 +34,7 @@ SIGNATURES = {
     "gta_aggregate_plan_build": (_i32, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
     "gta_aggregate_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
     "gta_aggregate_blocked_plan_bytes": (_i64, [_i64, _i64, _i64, _i64]),
-    "gta_aggregate_blocked_plan_build": (_i32, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp]),
+    "gta_aggregate_blocked_plan_build": (_i32, [_vp, _vp, _i64, _i64, _i64, _i64, _i64, _i64, _vp, _i64, _vp]),
     "gta_aggregate_blocked_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64, _i64]),
     "gta_aggregate_blocked": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _i64,
                                      _i32, _vp, _i64, _i64, _vp, _vp]),

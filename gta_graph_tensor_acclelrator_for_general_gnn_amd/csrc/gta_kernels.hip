@@ -808,6 +808,113 @@ k_agg_seg4(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_it
   }
 }
 
+// Lean half-wave form of k_agg_seg4 for F = 128 fp32 (the metric shape): two items
+// per wave, 32 lanes x float4 each, 8 edges per step.  What it removes from the
+// per-edge instruction stream of the generic form:
+//  * 64-bit address arithmetic: a source row is addressed as the uniform base x plus
+//    a 32-bit byte offset src * row_bytes (v_mul_u32_u24; the host checks the
+//    gathered table spans < 2^32 bytes and n_cols < 2^24), so the load takes the
+//    SGPR-base + VGPR-offset form;
+//  * per-edge exec masking: a step where BOTH items still hold 8 edges (wave-uniform
+//    test against the shorter item) runs unmasked; only the tail steps are masked;
+//  * per-edge weight loads (8 heads, 4 lanes per head, WEIGHTED): lane (h, q) loads
+//    alpha[e + 2q][h] and alpha[e + 2q + 1][h] -- two dword loads per step -- and edge
+//    u's weight reaches its head's 4 lanes by a DPP quad broadcast from quad lane u/2.
+// Same per-lane edge order and fma chain as k_agg_seg4: results bitwise equal to it.
+template <int SEL>
+__device__ __forceinline__ float quad_bcast(float v) {  // lane (l & ~3) | SEL of each quad
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), SEL * 0x55, 0xF, 0xF, false));
+}
+
+template <bool WEIGHTED, int NT>
+__global__ void __launch_bounds__(kBlock)
+k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
+          uint32_t row_bytes, const float* __restrict__ w, int64_t ldw, float* __restrict__ slabs,
+          const SegItem* __restrict__ items) {
+  constexpr int G = 32, F = 128, U = 8;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int l32 = lane & (G - 1);
+  const int64_t k = (static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform()) * 2 + (lane >> 5);
+  const int64_t n_items = *n_items_p;
+  SegItem it{0, 0, 0};
+  if (k < n_items) it = items[k];
+  const int len = it.len;
+  const int other = __shfl_xor(len, 32);
+  const int maxlen = __builtin_amdgcn_readfirstlane(max(len, other));
+  const int minlen = __builtin_amdgcn_readfirstlane(min(len, other));
+  if (maxlen == 0) return;
+  const uint32_t colb = static_cast<uint32_t>(l32) * 16u;
+  const char* xb = reinterpret_cast<const char*>(x);
+  const int h = l32 >> 2, q = l32 & 3;
+  const int ldw32 = static_cast<int>(ldw);
+  // chunk cursors: advanced once per 32 edges, so no per-edge 64-bit offsets are live
+  const int32_t* ic = indices + it.beg;
+  const float* wc = WEIGHTED ? w + it.beg * ldw + h : nullptr;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  auto ldi = [&](const int32_t* p) { return (NT & 1) ? __builtin_nontemporal_load(p) : *p; };
+  auto ldw_ = [&](const float* p) { return (NT & 1) ? __builtin_nontemporal_load(p) : *p; };
+  auto row = [&](int src) -> float4 {
+    return *reinterpret_cast<const float4*>(xb + (__umul24(static_cast<uint32_t>(src), row_bytes) + colb));
+  };
+  int idxv = (l32 < len) ? ldi(ic + l32) : 0;
+  for (int c = 0; c < maxlen; c += G) {
+    const int idxn = (c + G + l32 < len) ? ldi(ic + G + l32) : 0;
+#pragma unroll
+    for (int s = 0; s < G; s += U) {
+      if (c + s >= maxlen) break;
+      float4 xv[U];
+      float wu[U];
+      if (c + s + U <= minlen) {  // full step for both items: no masks
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[u] = row(bcastG<G>(idxv, s + u));
+        if (WEIGHTED) {
+          const float* wp = wc + (s + 2 * q) * ldw32;
+          const float w0 = ldw_(wp), w1 = ldw_(wp + ldw32);
+          wu[0] = quad_bcast<0>(w0); wu[1] = quad_bcast<0>(w1);
+          wu[2] = quad_bcast<1>(w0); wu[3] = quad_bcast<1>(w1);
+          wu[4] = quad_bcast<2>(w0); wu[5] = quad_bcast<2>(w1);
+          wu[6] = quad_bcast<3>(w0); wu[7] = quad_bcast<3>(w1);
+        }
+      } else {
+        const int rem = len - c - s;  // edges of this item left at this step (may be <= 0)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int src = bcastG<G>(idxv, s + u);
+          if (u < rem) {
+            xv[u] = row(src);
+            if (WEIGHTED) wu[u] = ldw_(wc + (s + u) * ldw32);
+          } else {
+            xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (WEIGHTED) wu[u] = 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (WEIGHTED) {
+          acc[0] = fmaf(wu[u], xv[u].x, acc[0]);
+          acc[1] = fmaf(wu[u], xv[u].y, acc[1]);
+          acc[2] = fmaf(wu[u], xv[u].z, acc[2]);
+          acc[3] = fmaf(wu[u], xv[u].w, acc[3]);
+        } else {
+          acc[0] += xv[u].x; acc[1] += xv[u].y; acc[2] += xv[u].z; acc[3] += xv[u].w;
+        }
+      }
+    }
+    idxv = idxn;
+    ic += G;
+    if (WEIGHTED) wc += static_cast<int64_t>(G) * ldw;
+  }
+  if (len > 0) {
+    float* o = slabs + k * F + l32 * 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (NT & 2) __builtin_nontemporal_store(acc[t], o + t);
+      else o[t] = acc[t];
+    }
+  }
+}
+
 // The row's slab rows (item ids row_items[row_ptr[row] .. row_ptr[row+1]), in
 // (block, part) order) summed in that order; ids arrive 64 at a time with one
 // coalesced load and are broadcast by readlane, 4 slab loads in flight.
@@ -918,8 +1025,14 @@ k_seg_reduce_att(int64_t n_rows, const float* __restrict__ slabs, int H, int nor
 // outlasts the rest of the launch (a Reddit row holds up to ~2.4e4 edges).  Item k
 // writes slab row k; row_items lists each row's items in (block, part) order, the
 // fixed order of the ordered reduce.
+// Light rows merge blocks (row_edges > 0): a row of deg edges uses blocks of
+// m = pow2 >= row_edges * B / deg fine blocks (m <= B), so its items still average
+// ~row_edges edges instead of deg / B -- each item costs a start-up and a 512-B
+// partial written and re-read, whatever its length.  A merged block is scheduled at
+// its first fine block's position.
 // layout (host-computable offsets first, then the item arrays):
-//   int64 hdr[8] {B, bsize, n_rows, unsorted_flag, n_items, item_edges, max_items, row_items byte offset}
+//   int64 hdr[16] {B, bsize, n_rows, unsorted_flag, n_items, item_edges, max_items, row_items byte offset,
+//                  row_edges}
 //   int32 perm[n_rows]             rows, heaviest degree bucket first
 //   int32 seg[n_rows*(B+1)]        per-row segment offsets
 //   int32 bucket[64]               (count, offset) per degree bucket
@@ -943,14 +1056,14 @@ inline int64_t blocked_max_items(int64_t n_rows, int64_t nnz, int B, int64_t ite
 }
 
 inline int64_t blocked_fixed_bytes(int64_t n_rows, int B) {
-  return round16(64) + round16(n_rows * 4) + round16(n_rows * (B + 1) * 4) + round16(64 * 4) +
+  return round16(128) + round16(n_rows * 4) + round16(n_rows * (B + 1) * 4) + round16(64 * 4) +
          round16((n_rows + 1) * 8) + round16(n_rows * B * 4);
 }
 
 BlockedView blocked_view(void* base, int64_t n_rows, int B, int64_t max_items) {
   char* p = static_cast<char*>(base);
   BlockedView v;
-  v.hdr = reinterpret_cast<int64_t*>(p); p += round16(8 * 8);
+  v.hdr = reinterpret_cast<int64_t*>(p); p += round16(16 * 8);
   v.perm = reinterpret_cast<int32_t*>(p); p += round16(n_rows * 4);
   v.seg = reinterpret_cast<int32_t*>(p); p += round16(n_rows * (B + 1) * 4);
   v.bucket = reinterpret_cast<int32_t*>(p); p += round16(64 * 4);
@@ -973,12 +1086,20 @@ __host__ __device__ __forceinline__ int64_t n_parts(int64_t len, int64_t item_ed
   return (len + item_edges - 1) / item_edges;
 }
 
+// fine blocks per merged block of a row with deg edges (1 = no merging)
+__device__ __forceinline__ int merge_of(int64_t deg, int B, int64_t row_edges) {
+  if (row_edges <= 0 || deg <= 0) return 1;
+  int m = 1;
+  while (m < B && deg * m < row_edges * B) m <<= 1;
+  return m;
+}
+
 // one wave per row: lane b (0..B) binary-searches the first edge with col >= b*bsize;
 // all lanes also verify the row's columns are sorted (the segments need it).  Also
 // writes the row's item count (sum over blocks of n_parts) into row_ptr[row].
 __global__ void __launch_bounds__(kBlock)
 k_blocked_seg(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows, int B,
-              int64_t bsize, int64_t item_edges, BlockedView v) {
+              int64_t bsize, int64_t item_edges, int64_t row_edges, BlockedView v) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
   if (row >= n_rows) return;
@@ -994,9 +1115,12 @@ k_blocked_seg(const int64_t* __restrict__ indptr, const int32_t* __restrict__ in
     pos = (b == B ? re : lo) - rb;
     v.seg[row * (B + 1) + b] = static_cast<int32_t>(pos);
   }
-  // B <= 63: lane b holds offset b; lane b's segment is [pos_b, pos_{b+1})
-  const int64_t nxt = __shfl_down(pos, 1);
-  int64_t parts = (lane < B) ? n_parts(nxt - pos, item_edges) : 0;
+  // B <= 63: lane b holds offset b; lane j's merged block is [pos_{j*m}, pos_{min((j+1)*m, B)})
+  const int m = merge_of(re - rb, B, row_edges);
+  const int nb = (B + m - 1) / m;
+  const int64_t lo = __shfl(pos, min(lane * m, B));
+  const int64_t hi = __shfl(pos, min((lane + 1) * m, B));
+  int64_t parts = (lane < nb) ? n_parts(hi - lo, item_edges) : 0;
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) parts += __shfl_xor(parts, off);
   if (lane == 0) v.row_ptr[row] = parts;
@@ -1024,14 +1148,16 @@ __global__ void k_blocked_perm(const int64_t* __restrict__ indptr, int64_t n_row
   v.perm[pos] = static_cast<int32_t>(r);
 }
 
-// cnt[k] = items of (block b = k / n_rows, row perm[k % n_rows])
-__global__ void k_blocked_cnt(int64_t n_rows, int B, int64_t item_edges, BlockedView v) {
+// cnt[k] = items of (block b = k / n_rows, row perm[k % n_rows]): the parts of the row's
+// merged block starting at fine block b, 0 if none starts there
+__global__ void k_blocked_cnt(int64_t n_rows, int B, int64_t item_edges, int64_t row_edges, BlockedView v) {
   const int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (k >= n_rows * B) return;
   const int b = static_cast<int>(k / n_rows);
   const int32_t row = v.perm[k - static_cast<int64_t>(b) * n_rows];
   const int32_t* sg = v.seg + static_cast<int64_t>(row) * (B + 1);
-  v.cnt[k] = static_cast<int32_t>(n_parts(sg[b + 1] - sg[b], item_edges));
+  const int m = merge_of(sg[B], B, row_edges);
+  v.cnt[k] = (b % m) ? 0 : static_cast<int32_t>(n_parts(sg[min(b + m, B)] - sg[b], item_edges));
 }
 
 // single-workgroup in-place exclusive scan (plan build only); out[n] = total when
@@ -1069,16 +1195,18 @@ __global__ void __launch_bounds__(1024) k_scan_excl(T* __restrict__ a, int64_t n
 // cnt[k] .. cnt[k] + parts - 1; each is also listed under its row, after the row's
 // items of blocks < b
 __global__ void k_blocked_items(const int64_t* __restrict__ indptr, int64_t n_rows, int B, int64_t item_edges,
-                                BlockedView v) {
+                                int64_t row_edges, BlockedView v) {
   const int64_t k = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
   if (k >= n_rows * B) return;
   const int b = static_cast<int>(k / n_rows);
   const int32_t row = v.perm[k - static_cast<int64_t>(b) * n_rows];
   const int32_t* sg = v.seg + static_cast<int64_t>(row) * (B + 1);
-  const int64_t len = sg[b + 1] - sg[b];
+  const int m = merge_of(sg[B], B, row_edges);
+  if (b % m) return;
+  const int64_t len = sg[min(b + m, B)] - sg[b];
   if (len == 0) return;
-  int64_t before = 0;  // the row's items in blocks < b
-  for (int q = 0; q < b; ++q) before += n_parts(sg[q + 1] - sg[q], item_edges);
+  int64_t before = 0;  // the row's items in merged blocks before b
+  for (int q = 0; q < b; q += m) before += n_parts(sg[min(q + m, B)] - sg[q], item_edges);
   const int64_t parts = n_parts(len, item_edges), part = (len + parts - 1) / parts;
   const int64_t id0 = v.cnt[k], slot0 = v.row_ptr[row] + before, beg = indptr[row] + sg[b];
   for (int64_t j = 0; j < parts; ++j) {
@@ -1840,6 +1968,7 @@ int g_seg_quarter = 1;     // quarter-wave (4 items per wave) form of the blocke
 int g_seg_lanes = 32;      // lanes per item of that form at F = 128: 32 (2 items/wave, measured 3 % faster) or 16
 int g_seg_nt = 2;          // non-temporal bits of the multi-item forms at F = 128, U = 8: 2 = slab stores (-1 %)
 int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
+int g_seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
 int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
 int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
 int g_apply_edge_form = 1;  // 1: row-sweep K3 kernels (cols / pack); 0: the generic per-element kernel
@@ -1867,6 +1996,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "seg_nt") { g_seg_nt = static_cast<int>(value); return 0; }
   if (k == "seg_u") { g_seg_u = static_cast<int>(value); return 0; }
   if (k == "seg_lanes") { g_seg_lanes = static_cast<int>(value); return 0; }
+  if (k == "seg_lean") { g_seg_lean = static_cast<int>(value); return 0; }
   if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
   if (k == "mm_prefetch") { g_mm_prefetch = static_cast<int>(value); return 0; }
   if (k == "mm_blocks_per_cu") { g_mm_blocks_per_cu = value; return 0; }
@@ -2012,9 +2142,10 @@ int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t nnz, int64_t bl
 }
 
 int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
-                                     int64_t nnz, int64_t blocks, int64_t item_edges, void* plan, int64_t plan_bytes,
-                                     void* stream) {
-  if (!indptr || !plan || n_rows <= 0 || n_cols <= 0 || nnz < 0 || blocks < 1 || blocks > 63 || item_edges < 1)
+                                     int64_t nnz, int64_t blocks, int64_t item_edges, int64_t row_edges, void* plan,
+                                     int64_t plan_bytes, void* stream) {
+  if (!indptr || !plan || n_rows <= 0 || n_cols <= 0 || nnz < 0 || blocks < 1 || blocks > 63 || item_edges < 1 ||
+      row_edges < 0)
     return fail(GTA_ERR_ARG, "blocked_plan_build: bad arguments");
   if (nnz > 0 && !indices) return fail(GTA_ERR_ARG, "blocked_plan_build: indices needed");
   if (n_rows > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "blocked_plan_build: > 2^31 rows");
@@ -2025,12 +2156,12 @@ int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indic
   BlockedView v = blocked_view(plan, n_rows, B, mi);
   hipStream_t s = S(stream);
   const int64_t bsize = (n_cols + B - 1) / B;
-  const int64_t hdr[8] = {B, bsize, n_rows, 0, 0, item_edges, mi,
-                          reinterpret_cast<char*>(v.row_items) - static_cast<char*>(plan)};
+  const int64_t hdr[16] = {B, bsize, n_rows, 0, 0, item_edges, mi,
+                           reinterpret_cast<char*>(v.row_items) - static_cast<char*>(plan), row_edges};
   GTA_HIP(hipMemcpyAsync(v.hdr, hdr, sizeof(hdr), hipMemcpyHostToDevice, s));
   GTA_HIP(hipMemsetAsync(v.bucket, 0, 64 * 4, s));
   k_blocked_seg<<<dim3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock)), dim3(kBlock), 0, s>>>(
-      indptr, indices, n_rows, B, bsize, item_edges, v);
+      indptr, indices, n_rows, B, bsize, item_edges, row_edges, v);
   GTA_LAUNCHED("k_blocked_seg");
   k_blocked_scan<<<1, 64, 0, s>>>(v);
   GTA_LAUNCHED("k_blocked_scan");
@@ -2039,11 +2170,11 @@ int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indic
   k_scan_excl<int64_t><<<1, 1024, 0, s>>>(v.row_ptr, n_rows, 1, nullptr);  // items per row -> row_ptr
   GTA_LAUNCHED("k_scan_excl");
   const dim3 gk(static_cast<unsigned>((n_rows * B + 255) / 256));
-  k_blocked_cnt<<<gk, dim3(256), 0, s>>>(n_rows, B, item_edges, v);
+  k_blocked_cnt<<<gk, dim3(256), 0, s>>>(n_rows, B, item_edges, row_edges, v);
   GTA_LAUNCHED("k_blocked_cnt");
   k_scan_excl<int32_t><<<1, 1024, 0, s>>>(v.cnt, n_rows * B, 0, &v.hdr[4]);  // -> first item id, n_items
   GTA_LAUNCHED("k_scan_excl");
-  k_blocked_items<<<gk, dim3(256), 0, s>>>(indptr, n_rows, B, item_edges, v);
+  k_blocked_items<<<gk, dim3(256), 0, s>>>(indptr, n_rows, B, item_edges, row_edges, v);
   GTA_LAUNCHED("k_blocked_items");
   return GTA_OK;
 }
@@ -2106,7 +2237,17 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
       if (vq == 8 && g_seg_lanes == 32) {  // half-wave items: 32 lanes x float4
         const int lph32 = w ? static_cast<int>((F / heads) / 4) : 0;
         const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
-        if (w && lph32 >= 1 && 32 % lph32 == 0 && (F / heads) % 4 == 0) {
+        const bool lean = g_seg_lean && g_seg_u == 8 && n_cols < (1 << 24) &&
+                          static_cast<uint64_t>(n_cols) * static_cast<uint64_t>(ldx) * 4u < (1ull << 32) &&
+                          (!w || lph32 == 4);
+        const uint32_t rb = static_cast<uint32_t>(ldx * 4);
+        if (lean) {
+          if (!w && g_seg_nt == 2) k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (!w) k_agg_h32<false, 0><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (g_seg_nt == 2) k_agg_h32<true, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (g_seg_nt == 1) k_agg_h32<true, 1><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else k_agg_h32<true, 0><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+        } else if (w && lph32 >= 1 && 32 % lph32 == 0 && (F / heads) % 4 == 0) {
           if (g_seg_u == 4)
             k_agg_seg4<4, 4, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                          lph32, slabs, its);

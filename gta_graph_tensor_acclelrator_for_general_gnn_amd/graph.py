@@ -69,13 +69,15 @@ class Graph:
             self._plans[chunk] = ops.AggregatePlan(self, chunk)
         return self._plans[chunk]
 
-    def blocked_plan(self, blocks=32, item_edges=None):
+    def blocked_plan(self, blocks=32, item_edges=None, row_edges=None):
         """Cached column-blocked plan (segment table over `blocks` source-column blocks, work items
-        of <= item_edges edges; None = ops.BlockedPlan.ITEM_EDGES)."""
+        of <= item_edges edges, light rows' blocks merged toward row_edges edges per item; None =
+        the ops.BlockedPlan defaults)."""
         from . import ops
-        key = ("blocked", blocks, int(item_edges or ops.BlockedPlan.ITEM_EDGES))
+        key = ("blocked", blocks, int(item_edges or ops.BlockedPlan.ITEM_EDGES),
+               int(ops.BlockedPlan.ROW_EDGES if row_edges is None else row_edges))
         if key not in self._plans:
-            self._plans[key] = ops.BlockedPlan(self, blocks, key[2])
+            self._plans[key] = ops.BlockedPlan(self, blocks, key[2], key[3])
         return self._plans[key]
 
     def numpy(self):

@@ -146,18 +146,21 @@ class BlockedPlan:
     segment cut into parts of <= item_edges edges -- with each row's item list for the ordered
     reduce."""
 
-    ITEM_EDGES = 256  # default part length (bench sweep: profiles/r01_agg_sweep_items.json)
+    ITEM_EDGES = 256  # default part length (profiles/r01_item_sweep.json)
+    ROW_EDGES = 0     # default merge target for light rows (0 = off)
 
-    def __init__(self, graph, blocks=32, item_edges=None):
+    def __init__(self, graph, blocks=32, item_edges=None, row_edges=None):
         _need_gpu(graph.indptr)
         L = _L()
         self.graph, self.blocks = graph, int(blocks)
         self.item_edges = int(item_edges or BlockedPlan.ITEM_EDGES)
+        self.row_edges = int(BlockedPlan.ROW_EDGES if row_edges is None else row_edges)
         nb = check(L.gta_aggregate_blocked_plan_bytes(graph.n_rows, graph.nnz, self.blocks, self.item_edges),
                    "blocked_plan_bytes")
         self.buf = torch.empty(int(nb), dtype=torch.uint8, device=graph.device)
         check(L.gta_aggregate_blocked_plan_build(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols,
-                                                 graph.nnz, self.blocks, self.item_edges, _ptr(self.buf), int(nb),
+                                                 graph.nnz, self.blocks, self.item_edges, self.row_edges,
+                                                 _ptr(self.buf), int(nb),
                                                  _stream(graph.device)),
               "blocked_plan_build")
         hdr = self.buf[:64].view(torch.int64).cpu()
@@ -195,14 +198,15 @@ class BlockedPlan:
 
     @staticmethod
     def auto_blocks(graph, F):
-        """Column blocks for a gathered table of graph.n_cols x F fp32: slices of ~7.5 MB (the
-        measured optimum on the 1-GPU Reddit shape was B = 16 for a 119 MB table, profiles/
-        r01_agg_sweep_*), capped so a row keeps >= 24 edges per block on average (each
-        (block, row) item pays a fixed start-up; an 8-GPU Reddit shard's rows hold ~61 edges).
+        """Column blocks for a gathered table of graph.n_cols x F fp32: slices of ~6 MB (measured
+        optima with the lean half-wave kernel: B = 20 for the 119 MB Reddit table, B = 10 for the
+        60 MB column half of a 2-D grid tile; profiles/r01_blocks_rowmerge_sweep.json,
+        r01_shard_b_sweep.json), capped so a row keeps >= 24 edges per block on average (each
+        (block, row) item pays a start-up and a partial row written and re-read).
         Below 4 the single-pass row-chunk kernel is the better choice."""
         table_mb = graph.n_cols * F * 4 / 1e6
         avg_deg = graph.nnz / max(1, graph.n_rows)
-        return int(max(1, min(16, round(table_mb / 7.5), avg_deg // 24)))
+        return int(max(1, min(24, round(table_mb / 6.0), avg_deg // 24)))
 
     @staticmethod
     def supports(F, heads, x=None):

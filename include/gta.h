@@ -123,11 +123,16 @@ int64_t gta_aggregate_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t chunk
  * items of near-equal length (the reference's tile split of a long row,
  * Tile_Times per row tile, code/interpreter.py:244-259): a heavy row's gathers
  * then spread over several waves instead of one long chain at the launch tail.
+ * row_edges > 0 merges column blocks for light rows: a row of deg edges uses
+ * blocks of m fine blocks (m the power of two >= row_edges * blocks / deg, at
+ * most blocks), so its items still hold ~row_edges edges; 0 = every row uses
+ * all blocks.  Only the plan build takes it (any value keeps y within fp32
+ * rounding; the sum order per row is fixed by the plan).
  * plan, workspace and launch must use the same (nnz, blocks, item_edges). */
 int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t item_edges);
 int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
-                                     int64_t nnz, int64_t blocks, int64_t item_edges, void* plan,
-                                     int64_t plan_bytes, void* stream);
+                                     int64_t nnz, int64_t blocks, int64_t item_edges, int64_t row_edges,
+                                     void* plan, int64_t plan_bytes, void* stream);
 /* workspace: NULL = B dependent launches accumulating into y; otherwise >=
  * gta_aggregate_blocked_workspace_bytes: one launch over the plan's items in
  * block-major order, item k writing partial row k, then an ordered reduce

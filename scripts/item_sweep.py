@@ -29,8 +29,11 @@ def main():
     ap.add_argument("--grids", default="1x1")
     ap.add_argument("--items", default="64,128,256,512,0")
     ap.add_argument("--blocks", default="0", help="comma list; 0 = bench's auto choice for the tile")
+    ap.add_argument("--rowedges", default="0", help="comma list of light-row merge targets (BlockedPlan row_edges)")
     ap.add_argument("--chunks", default="1", help="comma list of row chunks per tile (one launch per chunk, "
                                                    "chunk-major padded rows as bench.py --row-chunks)")
+    ap.add_argument("--knobs", default="", help="';'-separated libgta debug settings per variant, e.g. "
+                                              "'seg_lean=0;seg_lean=1' (each a ','-list of key=value)")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--n", type=int, default=bench.N_REDDIT)
@@ -40,6 +43,7 @@ def main():
     t0 = time.time()
     g, x, alpha = bench.make_inputs(args.n, args.e, dev)
     print(f"inputs {time.time() - t0:.1f} s", flush=True)
+    defaults = {"seg_lean": 1, "seg_lanes": 32, "seg_u": 8, "seg_nt": 2, "seg_quarter": 1}
     out = {}
     for grid in args.grids.split(","):
         pr, pc = map(int, grid.lower().split("x"))
@@ -57,12 +61,19 @@ def main():
                 B = int(b) or bench.auto_blocks(gg, bench.F)
                 for it in args.items.split(","):
                     ie = int(it) or UNBOUNDED
-                    plans = [sg.blocked_plan(B, ie) for sg in subs]
-                    variants.append((f"{grid}:c{ch}:B{B}:i{it}", B, plans, subs, parts, gg, xl, wl, y))
+                    for re_ in map(int, args.rowedges.split(",")):
+                        plans = [sg.blocked_plan(B, ie, re_) for sg in subs]
+                        for kn in (args.knobs.split(";") if args.knobs else [""]):
+                            kv = dict(p_.split("=") for p_ in kn.split(",") if p_)
+                            tag = f"{grid}:c{ch}:B{B}:i{it}:r{re_}" + (f":{kn}" if kn else "")
+                            variants.append((tag, B, plans, subs, parts, gg, xl, wl, y, kv))
         times = {v[0]: [] for v in variants}
         ref = {}
         for r in range(args.rounds):
-            for name, B, plans, subs, parts, gg, xl, wl, y in variants:
+            for name, B, plans, subs, parts, gg, xl, wl, y, kv in variants:
+                for k_, v_ in kv.items():
+                    ops.set_debug(k_, int(v_))
+
                 def run():
                     for (a, b), sg, plan in zip(parts, subs, plans):
                         ops.aggregate_blocked(sg, xl, wl, out=y[a:b], plan=plan, blocks=B)
@@ -81,7 +92,9 @@ def main():
                     else:
                         d = (y - ref[key]).abs().max().item()
                         assert d < 1e-3, f"variant {name} differs from the first by {d}"
-        for name, B, plans, subs, parts, gg, xl, wl, y in variants:
+                for k_ in kv:
+                    ops.set_debug(k_, defaults[k_])
+        for name, B, plans, subs, parts, gg, xl, wl, y, kv in variants:
             ab = bench.alg_bytes(gg.n_rows, gg.nnz)
             med = float(np.median(times[name]))
             n_items = sum(p.n_items for p in plans)

@@ -250,12 +250,13 @@ def test_aggregate_blocked_matches_oracle(dev, F, heads, blocks, single):
     assert torch.equal(y, y2)
 
 
+@pytest.mark.parametrize("row_edges", [0, 40])
 @pytest.mark.parametrize("item_edges", [1, 7, 64, 256, 1 << 30])
 @pytest.mark.parametrize("blocks", [1, 5, 16])
-def test_blocked_plan_items(dev, item_edges, blocks):
-    """Bounded work items: every non-empty (block, row) segment becomes ceil(len / item_edges) items
-    (empty segments none); the aggregate and the attention form still match the oracle, and any
-    item length gives the same y to fp32 rounding (sum order changes only at part boundaries)."""
+def test_blocked_plan_items(dev, item_edges, blocks, row_edges):
+    """Bounded work items: every non-empty (merged block, row) segment becomes ceil(len / item_edges)
+    items (empty segments none); a row of deg edges merges m = pow2 >= row_edges*B/deg blocks; the
+    aggregate and the attention form still match the oracle."""
     n, e, F, H = 600, 15000, 128, 8
     g0 = G.synthetic(n, e, seed=11, device="cpu")
     ip, ix = g0.numpy()
@@ -266,11 +267,15 @@ def test_blocked_plan_items(dev, item_edges, blocks):
     rng = np.random.default_rng(item_edges % 1000 + blocks)
     ix = np.concatenate([np.sort(rng.integers(0, n, d)) for d in deg]).astype(np.int32)
     g = G.from_numpy(ip, ix, device=dev)
-    plan = g.blocked_plan(blocks, item_edges)
+    plan = g.blocked_plan(blocks, item_edges, row_edges)
     bsize = -(-n // blocks)
     want = 0
     for r in range(n):
         seg = np.bincount(ix[ip[r]:ip[r + 1]] // bsize, minlength=blocks)
+        m = 1
+        while row_edges and deg[r] and m < blocks and deg[r] * m < row_edges * blocks:
+            m *= 2
+        seg = np.array([seg[j:j + m].sum() for j in range(0, blocks, m)])
         want += int(np.sum(-(-seg // item_edges)))
     assert plan.n_items == want
     x = rng.standard_normal((n, F)).astype(np.float32)
@@ -362,7 +367,7 @@ def test_edge_softmax_other_sf_and_errors(dev):
 
 
 @pytest.mark.parametrize("knobs", [{"seg_quarter": 0}, {"seg_u": 2}, {"seg_u": 4}, {"seg_nt": 3}, {"seg_lanes": 16},
-                                   {"seg_lanes": 16, "seg_u": 4}])
+                                   {"seg_lanes": 16, "seg_u": 4}, {"seg_lean": 0}, {"seg_nt": 0}, {"seg_nt": 1}])
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 0), (64, 4), (256, 16), (128, 1)])
 def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     """Every form of the blocked kernel (one item per wave, quarter-wave with 2/4/8 edges per
@@ -374,7 +379,7 @@ def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
     w = torch.from_numpy(rng.random((g.nnz, heads)).astype(np.float32)).to(dev) if heads else None
     y0 = ops.aggregate_blocked(g, x, w, blocks=8)
-    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 2, "seg_lanes": 32}
+    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 2, "seg_lanes": 32, "seg_lean": 1}
     try:
         for k, v in knobs.items():
             ops.set_debug(k, v)
