@@ -373,7 +373,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": ab,
-                     "kernels": ("k_agg_seg4 + k_seg_reduce" if impl == "blocked" else "k_aggregate + combine")},
+                     "kernels": ("k_agg_h32 + k_seg_reduce" if impl == "blocked" else "k_aggregate + combine")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(g, x, alpha)

@@ -20,9 +20,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 # the metric's aggregate kernels: plan path k_aggregate<..., 0, 1> / k_agg_lean, blocked path
-# k_agg_seg4 (quarter-wave, default) or k_agg_seg2d, then k_seg_reduce
+# k_agg_h32 (lean half-wave, default), k_agg_seg4 or k_agg_seg2d, then k_seg_reduce
 METRIC_KERNELS = {"plan": re.compile(r"k_aggregate<\d+, \d+, \d+, 0, 1>|k_agg_lean<"),
-                  "blocked": re.compile(r"k_agg_seg2d<|k_agg_seg4<|k_seg_reduce<")}
+                  "blocked": re.compile(r"k_agg_seg2d<|k_agg_seg4<|k_agg_h32<|k_seg_reduce<")}
 METRIC_KERNEL = METRIC_KERNELS["blocked"]
 
 
@@ -39,7 +39,7 @@ def read_counter(d, counter):
     vals, cur = [], 0.0
     for _, name, v in rows:
         cur += v
-        if "k_seg_reduce" in name or not ("k_agg_seg2d" in name or "k_agg_seg4" in name):
+        if "k_seg_reduce" in name or not ("k_agg_seg2d" in name or "k_agg_seg4" in name or "k_agg_h32" in name):
             vals.append(cur)
             cur = 0.0
     return vals
@@ -57,7 +57,7 @@ def main(fetch_dir="gpurun_out/pmc_fetch", write_dir="gpurun_out/pmc_write", n=2
     fetch_kb = sum(fs) / len(fs)
     write_kb = sum(ws) / len(ws)
     hbm = 2 * fetch_kb * 1024 + write_kb * 1024
-    out = {"n": n, "e": e, "impl": "blocked", "kernel": "k_agg_seg4 + k_seg_reduce", "dispatches": [len(f), len(w)],
+    out = {"n": n, "e": e, "impl": "blocked", "kernel": "k_agg_h32 + k_seg_reduce", "dispatches": [len(f), len(w)],
            "FETCH_SIZE_KB_avg": fetch_kb, "WRITE_SIZE_KB_avg": write_kb,
            "hbm_bytes_per_launch": hbm,
            "method": "2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950 FETCH_SIZE half-count correction), "
