@@ -38,10 +38,23 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--n", type=int, default=bench.N_REDDIT)
     ap.add_argument("--e", type=int, default=bench.E_REDDIT)
+    ap.add_argument("--slices", type=int, default=1, help="confine sources to n/slices nodes (L2-only probe)")
+    ap.add_argument("--plan-knobs", default="", help="libgta settings applied before any plan is built, "
+                                                     "e.g. 'rows_cap=1024'")
     args = ap.parse_args()
+    for kv in filter(None, args.plan_knobs.split(",")):
+        k_, v_ = kv.split("=")
+        ops.set_debug(k_, int(v_))
     dev = torch.device("cuda:0")
     t0 = time.time()
     g, x, alpha = bench.make_inputs(args.n, args.e, dev)
+    if args.slices > 1:  # every gather hits a table of n/slices rows (columns kept sorted within rows)
+        from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G
+        cols = torch.remainder(g.indices.long(), args.n // args.slices)
+        rows = g.row_of_edge().long()
+        order = torch.sort(rows * args.n + cols).indices
+        g = G.Graph(g.indptr, cols[order].to(torch.int32).contiguous())
+        alpha = alpha[order].contiguous()
     print(f"inputs {time.time() - t0:.1f} s", flush=True)
     defaults = {"seg_lean": 1, "seg_lanes": 32, "seg_u": 8, "seg_nt": 2, "seg_quarter": 1}
     out = {}
