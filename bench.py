@@ -9,17 +9,19 @@ fp32.  Inputs are synthetic (seeded lognormal-degree CSR, uniform sources,
 X ~ N(0,1), alpha = softmax over in-edges of N(0,1) logits) and resident in
 HBM before the timed region.
 
---gpus N (launched by torch.distributed.run): the edges are cut into a 2-D grid
-of tiles -- pr row groups (destination rows, nnz-balanced) x pc column groups
+--gpus N (launched by torch.distributed.run): the edges are cut into a grid of
+tiles -- pr row groups (destination rows, nnz-balanced) x pc column groups
 (source columns, nnz-balanced), the reference's row-tile x column blocking
-(code/preprocessing.py:26-38) -- 1x2, 2x2, 4x2 at N = 2, 4, 8.  Each rank
-aggregates its tile in one launch and the pc ranks of a row group sum their
-partial aggregates with one RCCL reduce-scatter, so every rank ends with its
-share of Y's rows.  Measured per-rank compute on one GPU (profiles/
-r01_shard_probe*.json) is why: a 1-D source-column shard keeps every row, and
-per-row work does not shrink with N.  --layout chunked keeps the 1-D shards
-with per-row-chunk collectives (--collective all_reduce | reduce_scatter).
-Total work fixed: "strong".
+(code/preprocessing.py:26-38).  Default pr = N, pc = 1: each rank aggregates
+the in-edges of its destination-row tile (X replicated, 119 MB of 288 GB) in
+one launch and ends with its rows of Y; row tiles are independent, so there is
+no data-path collective.  Per-rank compute of a row tile equals that of a 2-D
+tile of the same edge count (profiles/r01_grid_sweep.json), so column groups
+would only add their exchange.  --grid PRxPC (pc > 1) gives the 2-D form: the
+pc ranks of a row group sum their partial aggregates with one RCCL
+reduce-scatter per row chunk, overlapped with the next chunk.  --layout chunked
+keeps 1-D source-column shards with per-row-chunk collectives (--collective
+all_reduce | reduce_scatter).  Total work fixed: "strong".
 
 Printed JSON (rank 0): value = edges/s of the whole job; roofline = the
 aggregate kernel's algorithmic HBM bytes (548 B/edge + 520 B/node, SURVEY.md
@@ -221,7 +223,7 @@ def main():
     y = torch.empty(gl.n_rows if (rs or grid) else g.n_rows, F, device=dev)
     y_own = torch.empty(shard.chunks * shard.mk, F, device=dev) if rs else None  # this rank's reduced rows
     if grid:
-        y_own = torch.empty(shard.out_rows(), F, device=dev)
+        y_own = y if pc == 1 else torch.empty(shard.out_rows(), F, device=dev)
         my_group = groups[shard.i]
     stream = torch.cuda.current_stream(dev)
 
@@ -235,10 +237,10 @@ def main():
             mk, works = shard.mk, []
             for k, (r0, r1, gg, plan) in enumerate(chunked.parts):
                 agg_chunk(gg, xl, wl, y[r0:r1], plan)
+                if pc == 1:  # row tile: the rows are complete, y is the rank's output
+                    continue
                 own = y_own[k * mk:(k + 1) * mk]
-                if pc == 1:
-                    own.copy_(y[r0:r1])
-                elif backend == "nccl":  # RCCL reduce-scatter among the pc ranks of this row group
+                if backend == "nccl":  # RCCL reduce-scatter among the pc ranks of this row group
                     works.append(dist.reduce_scatter_tensor(own, y[r0:r1], group=my_group, async_op=True))
                 else:  # gloo (1-GPU rehearsal): no reduce-scatter
                     dist.all_reduce(y[r0:r1], group=my_group)
@@ -312,7 +314,8 @@ def main():
                 rows = shard.owned_rows(q).to(dev)
                 ok = rows >= 0
                 full[rows[ok]] = parts[q][:rows.numel()][ok]
-            y_mine, what = full, f"{pr}x{pc} grid tiles, reduce-scattered per row group (reassembled) vs 1-GPU"
+            y_mine, what = full, (f"{pr}x{pc} grid tiles" + (", reduce-scattered per row group" if pc > 1 else "") +
+                                  " (reassembled) vs 1-GPU")
         elif rs:  # reassemble Y from every rank's reduced rows
             parts = [torch.empty_like(y_own) for _ in range(world)]
             dist.all_gather(parts, y_own)
@@ -360,7 +363,9 @@ def main():
                 "alpha=per-head softmax over in-edges",
         "config": {"workload": "GAT layer-1 aggregate block [3,11,12] (scatter C -> applyedge MUL -> gather ADD)",
                    "graph": "reddit-shaped", "N": args.n, "E": nnz_total, "F": F, "heads": HEADS,
-                   "parallelism": (f"2-D edge tiles {pr}x{pc} (row groups x source-column groups), RCCL reduce-scatter "
+                   "parallelism": (f"destination-row tiles x{pr} (X replicated, no data-path collective)"
+                                   if grid and pc == 1 else
+                                   f"2-D edge tiles {pr}x{pc} (row groups x source-column groups), RCCL reduce-scatter "
                                    f"of the partial aggregates inside each row group" if grid else
                                    f"edge-partition by source column x{world}" + (
                                        (" + RCCL reduce-scatter per row chunk (each rank ends with its node "

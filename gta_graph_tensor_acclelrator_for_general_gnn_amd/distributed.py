@@ -164,13 +164,15 @@ def run_stream(opgraph, stream, shard, tensors, semantics=None, group=None, plan
 
 
 def grid_shape(world):
-    """Default 2-D rank grid (row groups pr x column groups pc) for the aggregate benchmark: the
-    edge tiles of the reference's (row tile x column) blocking, code/preprocessing.py:26-38.
-    pc = 2 keeps a real partial-aggregate reduction at every p > 1 while each rank's row count,
-    and with it its per-row work and its share of the exchange, falls as 1/pr."""
-    if world <= 2:
-        return 1, world
-    return world // 2, 2
+    """Default rank grid (row groups pr x column groups pc) for the aggregate benchmark: pr = world,
+    pc = 1, i.e. destination-row tiles of the reference's row-tile blocking
+    (code/preprocessing.py:26-38) with X replicated.  Measured per-rank compute of one launch on
+    one GPU (profiles/r01_grid_sweep.json) is the same for row tiles and 2-D tiles of equal edge
+    count (8x1 0.665 ms vs 4x2 0.645; 4x1 1.274 vs 2x2 1.273; 2x1 2.494 vs 1x2 2.544), so column
+    groups only add the reduce-scatter of partial aggregates (60 MB per rank at 1x2).  Row tiles
+    are independent: no data-path collective.  --grid PRxPC selects the 2-D form with its RCCL
+    reduce-scatter."""
+    return world, 1
 
 
 class GridShard:
