@@ -915,6 +915,109 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
   }
 }
 
+// Lean half-wave form of the fused GAT attention item (k_agg_seg4<4, 8, ATT, SFC = exp-leaky-
+// relu, G = 32>) for F = 128, 8 heads: the weighted k_agg_h32 loop with the edge weight computed,
+// v = exp(leaky_relu(a[row, h] + b[src, h])), instead of loaded.  Per full 8-edge step lane
+// (h, q) gathers the scores of edges 2q and 2q+1 (their sources picked from the step's
+// broadcast indices by q), evaluates 2 special functions instead of 8, and edge u's v reaches the
+// head's four lanes by a DPP quad broadcast, as the weights do in k_agg_h32.  Score rows are
+// addressed like X rows (uniform base + 32-bit byte offset).  Same per-lane edge order, fma chain
+// and per-head sum order as the generic form: bitwise equal to it.  Slab row k: 128 partials,
+// then the 8 per-head sums of v.
+template <int NT>
+__global__ void __launch_bounds__(kBlock)
+k_att_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
+          uint32_t row_bytes, const float* __restrict__ a, int64_t lda, const float* __restrict__ b,
+          uint32_t brow_bytes, float* __restrict__ slabs, const SegItem* __restrict__ items) {
+  constexpr int G = 32, U = 8, F = 128, LDS = F + 8;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int l32 = lane & (G - 1);
+  const int64_t k = (static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform()) * 2 + (lane >> 5);
+  const int64_t n_items = *n_items_p;
+  SegItem it{0, 0, 0};
+  if (k < n_items) it = items[k];
+  const int len = it.len;
+  const int other = __shfl_xor(len, 32);
+  const int maxlen = __builtin_amdgcn_readfirstlane(max(len, other));
+  const int minlen = __builtin_amdgcn_readfirstlane(min(len, other));
+  if (maxlen == 0) return;
+  const int h = l32 >> 2, q = l32 & 3;
+  const uint32_t colb = static_cast<uint32_t>(l32) * 16u, hb = static_cast<uint32_t>(h) * 4u;
+  const char* xb = reinterpret_cast<const char*>(x);
+  const char* bb = reinterpret_cast<const char*>(b);
+  const float arow = (len > 0) ? a[static_cast<int64_t>(it.row) * lda + h] : 0.f;
+  auto ldi = [&](const int32_t* p) { return (NT & 1) ? __builtin_nontemporal_load(p) : *p; };
+  auto row = [&](int src) -> float4 {
+    return *reinterpret_cast<const float4*>(xb + (__umul24(static_cast<uint32_t>(src), row_bytes) + colb));
+  };
+  auto score = [&](int src) -> float {
+    const float sv = arow + *reinterpret_cast<const float*>(bb + (__umul24(static_cast<uint32_t>(src), brow_bytes) + hb));
+    return sf_apply(GTA_SF_EXP_LEAKY_RELU, sv);
+  };
+  const int32_t* ic = indices + it.beg;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  float ssum = 0.f;
+  int idxv = (l32 < len) ? ldi(ic + l32) : 0;
+  for (int c = 0; c < maxlen; c += G) {
+    const int idxn = (c + G + l32 < len) ? ldi(ic + G + l32) : 0;
+#pragma unroll
+    for (int s = 0; s < G; s += U) {
+      if (c + s >= maxlen) break;
+      float4 xv[U];
+      float wu[U];
+      if (c + s + U <= minlen) {  // full step for both items: no masks
+        int src[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          src[u] = bcastG<G>(idxv, s + u);
+          xv[u] = row(src[u]);
+        }
+        const int sa = q == 0 ? src[0] : q == 1 ? src[2] : q == 2 ? src[4] : src[6];
+        const int sb = q == 0 ? src[1] : q == 1 ? src[3] : q == 2 ? src[5] : src[7];
+        const float v0 = score(sa), v1 = score(sb);
+        wu[0] = quad_bcast<0>(v0); wu[1] = quad_bcast<0>(v1);
+        wu[2] = quad_bcast<1>(v0); wu[3] = quad_bcast<1>(v1);
+        wu[4] = quad_bcast<2>(v0); wu[5] = quad_bcast<2>(v1);
+        wu[6] = quad_bcast<3>(v0); wu[7] = quad_bcast<3>(v1);
+#pragma unroll
+        for (int u = 0; u < U; ++u) ssum += wu[u];
+      } else {
+        const int rem = len - c - s;  // edges of this item left at this step (may be <= 0)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int src = bcastG<G>(idxv, s + u);
+          if (u < rem) {
+            xv[u] = row(src);
+            wu[u] = score(src);
+            ssum += wu[u];
+          } else {
+            xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            wu[u] = 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc[0] = fmaf(wu[u], xv[u].x, acc[0]);
+        acc[1] = fmaf(wu[u], xv[u].y, acc[1]);
+        acc[2] = fmaf(wu[u], xv[u].z, acc[2]);
+        acc[3] = fmaf(wu[u], xv[u].w, acc[3]);
+      }
+    }
+    idxv = idxn;
+    ic += G;
+  }
+  if (len > 0) {
+    float* o = slabs + k * LDS;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (NT & 2) __builtin_nontemporal_store(acc[t], o + l32 * 4 + t);
+      else o[l32 * 4 + t] = acc[t];
+    }
+    if (q == 0) o[F + h] = ssum;
+  }
+}
+
 // The row's slab rows (item ids row_items[row_ptr[row] .. row_ptr[row+1]), in
 // (block, part) order) summed in that order; ids arrive 64 at a time with one
 // coalesced load and are broadcast by readlane, 4 slab loads in flight.
@@ -1969,6 +2072,7 @@ int g_seg_lanes = 32;      // lanes per item of that form at F = 128: 32 (2 item
 int g_seg_nt = 2;          // non-temporal bits of the multi-item forms at F = 128, U = 8: 2 = slab stores (-1 %)
 int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
 int g_seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
+int g_att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
 int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
 int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
 int g_apply_edge_form = 1;  // 1: row-sweep K3 kernels (cols / pack); 0: the generic per-element kernel
@@ -1997,6 +2101,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "seg_u") { g_seg_u = static_cast<int>(value); return 0; }
   if (k == "seg_lanes") { g_seg_lanes = static_cast<int>(value); return 0; }
   if (k == "seg_lean") { g_seg_lean = static_cast<int>(value); return 0; }
+  if (k == "att_lean") { g_att_lean = static_cast<int>(value); return 0; }
   if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
   if (k == "mm_prefetch") { g_mm_prefetch = static_cast<int>(value); return 0; }
   if (k == "mm_blocks_per_cu") { g_mm_blocks_per_cu = value; return 0; }
@@ -2366,7 +2471,17 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
   else k_agg_seg4<VW_, U_, false, 0, true><<<g4, blk, 0, s>>>(indices, nit, x, ldx, nullptr, 0, lph, slabs, \
                                                              it, att)
   const int lph32 = static_cast<int>((F / heads) / 4);
-  if (F == 128 && g_seg_lanes == 32 && (F / heads) % 4 == 0 && lph32 >= 1 && 32 % lph32 == 0) {
+  const bool lean = g_att_lean && elr && F == 128 && heads == 8 && g_seg_lanes == 32 && n_cols < (1 << 24) &&
+                    static_cast<uint64_t>(n_cols) * static_cast<uint64_t>(ldx) * 4u < (1ull << 32) &&
+                    static_cast<uint64_t>(n_cols) * static_cast<uint64_t>(ldb) * 4u < (1ull << 32);
+  if (lean) {
+    const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
+    const uint32_t rb = static_cast<uint32_t>(ldx * 4), bbytes = static_cast<uint32_t>(ldb * 4);
+    if (g_att_lean == 2)
+      k_att_h32<2><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it);
+    else
+      k_att_h32<0><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it);
+  } else if (F == 128 && g_seg_lanes == 32 && (F / heads) % 4 == 0 && lph32 >= 1 && 32 % lph32 == 0) {
     const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
     if (elr) k_agg_seg4<4, 8, false, 0, true, GTA_SF_EXP_LEAKY_RELU, 32><<<g2h, blk, 0, s>>>(
         indices, nit, x, ldx, nullptr, 0, lph32, slabs, it, att);

@@ -476,6 +476,39 @@ def test_gat_aggregate_blocked_matches_oracle(dev, F, heads, normalize, blocks, 
         assert torch.all(y[3] == 0) and torch.all(y[4] == 0)
 
 
+@pytest.mark.parametrize("blocks,item_edges", [(1, 1 << 30), (5, 256), (16, 64), (20, 256)])
+@pytest.mark.parametrize("ldb", [8, 24])
+def test_gat_aggregate_lean_bitwise(dev, blocks, item_edges, ldb):
+    """k_att_h32 (lean fused attention, F = 128, 8 heads) == the generic half-wave attention
+    kernel bitwise (y and the per-head sums; same per-lane edge order, fma chain and sum order),
+    with strided score tables and rows that are empty, short (masked steps only) and long."""
+    n, e, F, H = 3000, 90000, 128, 8
+    rng = np.random.default_rng(blocks + ldb)
+    deg = np.diff(G.synthetic(n, e, seed=5).numpy()[0]).copy()
+    deg[7], deg[8], deg[9] = 5000, 3, 0
+    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    ix = np.concatenate([np.sort(rng.integers(0, n, d)) for d in deg]).astype(np.int32)
+    g = G.from_numpy(ip, ix, device=dev)
+    x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
+    a = torch.from_numpy(rng.standard_normal((n, H)).astype(np.float32)).to(dev)
+    bw = torch.from_numpy(rng.standard_normal((n, ldb)).astype(np.float32)).to(dev)
+    b = bw[:, ldb - H:]
+    plan = g.blocked_plan(blocks, item_edges)
+    outs = {}
+    try:
+        for lean in (0, 1, 2):
+            ops.set_debug("att_lean", lean)
+            outs[lean] = ops.gat_aggregate_blocked(g, x, a, b, want_sums=True, plan=plan)
+    finally:
+        ops.set_debug("att_lean", 2)
+    for lean in (1, 2):
+        assert torch.equal(outs[0][0], outs[lean][0]), lean
+        assert torch.equal(outs[0][1], outs[lean][1]), lean
+    ref, rsum = isa_ref.gat_aggregate(ip, ix, x.cpu().numpy().astype(np.float64), a.cpu().numpy().astype(np.float64),
+                                      b.cpu().numpy().astype(np.float64), "EXP_LEAKY_RELU", True)
+    _check(outs[1][1], rsum, rsum, "lean gat sums")
+
+
 @pytest.mark.parametrize("case", ["no_edges", "no_rows", "one_row", "dup_self"])
 def test_degenerate_graphs_every_op(dev, case):
     """Empty and ragged extremes through every entry point: a graph without edges, without rows,
