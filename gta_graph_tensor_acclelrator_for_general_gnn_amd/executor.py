@@ -155,6 +155,12 @@ class Executor:
         self.sibling_mm = True
         self._wcat = {}
         self.pushdown = self._match_pushdown()
+        #   gather_acc: applynode ADD(gather G, node op T), each the other's only reader (GIN op 4:
+        #   agg + (1+eps) x), runs as the aggregate accumulating into T's fresh output buffer:
+        #   T + sum == sum + T bitwise, and the ADD pass over [N, F] disappears.  G and T stay
+        #   available (recomputed on demand).
+        self.gather_acc = dist is None or not dist.on
+        self.gacc = self._match_gather_acc()
 
     # ---------------------------------------------------------------- inputs
     def _ext(self, op, slot):
@@ -314,6 +320,50 @@ class Executor:
                     and self.sem.bin_of(op) == "ADD":
                 found[op.idx] = m.idx
         return found
+
+    def _match_gather_acc(self):
+        """{applynode ADD A: (gather G, slot of T, node op T)} for A = ADD(G, T) where A is G's and T's
+        only consumer, T a two-operand applynode ADD/MUL/DIV/SUB (so its output is a tensor it
+        allocated itself) and A carries no SF post-op."""
+        found = {}
+        for A in self.g.ops:
+            ins = self.g.inputs[A.idx]
+            if A.type != "applynode" or A.comp != "ADD" or len(ins) != 2 or any(x.kind != "op" for x in ins):
+                continue
+            if self.sem.bin_of(A) != "ADD":
+                continue
+            kinds = [self.g.ops[x.op].type for x in ins]
+            if sorted(kinds) != ["applynode", "gather"] or ins[0].op == ins[1].op:
+                continue
+            gs = 0 if kinds[0] == "gather" else 1
+            G, T = self.g.ops[ins[gs].op], self.g.ops[ins[1 - gs].op]
+            if G.order != "R" or self.consumers[G.idx] != [A.idx] or self.consumers[T.idx] != [A.idx]:
+                continue
+            if T.comp not in ("ADD", "MUL") or len(self.g.inputs[T.idx]) != 2:
+                continue
+            cons = self.consumers[A.idx]
+            if len(cons) == 1 and self.g.ops[cons[0]].comp == "SF" and self.g.ops[cons[0]].type == "applynode":
+                continue  # keep A's SF post-op fusion
+            found[A.idx] = (G.idx, 1 - gs, T.idx)
+        return found
+
+    def _eval_gather_acc(self, A):
+        """A = ADD(G, T) as G's aggregate accumulated into T's buffer; None if G's form cannot
+        accumulate (then A runs unfused)."""
+        G, slot_t, T = self.gacc[A.idx]
+        raw = self.values.get(G)
+        if not (isinstance(raw, Lazy) and raw.v is None):
+            return None
+        t = self._source(A, slot_t)
+        if not isinstance(t, NodeT) or t.t.dtype != torch.float32 or not t.t.is_contiguous():
+            return None
+        y = self._eval_gather(self.g.ops[G], acc=t.t)
+        if y.t.data_ptr() != t.t.data_ptr():  # G's form computed a fresh tensor: add it as the ADD would
+            raw.v = y
+            return None
+        top = self.g.ops[T]
+        self.values[T] = Lazy(lambda: self._eval_applynode(top))  # T's buffer now holds A
+        return y
 
     def _node_mm(self, op, v, post_sf=None):
         """applyedge MM of a virtual scatter: the GEMM runs over the node rows, the result stays virtual."""
@@ -587,7 +637,7 @@ class Executor:
             x = x.float()
         return x, W
 
-    def _eval_gather(self, op):
+    def _eval_gather(self, op, acc=None):
         if op.order != "R":
             raise NotImplementedError("gather ORDER C (to source) is not emitted by genGraphOP")
         src = self.g.inputs[op.idx][0]
@@ -619,22 +669,22 @@ class Executor:
             if len(pins) == 1:
                 v = pins[0]
             elif bin_ == "MUL":
-                return NodeT(self._weighted_aggregate(pins[0], pins[1]))
+                return NodeT(self._weighted_aggregate(pins[0], pins[1], acc))
             else:  # a non-MUL fused pair: evaluate the producer, then gather
                 v = self._materialize_deferred(v)
         if isinstance(v, Scat):
-            y = self._spmm(v.t, v.mode, None)
+            y = self._spmm(v.t, v.mode, None, acc)
             self._count(E * (4 + v.t.shape[1] * 4) + n * (8 + v.t.shape[1] * 4))
             return NodeT(y)
         xe = self._to_edge_tensor(v)
-        y = ops.aggregate(self.graph, xe, "edge", None, plan=self._plan())
+        y = ops.aggregate(self.graph, xe, "edge", None, out=acc, accumulate=acc is not None, plan=self._plan())
         self._count(E * xe.shape[1] * 4 + n * (8 + xe.shape[1] * 4))
         return NodeT(y)
 
     def _plan(self):
         return self.plan_chunk if self.plan_chunk else None
 
-    def _weighted_aggregate(self, u, v):
+    def _weighted_aggregate(self, u, v, acc=None):
         """sum_e u(e) (.) v(e): the wider operand is the feature row, the narrower the (head) weight."""
         n, E = self.graph.n_rows, self.graph.nnz
 
@@ -654,11 +704,11 @@ class Executor:
             xt, mode = self._to_edge_tensor(x), "edge"
         if xt.shape[1] % wt.shape[1]:
             raise ValueError(f"weighted aggregate: weight width {wt.shape[1]} does not divide {xt.shape[1]}")
-        y = self._spmm(xt, mode, wt)
+        y = self._spmm(xt, mode, wt, acc)
         self._count(E * (4 + 4 * wt.shape[1] + 4 * xt.shape[1]) + n * (8 + 4 * xt.shape[1]))
         return y
 
-    def _spmm(self, xt, mode, wt):
+    def _spmm(self, xt, mode, wt, acc=None):
         """SpMM-form aggregate: column-blocked when the gathered table outgrows L2, else row-chunked."""
         heads = 0 if wt is None else wt.shape[1]
         if (mode == "src" and self.blocked_blocks and xt.shape[0] * xt.shape[1] * 4 >= self.blocked_min_table_bytes
@@ -668,8 +718,8 @@ class Executor:
                 B = ops.BlockedPlan.auto_blocks(self.graph, xt.shape[1])
                 B = B if B >= 4 else 0
             if B and self.graph.blocked_plan(B).sorted:
-                return ops.aggregate_blocked(self.graph, xt, wt, blocks=B)
-        return ops.aggregate(self.graph, xt, mode, wt, plan=self._plan())
+                return ops.aggregate_blocked(self.graph, xt, wt, out=acc, accumulate=acc is not None, blocks=B)
+        return ops.aggregate(self.graph, xt, mode, wt, out=acc, accumulate=acc is not None, plan=self._plan())
 
     def _unweighted(self, x):
         if isinstance(x, Scat):
@@ -677,6 +727,11 @@ class Executor:
         return ops.aggregate(self.graph, self._to_edge_tensor(x), "edge", None, plan=self._plan())
 
     def _eval_applynode(self, op, post_sf=None):
+        if self.gather_acc and post_sf is None and op.idx in self.gacc:
+            y = self._eval_gather_acc(op)
+            if y is not None:
+                self._count(self.n_nodes * y.t.shape[1] * 4)  # the aggregate's extra read of T
+                return y
         ins = self._inputs(op)
         n = self.n_nodes
         if op.comp == "MM":
@@ -754,6 +809,8 @@ class Executor:
         if op.type == "applyedge":
             return self._eval_applyedge(op)
         if op.type == "gather":
+            if self.gather_acc and any(g == op.idx for g, _, _ in self.gacc.values()):
+                return Lazy(lambda: self._gather_value(op))  # its ADD consumer accumulates it
             if self.mm_first and op.idx in self.reorder:
                 v = self._eval_mm_first(op, self.g.ops[self.reorder[op.idx]])
                 if v is not None:

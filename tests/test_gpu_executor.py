@@ -232,3 +232,27 @@ def test_graphed_run_replays_the_stream(golden_dir, manifest, cora, dev, network
             a, b = out[k], ref[k]
             assert torch.equal(torch.isfinite(a), torch.isfinite(b))
             assert torch.equal(a[torch.isfinite(a)], b[torch.isfinite(b)]), (network, k, trial)
+
+
+@pytest.mark.parametrize("plan_chunk", [0, 64])
+def test_gather_acc_fusion_bitwise_on_gpu(golden_dir, manifest, cora, dev, plan_chunk):
+    """GIN's ADD(gather, (1+eps) x) as the aggregate accumulating into op 3's buffer gives every
+    op's value bitwise equal to the unfused run (T + sum == sum + T in fp32)."""
+    ip, ix = cora
+    recs = [s for s in _all_streams(manifest) if s["network"] == "GIN" and not s["reorder"]]
+    assert recs
+    gd = G.from_numpy(ip, ix, device=dev)
+    for rec in recs:
+        sem = Semantics.for_network("GIN", False)
+        og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+        st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+        tensors = workloads.make_tensors(og, gd, "GIN", seed=4)
+        vals = {}
+        for on in (True, False):
+            ex = executor.Executor(og, st, gd, tensors, sem, plan_chunk=plan_chunk)
+            ex.gather_acc = on
+            assert bool(ex.gacc)
+            ex.run()
+            vals[on] = [ex.tensor_of(i) for i in range(len(og))]
+        for i, (a, b) in enumerate(zip(vals[True], vals[False])):
+            assert torch.equal(a, b), f"{rec['file']} op {i}"

@@ -219,3 +219,29 @@ def test_node_mm_and_pushdown_cpu(golden_dir, manifest, monkeypatch, network):
         nbytes[on] = ex.alg_bytes
         compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
     assert nbytes[True] < nbytes[False]
+
+
+def test_gather_acc_fusion_cpu(golden_dir, manifest, monkeypatch):
+    """GIN op 4 = ADD(gather, (1+eps) x) runs as the aggregate accumulating into op 3's buffer: every
+    op (op 3 and the gather included, recomputed on demand) still matches the oracle, and the ADD's
+    [N, F] pass is gone from the algorithmic bytes."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    recs = [s for s in _streams(manifest) if s["network"] == "GIN" and not s["reorder"]]
+    assert recs
+    for rec in recs:
+        sem = Semantics.for_network("GIN", False)
+        og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+        st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+        gc, ip, ix = _cora_graph(golden_dir)
+        tensors = workloads.make_tensors(og, gc, "GIN", seed=5)
+        ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
+        nbytes = {}
+        for on in (True, False):
+            ex = executor.Executor(og, st, gc, tensors, sem)
+            ex.gather_acc = on
+            if on:
+                assert ex.gacc, "GIN's ADD(gather, MUL) not matched"
+            ex.run()
+            nbytes[on] = ex.alg_bytes
+            compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
+        assert nbytes[True] < nbytes[False]
