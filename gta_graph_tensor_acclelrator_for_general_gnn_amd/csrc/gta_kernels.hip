@@ -1493,6 +1493,31 @@ k_apply_node(int bin, int sf, int64_t n, const float* __restrict__ a, int64_t ld
   }
 }
 
+// Vector form of k_apply_node for the common shapes (same per-element ops, so bitwise equal):
+// a and out [n, F] with F % 4 == 0 and 16-B rows, b none (BM 0), [n, F] (BM 1) or one value
+// per node b[i * ldb] (BM 2; ldb 0 = one value for all, e.g. GIN's 1 + eps).  One float4 per
+// thread step, 32-bit index math (n * F / 4 < 2^32).
+template <int BM>
+__global__ void __launch_bounds__(kBlock)
+k_apply_node4(int bin, int sf, uint32_t n4, uint32_t F4, const float* __restrict__ a, int64_t lda,
+              const float* __restrict__ b, int64_t ldb, float* __restrict__ out, int64_t ldo) {
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += gridDim.x * blockDim.x) {
+    const uint32_t i = t / F4, c = (t - i * F4) * 4u;
+    float4 v = *reinterpret_cast<const float4*>(a + i * lda + c);
+    if (BM == 1) {
+      const float4 w = *reinterpret_cast<const float4*>(b + i * ldb + c);
+      v.x = bin_apply(bin, v.x, w.x); v.y = bin_apply(bin, v.y, w.y);
+      v.z = bin_apply(bin, v.z, w.z); v.w = bin_apply(bin, v.w, w.w);
+    } else if (BM == 2) {
+      const float w = b[i * ldb];
+      v.x = bin_apply(bin, v.x, w); v.y = bin_apply(bin, v.y, w);
+      v.z = bin_apply(bin, v.z, w); v.w = bin_apply(bin, v.w, w);
+    }
+    v.x = sf_apply(sf, v.x); v.y = sf_apply(sf, v.y); v.z = sf_apply(sf, v.z); v.w = sf_apply(sf, v.w);
+    *reinterpret_cast<float4*>(out + i * ldo + c) = v;
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K3' fused GAT edge-softmax: one wave per destination row; lane = k*H + h
 // handles edge slot k (64/H edges per step) and head h.  Indices arrive 64 at
@@ -2072,6 +2097,7 @@ int g_seg_lanes = 32;      // lanes per item of that form at F = 128: 32 (2 item
 int g_seg_nt = 2;          // non-temporal bits of the multi-item forms at F = 128, U = 8: 2 = slab stores (-1 %)
 int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
 int g_seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
+int g_apply_node_vec = 1;  // k_apply_node4 (float4, 32-bit index math) for the common apply_node shapes
 int g_att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
 int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
 int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
@@ -2102,6 +2128,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "seg_lanes") { g_seg_lanes = static_cast<int>(value); return 0; }
   if (k == "seg_lean") { g_seg_lean = static_cast<int>(value); return 0; }
   if (k == "att_lean") { g_att_lean = static_cast<int>(value); return 0; }
+  if (k == "apply_node_vec") { g_apply_node_vec = static_cast<int>(value); return 0; }
   if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
   if (k == "mm_prefetch") { g_mm_prefetch = static_cast<int>(value); return 0; }
   if (k == "mm_blocks_per_cu") { g_mm_blocks_per_cu = value; return 0; }
@@ -2599,6 +2626,17 @@ int gta_apply_node(int bin, int sf, int64_t n, const float* a, int64_t lda, int6
   if (check_bcast(Fa, Fb, b != nullptr, &Fo)) return fail(GTA_ERR_ARG, "apply_node: widths must divide");
   if (n == 0) return GTA_OK;
   const int64_t total = n * Fo;
+  const int bm = !b ? 0 : (Fb == Fo ? 1 : (Fb == 1 ? 2 : -1));
+  if (g_apply_node_vec && bm >= 0 && Fa == Fo && Fo % 4 == 0 && total / 4 < (int64_t(1) << 32) && lda % 4 == 0 &&
+      ldo % 4 == 0 && aligned(a, 16) && aligned(out, 16) && (bm != 1 || (ldb % 4 == 0 && aligned(b, 16)))) {
+    const uint32_t n4 = static_cast<uint32_t>(total / 4), F4 = static_cast<uint32_t>(Fo / 4);
+    const dim3 g(static_cast<unsigned>(std::min<int64_t>((n4 + kBlock - 1) / kBlock, 256 * 16))), blk(kBlock);
+    if (bm == 0) k_apply_node4<0><<<g, blk, 0, S(stream)>>>(bin, sf, n4, F4, a, lda, b, ldb, out, ldo);
+    else if (bm == 1) k_apply_node4<1><<<g, blk, 0, S(stream)>>>(bin, sf, n4, F4, a, lda, b, ldb, out, ldo);
+    else k_apply_node4<2><<<g, blk, 0, S(stream)>>>(bin, sf, n4, F4, a, lda, b, ldb, out, ldo);
+    GTA_LAUNCHED("k_apply_node4");
+    return GTA_OK;
+  }
   const int64_t blocks = std::min<int64_t>((total + kBlock - 1) / kBlock, 256 * 16);
   k_apply_node<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, S(stream)>>>(
       bin, sf, n, a, lda, static_cast<int>(Fa), b, ldb, static_cast<int>(Fb), out, ldo, static_cast<int>(Fo));

@@ -166,6 +166,31 @@ def test_apply_node(dev, bin_kind, sf, Fa, Fb, bcast):
     assert np.allclose(out.cpu().numpy(), ref, rtol=2e-6, atol=1e-6)
 
 
+@pytest.mark.parametrize("bin_kind,sf,Fa,Fb,bcast", [
+    ("MUL", None, 100, 1, True), ("ADD", None, 100, 100, False), ("MUL", "ELU", 128, 1, False),
+    (None, "RELU", 128, None, False), ("DIV", "EXP", 4, 4, False), ("SUB", "SIGMOID", 16, 1, True),
+    ("ADD", None, 128, 16, False),  # head broadcast: generic kernel
+])
+def test_apply_node_vector_form_bitwise(dev, bin_kind, sf, Fa, Fb, bcast):
+    """k_apply_node4 (float4 rows; b none, same shape or one value per node / for all) == the
+    generic per-element kernel bitwise, and == the oracle."""
+    rng = np.random.default_rng(Fa + (Fb or 0))
+    n = 5003
+    a = torch.from_numpy(rng.standard_normal((n, Fa)).astype(np.float32)).to(dev)
+    b = None if Fb is None else torch.from_numpy((rng.random((1 if bcast else n, Fb)) + 0.5).astype(np.float32)).to(dev)
+    outs = []
+    try:
+        for vec in (1, 0):
+            ops.set_debug("apply_node_vec", vec)
+            outs.append(ops.apply_node(bin_kind, sf, a, b, b_broadcast_row=bcast))
+    finally:
+        ops.set_debug("apply_node_vec", 1)
+    assert torch.equal(outs[0], outs[1])
+    ref = isa_ref.apply_node(bin_kind, sf, a.cpu().numpy(), None if b is None else b.cpu().numpy(),
+                             b_broadcast_row=bcast)
+    assert np.allclose(outs[0].cpu().numpy(), ref, rtol=2e-6, atol=1e-6)
+
+
 @pytest.mark.parametrize("M,K,N", [(2708, 1433, 128), (1000, 602, 128), (777, 128, 16), (64, 64, 64),
                                    (5, 3, 7), (3000, 100, 128), (513, 130, 65)])
 @pytest.mark.parametrize("gathered", [False, True])
