@@ -1872,7 +1872,9 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
   const int ncb = (N + BN - 1) / BN;
   const int n0 = static_cast<int>(blockIdx.x % ncb) * BN;
   constexpr int AV = BF ? 8 : 4;  // A values per lane per fragment
-  const bool avec = (ldx % AV == 0) && aligned(x, sizeof(TA) * AV);
+  // fp32 x is loaded as float4s (16-B rows suffice); bf16 x as one 16-B load of 8 values
+  constexpr int AVL = sizeof(TA) == 4 ? 4 : 8;
+  const bool avec = (ldx % AVL == 0) && aligned(x, sizeof(TA) * AVL);
   const bool wvec = (ldwt % WV == 0) && aligned(wt, 16);
   const int64_t n_groups = (M + 127) / 128;
   const bool one_chunk = K <= KC;
@@ -1932,13 +1934,28 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
         const int k0 = kc + ks + AV * g;  // first k of this lane's fragment
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          if (avec && aok[i] && k0 + AV <= K) {
-            if constexpr (sizeof(TA) == 4) {
+          if constexpr (sizeof(TA) == 4) {
+            if (avec) {  // float4 pieces; a piece past K (K % 4 == 0) or past M reads zeros
 #pragma unroll
               for (int q = 0; q < AV / 4; ++q) {
-                const float4 v4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(ap[i]) + k0 + 4 * q);
+                const int kq = k0 + 4 * q;
+                float4 v4 = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (aok[i] && kq + 4 <= K) {
+                  v4 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(ap[i]) + kq);
+                } else if (aok[i] && kq < K) {
+                  const float* pr = reinterpret_cast<const float*>(ap[i]) + kq;
+                  v4.x = pr[0];
+                  if (kq + 1 < K) v4.y = pr[1];
+                  if (kq + 2 < K) v4.z = pr[2];
+                }
                 av[i][4 * q] = v4.x; av[i][4 * q + 1] = v4.y; av[i][4 * q + 2] = v4.z; av[i][4 * q + 3] = v4.w;
               }
+              continue;
+            }
+          }
+          if (avec && aok[i] && k0 + AV <= K) {
+            if constexpr (sizeof(TA) == 4) {
+              // handled above
             } else {
               const uint4 u = *reinterpret_cast<const uint4*>(ap[i] + k0);
               const uint32_t uw[4] = {u.x, u.y, u.z, u.w};
@@ -2724,9 +2741,10 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
   const int64_t cap = (K <= kc) ? std::max<int64_t>(1, 256 * per_cu / ncb) : groups;  // W staged once: persistent
   const dim3 gr(static_cast<unsigned>(std::min<int64_t>(groups, cap) * ncb));
-  // prefetch the next A fragment: measured 1.2x on fp32 (K = 602) and bf16 K = 128, slower with a
-  // K tail on the mixed path (profiles/r01_mm_bench.json); g_mm_prefetch 2 = always, 0 = never
-  const bool pf = g_mm_prefetch == 2 || (g_mm_prefetch == 1 && (dtype == GTA_F32 || K % 32 == 0));
+  // prefetch the next A fragment: measured 1.2x on fp32 (K = 602) and bf16 K = 128, and 1.1x on the
+  // mixed path with a K tail since fp32 A loads are float4 pieces (GIN K = 100: 0.70 -> 0.64 ms,
+  // profiles/r01_mm_bench_2.json); bf16 x with a K tail stays without; g_mm_prefetch 2 = always, 0 = never
+  const bool pf = g_mm_prefetch == 2 || (g_mm_prefetch == 1 && (dtype != GTA_BF16 || K % 32 == 0));
 #define GTA_MMR(TA_, WT_, NT_)                                                                                \
   if (pf) k_mm_rows<TA_, WT_, NT_, true><<<gr, dim3(kBlock), 0, S(stream)>>>(                        \
       static_cast<const TA_*>(x), ldx, row_idx, M, static_cast<int>(K), static_cast<const WT_*>(wt), ldwt,        \
