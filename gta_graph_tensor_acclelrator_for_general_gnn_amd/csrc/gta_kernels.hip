@@ -826,7 +826,10 @@ __device__ __forceinline__ float quad_bcast(float v) {  // lane (l & ~3) | SEL o
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), SEL * 0x55, 0xF, 0xF, false));
 }
 
-template <bool WEIGHTED, int NT>
+// W1 (WEIGHTED with one weight per edge, e.g. GCN / GraphSAGE-mean [E, 1]): the weights of a
+// 32-edge chunk arrive with its indices (lane l loads w[e + l]) and edge u's weight is broadcast
+// like its index (bcastG), instead of one load per edge per lane.
+template <bool WEIGHTED, int NT, bool W1 = false>
 __global__ void __launch_bounds__(kBlock)
 k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
           uint32_t row_bytes, const float* __restrict__ w, int64_t ldw, float* __restrict__ slabs,
@@ -849,7 +852,7 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
   const int ldw32 = static_cast<int>(ldw);
   // chunk cursors: advanced once per 32 edges, so no per-edge 64-bit offsets are live
   const int32_t* ic = indices + it.beg;
-  const float* wc = WEIGHTED ? w + it.beg * ldw + h : nullptr;
+  const float* wc = WEIGHTED ? w + it.beg * ldw + (W1 ? 0 : h) : nullptr;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   auto ldi = [&](const int32_t* p) { return (NT & 1) ? __builtin_nontemporal_load(p) : *p; };
   auto ldw_ = [&](const float* p) { return (NT & 1) ? __builtin_nontemporal_load(p) : *p; };
@@ -857,8 +860,10 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
     return *reinterpret_cast<const float4*>(xb + (__umul24(static_cast<uint32_t>(src), row_bytes) + colb));
   };
   int idxv = (l32 < len) ? ldi(ic + l32) : 0;
+  float wv = (W1 && l32 < len) ? ldw_(wc + l32 * ldw32) : 0.f;  // W1: this chunk's weights, lane = edge
   for (int c = 0; c < maxlen; c += G) {
     const int idxn = (c + G + l32 < len) ? ldi(ic + G + l32) : 0;
+    const float wvn = (W1 && c + G + l32 < len) ? ldw_(wc + (G + l32) * ldw32) : 0.f;
 #pragma unroll
     for (int s = 0; s < G; s += U) {
       if (c + s >= maxlen) break;
@@ -867,7 +872,10 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
       if (c + s + U <= minlen) {  // full step for both items: no masks
 #pragma unroll
         for (int u = 0; u < U; ++u) xv[u] = row(bcastG<G>(idxv, s + u));
-        if (WEIGHTED) {
+        if (WEIGHTED && W1) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) wu[u] = __int_as_float(bcastG<G>(__float_as_int(wv), s + u));
+        } else if (WEIGHTED) {
           const float* wp = wc + (s + 2 * q) * ldw32;
           const float w0 = ldw_(wp), w1 = ldw_(wp + ldw32);
           wu[0] = quad_bcast<0>(w0); wu[1] = quad_bcast<0>(w1);
@@ -882,7 +890,7 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
           const int src = bcastG<G>(idxv, s + u);
           if (u < rem) {
             xv[u] = row(src);
-            if (WEIGHTED) wu[u] = ldw_(wc + (s + u) * ldw32);
+            if (WEIGHTED) wu[u] = W1 ? __int_as_float(bcastG<G>(__float_as_int(wv), s + u)) : ldw_(wc + (s + u) * ldw32);
           } else {
             xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (WEIGHTED) wu[u] = 0.f;
@@ -902,6 +910,7 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
       }
     }
     idxv = idxn;
+    if (W1) wv = wvn;
     ic += G;
     if (WEIGHTED) wc += static_cast<int64_t>(G) * ldw;
   }
@@ -2115,6 +2124,7 @@ int g_seg_nt = 2;          // non-temporal bits of the multi-item forms at F = 1
 int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
 int g_seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
 int g_apply_node_vec = 1;  // k_apply_node4 (float4, 32-bit index math) for the common apply_node shapes
+int g_seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
 int g_att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
 int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
 int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
@@ -2145,6 +2155,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "seg_lanes") { g_seg_lanes = static_cast<int>(value); return 0; }
   if (k == "seg_lean") { g_seg_lean = static_cast<int>(value); return 0; }
   if (k == "att_lean") { g_att_lean = static_cast<int>(value); return 0; }
+  if (k == "seg_lean_w1") { g_seg_lean_w1 = static_cast<int>(value); return 0; }
   if (k == "apply_node_vec") { g_apply_node_vec = static_cast<int>(value); return 0; }
   if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
   if (k == "mm_prefetch") { g_mm_prefetch = static_cast<int>(value); return 0; }
@@ -2388,10 +2399,11 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
         const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
         const bool lean = g_seg_lean && g_seg_u == 8 && n_cols < (1 << 24) &&
                           static_cast<uint64_t>(n_cols) * static_cast<uint64_t>(ldx) * 4u < (1ull << 32) &&
-                          (!w || lph32 == 4);
+                          (!w || lph32 == 4 || (heads == 1 && g_seg_lean_w1 && ldw < (int64_t(1) << 24)));
         const uint32_t rb = static_cast<uint32_t>(ldx * 4);
         if (lean) {
-          if (!w && g_seg_nt == 2) k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          if (w && heads == 1) k_agg_h32<true, 2, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (!w && g_seg_nt == 2) k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
           else if (!w) k_agg_h32<false, 0><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
           else if (g_seg_nt == 2) k_agg_h32<true, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
           else if (g_seg_nt == 1) k_agg_h32<true, 1><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
