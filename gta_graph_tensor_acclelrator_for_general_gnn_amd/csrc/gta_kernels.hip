@@ -1159,6 +1159,7 @@ struct BlockedView {
   int32_t* bucket;
   int64_t* row_ptr;
   int32_t* cnt;
+  int64_t* scan;  // scan scratch (kScanMaxTiles + 1)
   SegItem* items;
   int32_t* row_items;
 };
@@ -1167,9 +1168,11 @@ inline int64_t blocked_max_items(int64_t n_rows, int64_t nnz, int B, int64_t ite
   return std::min<int64_t>(n_rows * B, nnz) + nnz / item_edges;
 }
 
+constexpr int64_t kScanMaxTiles = 4096;  // plan-build scan (scan_excl): tile sums kept in the plan
+
 inline int64_t blocked_fixed_bytes(int64_t n_rows, int B) {
   return round16(128) + round16(n_rows * 4) + round16(n_rows * (B + 1) * 4) + round16(64 * 4) +
-         round16((n_rows + 1) * 8) + round16(n_rows * B * 4);
+         round16((n_rows + 1) * 8) + round16(n_rows * B * 4) + round16((kScanMaxTiles + 1) * 8);
 }
 
 BlockedView blocked_view(void* base, int64_t n_rows, int B, int64_t max_items) {
@@ -1181,6 +1184,7 @@ BlockedView blocked_view(void* base, int64_t n_rows, int B, int64_t max_items) {
   v.bucket = reinterpret_cast<int32_t*>(p); p += round16(64 * 4);
   v.row_ptr = reinterpret_cast<int64_t*>(p); p += round16((n_rows + 1) * 8);
   v.cnt = reinterpret_cast<int32_t*>(p); p += round16(n_rows * B * 4);
+  v.scan = reinterpret_cast<int64_t*>(p); p += round16((kScanMaxTiles + 1) * 8);
   v.items = reinterpret_cast<SegItem*>(p); p += round16(max_items * 16);
   v.row_items = reinterpret_cast<int32_t*>(p);
   return v;
@@ -1301,6 +1305,79 @@ __global__ void __launch_bounds__(1024) k_scan_excl(T* __restrict__ a, int64_t n
     if (total_at_end) a[n] = static_cast<T>(part[1023]);
     if (total) *total = part[1023];
   }
+}
+
+// Multi-workgroup form of k_scan_excl for the large plan arrays (n_rows * B counts): tile b =
+// [b * tile, (b + 1) * tile) of 1024 threads x kScanPer elements.  k_scan_tiles sums each tile
+// (coalesced), k_scan_excl scans the tile sums (sums[nt] = total), k_scan_apply rescans each tile
+// from its offset.  Same result as k_scan_excl.
+constexpr int kScanPer = 16;
+constexpr int64_t kScanTile = 1024 * kScanPer;
+
+template <typename T>
+__global__ void __launch_bounds__(1024) k_scan_tiles(const T* __restrict__ a, int64_t n, int64_t tile,
+                                                     int64_t* __restrict__ sums) {
+  __shared__ int64_t red[16];
+  const int t = threadIdx.x;
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * tile, b1 = min<int64_t>(n, b0 + tile);
+  int64_t s = 0;
+  for (int64_t i = b0 + t; i < b1; i += 1024) s += a[i];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
+  if ((t & 63) == 0) red[t >> 6] = s;
+  __syncthreads();
+  if (t == 0) {
+    int64_t tot = 0;
+    for (int w = 0; w < 16; ++w) tot += red[w];
+    sums[blockIdx.x] = tot;
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(1024) k_scan_apply(T* __restrict__ a, int64_t n, int64_t tile,
+                                                     const int64_t* __restrict__ offs, int64_t nt, int total_at_end,
+                                                     int64_t* __restrict__ total) {
+  __shared__ int64_t part[1024];
+  const int t = threadIdx.x;
+  const int64_t b0 = static_cast<int64_t>(blockIdx.x) * tile, b1 = min<int64_t>(n, b0 + tile);
+  const int64_t per = tile / 1024;
+  const int64_t e0 = min<int64_t>(b1, b0 + t * per), e1 = min<int64_t>(b1, e0 + per);
+  int64_t s = 0;
+  for (int64_t i = e0; i < e1; ++i) s += a[i];
+  part[t] = s;
+  __syncthreads();
+  for (int off = 1; off < 1024; off <<= 1) {  // Hillis-Steele inclusive scan
+    const int64_t x = (t >= off) ? part[t - off] : 0;
+    __syncthreads();
+    part[t] += x;
+    __syncthreads();
+  }
+  int64_t run = offs[blockIdx.x] + ((t == 0) ? 0 : part[t - 1]);
+  for (int64_t i = e0; i < e1; ++i) {
+    const int64_t x = a[i];
+    a[i] = static_cast<T>(run);
+    run += x;
+  }
+  if (blockIdx.x == nt - 1 && t == 0) {
+    if (total_at_end) a[n] = static_cast<T>(offs[nt]);
+    if (total) *total = offs[nt];
+  }
+}
+
+// exclusive scan of a[0, n) in place (a[n] = total when total_at_end; *total when given);
+// scratch holds kScanMaxTiles + 1 int64
+template <typename T>
+void scan_excl(T* a, int64_t n, int total_at_end, int64_t* total, int64_t* scratch, hipStream_t s) {
+  int64_t tile = kScanTile;
+  while ((n + tile - 1) / tile > kScanMaxTiles) tile *= 2;
+  const int64_t nt = (n + tile - 1) / tile;
+  if (nt <= 1) {
+    k_scan_excl<T><<<1, 1024, 0, s>>>(a, n, total_at_end, total);
+    return;
+  }
+  k_scan_tiles<T><<<dim3(static_cast<unsigned>(nt)), dim3(1024), 0, s>>>(a, n, tile, scratch);
+  k_scan_excl<int64_t><<<1, 1024, 0, s>>>(scratch, nt, 1, nullptr);
+  k_scan_apply<T><<<dim3(static_cast<unsigned>(nt)), dim3(1024), 0, s>>>(a, n, tile, scratch, nt, total_at_end, total);
 }
 
 // items of (block b, perm position i): near-equal parts of the segment, item ids
@@ -2327,13 +2404,13 @@ int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indic
   GTA_LAUNCHED("k_blocked_scan");
   k_blocked_perm<<<dim3(static_cast<unsigned>((n_rows + 255) / 256)), dim3(256), 0, s>>>(indptr, n_rows, v);
   GTA_LAUNCHED("k_blocked_perm");
-  k_scan_excl<int64_t><<<1, 1024, 0, s>>>(v.row_ptr, n_rows, 1, nullptr);  // items per row -> row_ptr
-  GTA_LAUNCHED("k_scan_excl");
+  scan_excl<int64_t>(v.row_ptr, n_rows, 1, nullptr, v.scan, s);  // items per row -> row_ptr
+  GTA_LAUNCHED("scan_excl");
   const dim3 gk(static_cast<unsigned>((n_rows * B + 255) / 256));
   k_blocked_cnt<<<gk, dim3(256), 0, s>>>(n_rows, B, item_edges, row_edges, v);
   GTA_LAUNCHED("k_blocked_cnt");
-  k_scan_excl<int32_t><<<1, 1024, 0, s>>>(v.cnt, n_rows * B, 0, &v.hdr[4]);  // -> first item id, n_items
-  GTA_LAUNCHED("k_scan_excl");
+  scan_excl<int32_t>(v.cnt, n_rows * B, 0, &v.hdr[4], v.scan, s);  // -> first item id, n_items
+  GTA_LAUNCHED("scan_excl");
   k_blocked_items<<<gk, dim3(256), 0, s>>>(indptr, n_rows, B, item_edges, row_edges, v);
   GTA_LAUNCHED("k_blocked_items");
   return GTA_OK;
