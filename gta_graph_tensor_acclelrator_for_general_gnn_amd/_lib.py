@@ -48,6 +48,9 @@ SIGNATURES = {
     "gta_apply_node": (_i32, [_i32, _i32, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp]),
     "gta_update_mm": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
     "gta_update_mm_t": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
+    "gta_update_mm_t_split_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
+    "gta_update_mm_t_split": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _i64, _vp,
+                                     _i64, _vp]),
     "gta_tile_nnz": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "gta_debug_set": (_i32, [_cp, _i64]),
 }

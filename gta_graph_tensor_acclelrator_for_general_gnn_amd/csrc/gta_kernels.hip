@@ -1943,7 +1943,18 @@ k_mm_bf16(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
 template <typename TA, typename WT, int NT, bool PF = false>  // PF: prefetch the next A fragment
 __global__ void __launch_bounds__(kBlock, PF ? 4 : 1)
 k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
-          const WT* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo) {
+          const WT* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
+          int64_t kslice = 0, int64_t oslice = 0) {
+  // split K (kslice > 0): block row y contracts k in [y * kslice, (y + 1) * kslice) into its own
+  // partial out + y * oslice (no SF); k_mm_slices_sum adds the slices in order
+  if (kslice > 0) {
+    const int64_t kb = static_cast<int64_t>(blockIdx.y) * kslice;
+    x += kb;
+    wt += kb;
+    K = static_cast<int>(min<int64_t>(kslice, K - kb));
+    out += static_cast<int64_t>(blockIdx.y) * oslice;
+    sf = GTA_SF_NONE;
+  }
   constexpr bool BF = sizeof(WT) == 2;
   constexpr int KS = BF ? 32 : 16;         // k covered by one A-fragment load
   constexpr int KC = BF ? (NT >= 8 ? 128 : 256) : (NT >= 8 ? 64 : 128);  // K chunk staged in LDS (<= 35 KB)
@@ -2116,6 +2127,19 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
           const int n = n0 + 16 * c + r16;
           if (m < M && n < N) out[m * ldo + n] = sf_apply(sf, acc[i][c][r]);
         }
+  }
+}
+
+// out[m, n] = sf(sum_s ws[s][m][n]) in slice order (split-K UPDATE; ws slices are [M, N] dense)
+__global__ void __launch_bounds__(kBlock)
+k_mm_slices_sum(const float* __restrict__ ws, int S, int64_t M, int N, int sf, float* __restrict__ out, int64_t ldo) {
+  const int64_t total = M * N;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < total;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    float a = 0.f;
+    for (int k = 0; k < S; ++k) a += ws[k * total + t];
+    const int64_t m = t / N;
+    out[m * ldo + (t - m * N)] = sf_apply(sf, a);
   }
 }
 
@@ -2849,6 +2873,57 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
 #undef GTA_MMR_NT
 #undef GTA_MMR
   GTA_LAUNCHED("k_mm_rows");
+  return GTA_OK;
+}
+
+// K slice of the split form: a multiple of 32 (whole fp32 and bf16 A fragments)
+static int64_t mm_kslice(int64_t K, int64_t splits) {
+  return std::max<int64_t>(32, ((K + splits - 1) / splits + 31) / 32 * 32);
+}
+
+int64_t gta_update_mm_t_split_workspace_bytes(int64_t M, int64_t K, int64_t N, int64_t splits) {
+  if (M < 0 || K <= 0 || N <= 0 || splits < 1) return fail(GTA_ERR_ARG, "update_mm_t_split_workspace_bytes: bad sizes");
+  const int64_t nsl = (K + mm_kslice(K, splits) - 1) / mm_kslice(K, splits);
+  return nsl * M * N * static_cast<int64_t>(sizeof(float));
+}
+
+int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
+                          int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, int64_t splits,
+                          void* workspace, int64_t workspace_bytes, void* stream) {
+  if (M < 0 || K <= 0 || N <= 0 || ldwt < K || splits < 1) return fail(GTA_ERR_ARG, "update_mm_t_split: bad sizes");
+  if (M == 0) return GTA_OK;
+  if (!x || !wt || !out || !workspace) return fail(GTA_ERR_ARG, "update_mm_t_split: bad arguments");
+  if (K > INT32_MAX || N > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t_split: K/N too large");
+  if (dtype != GTA_F32 && dtype != GTA_BF16 && dtype != GTA_F32_BF16) return fail(GTA_ERR_ARG, "update_mm_t_split: bad dtype");
+  const int64_t ks = mm_kslice(K, splits), nsl = (K + ks - 1) / ks;
+  if (workspace_bytes < nsl * M * N * static_cast<int64_t>(sizeof(float)))
+    return fail(GTA_ERR_ARG, "update_mm_t_split: workspace too small");
+  if (nsl > 65535) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t_split: too many slices");
+  float* ws = static_cast<float*>(workspace);
+  const int nt = N <= 16 ? 1 : N <= 32 ? 2 : N <= 64 ? 4 : 8;
+  const int64_t groups = (M + 127) / 128;
+  const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
+  const dim3 gr(static_cast<unsigned>(groups * ncb), static_cast<unsigned>(nsl));
+  const bool pf = g_mm_prefetch == 2 || (g_mm_prefetch == 1 && (dtype != GTA_BF16 || ks % 32 == 0));
+  const int ki = static_cast<int>(K);
+  hipStream_t s = S(stream);
+#define GTA_MMS(TA_, WT_, NT_)                                                                                    \
+  if (pf) k_mm_rows<TA_, WT_, NT_, true><<<gr, dim3(kBlock), 0, s>>>(static_cast<const TA_*>(x), ldx, row_idx, M, ki, \
+      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N);                                 \
+  else k_mm_rows<TA_, WT_, NT_><<<gr, dim3(kBlock), 0, s>>>(static_cast<const TA_*>(x), ldx, row_idx, M, ki,          \
+      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N)
+#define GTA_MMS_NT(TA_, WT_) \
+  if (nt == 1) GTA_MMS(TA_, WT_, 1); else if (nt == 2) GTA_MMS(TA_, WT_, 2); else if (nt == 4) GTA_MMS(TA_, WT_, 4); else GTA_MMS(TA_, WT_, 8)
+  if (dtype == GTA_F32) { GTA_MMS_NT(float, float); }
+  else if (dtype == GTA_BF16) { GTA_MMS_NT(uint16_t, uint16_t); }
+  else { GTA_MMS_NT(float, uint16_t); }
+#undef GTA_MMS_NT
+#undef GTA_MMS
+  GTA_LAUNCHED("k_mm_rows<split>");
+  const int64_t total = M * N;
+  k_mm_slices_sum<<<dim3(static_cast<unsigned>(std::min<int64_t>((total + kBlock - 1) / kBlock, 4096))), dim3(kBlock), 0,
+                    s>>>(ws, static_cast<int>(nsl), M, static_cast<int>(N), sf, out, ldo);
+  GTA_LAUNCHED("k_mm_slices_sum");
   return GTA_OK;
 }
 

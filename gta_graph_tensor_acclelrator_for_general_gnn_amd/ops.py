@@ -434,7 +434,15 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
         out = torch.empty(M, N, dtype=torch.float32, device=x.device)
     ldo = _rows(out, "out")
     dt = _lib.GTA_F32_BF16 if mixed else (_lib.GTA_F32 if x.dtype == torch.float32 else _lib.GTA_BF16)
-    if MM_FORM == "rows" and M >= MM_ROWS_MIN_M:  # row-streaming kernel on W^T (cached per weight version)
+    splits = _mm_splits(M, K, N) if MM_FORM == "rows" else 1
+    if splits > 1:  # few rows: split K over blocks, slices summed in order (deterministic)
+        wt = _transposed(w)
+        nb = check(_L().gta_update_mm_t_split_workspace_bytes(M, K, N, splits), "update_mm_t_split_workspace_bytes")
+        ws = torch.empty(max(1, nb // 4), dtype=torch.float32, device=x.device)
+        check(_L().gta_update_mm_t_split(_ptr(x), ldx, _ptr(row_idx), M, K, _ptr(wt), _rows(wt, "w^T", wt.dtype), N,
+                                         dt, _sf(sf), _ptr(out), ldo, splits, _ptr(ws), nb, _stream(x.device)),
+              "update_mm_t_split")
+    elif MM_FORM == "rows" and M >= MM_ROWS_MIN_M:  # row-streaming kernel on W^T (cached per weight version)
         wt = _transposed(w)
         check(_L().gta_update_mm_t(_ptr(x), ldx, _ptr(row_idx), M, K, _ptr(wt), _rows(wt, "w^T", wt.dtype), N, dt, _sf(sf),
                                    _ptr(out), ldo, _stream(x.device)), "update_mm_t")
@@ -445,8 +453,17 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
 
 
 MM_FORM = "rows"  # "rows": gta_update_mm_t (x read once per output); "tile": gta_update_mm 64x64 tiles
+MM_SPLIT_MAX_BLOCKS = 128  # split K when the row-streaming grid has fewer blocks than this (of 256 CUs)
 MM_ROWS_MIN_M = 32768  # below this the 128-row groups are too few to fill 256 CUs: 64x64 tiles win
 _WT_CACHE = {}
+
+
+def _mm_splits(M, K, N):
+    """K slices for gta_update_mm_t_split: enough blocks for ~2 per CU, slices of >= 64 k; 1 = no split."""
+    blocks = -(-M // 128) * -(-N // 128)
+    if K < 256 or blocks >= MM_SPLIT_MAX_BLOCKS:
+        return 1
+    return max(1, min(16, -(-512 // blocks), K // 64))
 
 
 def _transposed(w):

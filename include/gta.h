@@ -221,6 +221,16 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
 int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                     int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream);
 
+/* Split-K form of gta_update_mm_t for few rows (M small against the chip): the K axis is cut
+ * into slices of ceil(K / splits) rounded up to 32; each slice's partial [M, N] goes to the
+ * workspace (gta_update_mm_t_split_workspace_bytes) and a second kernel adds the slices in order
+ * and applies sf.  Deterministic; the contraction order differs from gta_update_mm_t (fp32
+ * rounding only).  Same reference as gta_update_mm. */
+int64_t gta_update_mm_t_split_workspace_bytes(int64_t M, int64_t K, int64_t N, int64_t splits);
+int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
+                          int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, int64_t splits,
+                          void* workspace, int64_t workspace_bytes, void* stream);
+
 /* ---- f2 TILE-NNZ metadata ----------------------------------------------
  * counts[t, j] = #{ distinct (dst, j) : dst in [t*T, (t+1)*T), an edge dst <- j, dst != j }
  * for t < ceil(n_rows/T), j < n_cols (int32 [ceil(n_rows/T), n_cols]).

@@ -636,3 +636,30 @@ def test_update_mm_prefetch_forms(dev, pf, M, K, N, dt):
         xr = torch.from_numpy(xr).to(torch.bfloat16).double().numpy()
     wf = w.float().numpy().astype(np.float64)
     _check(out, xr @ wf, np.abs(xr) @ np.abs(wf), f"update_mm pf={pf} {dt}")
+
+
+@pytest.mark.parametrize("M,K,N,dt,gathered", [(2708, 1433, 128, "f32", False), (2708, 1433, 128, "f32", True),
+                                                (1000, 602, 64, "f32", False), (700, 1000, 16, "bf16", False),
+                                                (1500, 300, 200, "mixed", True), (333, 290, 128, "f32", False)])
+def test_update_mm_split_k(dev, M, K, N, dt, gathered):
+    """Split-K UPDATE for few rows (K slices of >= 32 summed in order by k_mm_slices_sum, SF applied
+    after the sum) vs fp64; deterministic run to run."""
+    rng = np.random.default_rng(M + K + N)
+    x = torch.from_numpy(rng.standard_normal((M + 7, K)).astype(np.float32))
+    w = torch.from_numpy(rng.standard_normal((K, N)).astype(np.float32))
+    if dt == "bf16":
+        x, w = x.to(torch.bfloat16), w.to(torch.bfloat16)
+    elif dt == "mixed":
+        w = w.to(torch.bfloat16)
+    idx = torch.from_numpy(rng.integers(0, M + 7, M).astype(np.int32)) if gathered else None
+    assert ops._mm_splits(M, K, N) > 1
+    xd, wd = x.to(dev), w.to(dev)
+    idd = None if idx is None else idx.to(dev)
+    out = ops.update_mm(xd, wd, idd, sf="RELU", m=None if gathered else M)
+    again = ops.update_mm(xd, wd, idd, sf="RELU", m=None if gathered else M)
+    assert torch.equal(out, again)
+    xr = x.to(torch.bfloat16).float().numpy() if dt != "f32" else x.numpy()
+    wf = w.float().numpy()
+    xs = xr[idx.numpy()] if gathered else xr[:M]
+    ref = isa_ref.mm(xs, wf, sf_kind="RELU")
+    _check(out, ref, np.abs(xs).astype(np.float64) @ np.abs(wf).astype(np.float64), f"split-K {dt}")
