@@ -933,11 +933,16 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
 // addressed like X rows (uniform base + 32-bit byte offset).  Same per-lane edge order, fma chain
 // and per-head sum order as the generic form: bitwise equal to it.  Slab row k: 128 partials,
 // then the 8 per-head sums of v.
+// Direct epilogue (row_ptr given): an item that is its row's only item (low-degree rows at
+// small B) writes y (and sums) itself, exactly as the ordered reduce would (0 + p = p), and the
+// reduce skips its row (k_seg_reduce_att with skip_single).
 template <int NT>
 __global__ void __launch_bounds__(kBlock)
 k_att_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
           uint32_t row_bytes, const float* __restrict__ a, int64_t lda, const float* __restrict__ b,
-          uint32_t brow_bytes, float* __restrict__ slabs, const SegItem* __restrict__ items) {
+          uint32_t brow_bytes, float* __restrict__ slabs, const SegItem* __restrict__ items,
+          const int64_t* __restrict__ row_ptr = nullptr, int normalize = 1, float* __restrict__ y = nullptr,
+          int64_t ldy = 0, float* __restrict__ sums = nullptr) {
   constexpr int G = 32, U = 8, F = 128, LDS = F + 8;
   const int lane = threadIdx.x & (kWave - 1);
   const int l32 = lane & (G - 1);
@@ -1017,6 +1022,17 @@ k_att_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
     ic += G;
   }
   if (len > 0) {
+    if (row_ptr != nullptr && row_ptr[it.row + 1] - row_ptr[it.row] == 1) {  // the row's only item
+      const float sh = 0.f + ssum;
+      float4 v;
+      v.x = 0.f + acc[0]; v.y = 0.f + acc[1]; v.z = 0.f + acc[2]; v.w = 0.f + acc[3];
+      if (normalize) {
+        v.x /= sh; v.y /= sh; v.z /= sh; v.w /= sh;
+      }
+      *reinterpret_cast<float4*>(y + static_cast<int64_t>(it.row) * ldy + l32 * 4) = v;
+      if (sums != nullptr && q == 0) sums[static_cast<int64_t>(it.row) * 8 + h] = sh;
+      return;
+    }
     float* o = slabs + k * LDS;
 #pragma unroll
     for (int t = 0; t < 4; ++t) {
@@ -1099,10 +1115,11 @@ k_seg_reduce(int64_t n_rows, const float* __restrict__ slabs, const float* __res
 template <int VW>
 __global__ void __launch_bounds__(kBlock)
 k_seg_reduce_att(int64_t n_rows, const float* __restrict__ slabs, int H, int normalize, float* __restrict__ y,
-                 int64_t ldy, float* __restrict__ sums, RowItems ri) {
+                 int64_t ldy, float* __restrict__ sums, RowItems ri, int skip_single = 0) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
   if (row >= n_rows) return;
+  if (skip_single && ri.row_ptr[row + 1] - ri.row_ptr[row] == 1) return;  // written by its item
   const int col = lane * VW;
   constexpr int F = kWave * VW;
   const int64_t lds = F + ((H + 3) & ~3);
@@ -2226,6 +2243,7 @@ int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (
 int g_seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
 int g_apply_node_vec = 1;  // k_apply_node4 (float4, 32-bit index math) for the common apply_node shapes
 int g_seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
+int g_att_direct = 1;      // k_att_h32: a row's only item writes y itself, the reduce skips the row
 int g_att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
 int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
 int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
@@ -2256,6 +2274,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "seg_lanes") { g_seg_lanes = static_cast<int>(value); return 0; }
   if (k == "seg_lean") { g_seg_lean = static_cast<int>(value); return 0; }
   if (k == "att_lean") { g_att_lean = static_cast<int>(value); return 0; }
+  if (k == "att_direct") { g_att_direct = static_cast<int>(value); return 0; }
   if (k == "seg_lean_w1") { g_seg_lean_w1 = static_cast<int>(value); return 0; }
   if (k == "apply_node_vec") { g_apply_node_vec = static_cast<int>(value); return 0; }
   if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
@@ -2620,6 +2639,7 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
   const int64_t* nit = &v.hdr[4];
   const dim3 g4(static_cast<unsigned>((items + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock))), blk(kBlock);
   const SegItem* it = v.items;
+  int skip_single = 0;  // rows whose only item wrote y directly (k_att_h32)
   if (items > 0) {  // no edges: no items, the reduce alone writes the empty rows
   const bool elr = sf == GTA_SF_EXP_LEAKY_RELU;  // GAT's score function, specialised
 #define GTA_ATT(VW_, U_)                                                                                          \
@@ -2634,10 +2654,15 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
   if (lean) {
     const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
     const uint32_t rb = static_cast<uint32_t>(ldx * 4), bbytes = static_cast<uint32_t>(ldb * 4);
+    const bool direct = g_att_direct && ldy % 4 == 0 && aligned(y, 16);
+    skip_single = direct;
+    const int64_t* rp = direct ? v.row_ptr : nullptr;
     if (g_att_lean == 2)
-      k_att_h32<2><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it);
+      k_att_h32<2><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it, rp, normalize, y,
+                                       ldy, sums);
     else
-      k_att_h32<0><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it);
+      k_att_h32<0><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it, rp, normalize, y,
+                                       ldy, sums);
   } else if (F == 128 && g_seg_lanes == 32 && (F / heads) % 4 == 0 && lph32 >= 1 && 32 % lph32 == 0) {
     const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
     if (elr) k_agg_seg4<4, 8, false, 0, true, GTA_SF_EXP_LEAKY_RELU, 32><<<g2h, blk, 0, s>>>(
@@ -2651,7 +2676,7 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
   const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
   const int H = static_cast<int>(heads);
   if (F == 64) k_seg_reduce_att<1><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri);
-  else if (F == 128) k_seg_reduce_att<2><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri);
+  else if (F == 128) k_seg_reduce_att<2><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri, skip_single);
   else k_seg_reduce_att<4><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri);
   GTA_LAUNCHED("k_seg_reduce_att");
   return GTA_OK;

@@ -524,7 +524,10 @@ class Executor:
         if x.dtype != torch.float32 or not ops.BlockedPlan.supports_att(F, H):
             return None
         B = self.attention_blocks or ops.BlockedPlan.auto_blocks(self.graph, F)
-        if B < (1 if self.attention_blocks else 4) or not ops.blocked_ready(self.graph, B):
+        # the lean fused kernel (F = 128, 8 heads) beats softmax + aggregate even unblocked (B = 1:
+        # Flickr 102 vs 168 us, scripts/att_small_probe.py); other shapes need a blocked table
+        lean = F == 128 and H == 8
+        if B < (1 if (self.attention_blocks or lean) else 4) or not ops.blocked_ready(self.graph, B):
             return None
         norm = pat["D"] is not None
         G = pat["G"]
