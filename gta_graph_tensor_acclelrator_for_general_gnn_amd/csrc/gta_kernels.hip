@@ -1961,7 +1961,7 @@ template <typename TA, typename WT, int NT, bool PF = false>  // PF: prefetch th
 __global__ void __launch_bounds__(kBlock, PF ? 4 : 1)
 k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const WT* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
-          int64_t kslice = 0, int64_t oslice = 0) {
+          int64_t kslice = 0, int64_t oslice = 0, int vec_store = 0) {
   // split K (kslice > 0): block row y contracts k in [y * kslice, (y + 1) * kslice) into its own
   // partial out + y * oslice (no SF); k_mm_slices_sum adds the slices in order
   if (kslice > 0) {
@@ -1992,6 +1992,7 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
   const bool wvec = (ldwt % WV == 0) && aligned(wt, 16);
   const int64_t n_groups = (M + 127) / 128;
   const bool one_chunk = K <= KC;
+  const bool vstore = vec_store && ldo % 4 == 0 && aligned(out, 16);  // 16-B output rows
 
   auto stage = [&](int kc) {
     if (wvec) {
@@ -2134,16 +2135,54 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
       }
       if (!one_chunk) __syncthreads();
     }
+    if (vstore) {
+      // lane (g, r16 = 4q + p) holds C[4g + r][4q + p], r = 0..3; a 4x4 transpose inside each
+      // lane quad (DPP swaps of lane bit 0, then bit 1) leaves C[4g + p][4q + r] -- four
+      // consecutive columns of one row -- for one 16-B store instead of four dword stores
+      const int p = r16 & 3, q = r16 >> 2;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int c = 0; c < NT; ++c)
+        for (int c = 0; c < NT; ++c) {
+          float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int64_t m = mw + 16 * i + 4 * g + r;
-          const int n = n0 + 16 * c + r16;
-          if (m < M && n < N) out[m * ldo + n] = sf_apply(sf, acc[i][c][r]);
+          for (int r = 0; r < 4; ++r) v[r] = sf_apply(sf, acc[i][c][r]);
+#pragma unroll
+          for (int m2 = 0; m2 < 2; ++m2) {  // bit 0: registers (2m2, 2m2+1) across lanes (p, p^1)
+            const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
+            const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2 + 1]), 0xB1, 0xF, 0xF, false));
+            if (p & 1) v[2 * m2] = sb; else v[2 * m2 + 1] = sa;
+          }
+#pragma unroll
+          for (int m2 = 0; m2 < 2; ++m2) {  // bit 1: registers (m2, m2+2) across lanes (p, p^2)
+            const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2]), 0x4E, 0xF, 0xF, false));
+            const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2 + 2]), 0x4E, 0xF, 0xF, false));
+            if (p & 2) v[m2] = sb; else v[m2 + 2] = sa;
+          }
+          const int64_t m = mw + 16 * i + 4 * g + p;
+          const int n = n0 + 16 * c + 4 * q;
+          if (m < M) {
+            if (n + 3 < N) {
+              *reinterpret_cast<float4*>(out + m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (n + r < N) out[m * ldo + n + r] = v[r];
+            }
+          }
         }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int c = 0; c < NT; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t m = mw + 16 * i + 4 * g + r;
+            const int n = n0 + 16 * c + r16;
+            if (m < M && n < N) out[m * ldo + n] = sf_apply(sf, acc[i][c][r]);
+          }
+    }
   }
 }
 
@@ -2245,6 +2284,7 @@ int g_apply_node_vec = 1;  // k_apply_node4 (float4, 32-bit index math) for the 
 int g_seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
 int g_att_direct = 1;      // k_att_h32: a row's only item writes y itself, the reduce skips the row
 int g_att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
+int g_mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
 int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
 int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
 int g_apply_edge_form = 1;  // 1: row-sweep K3 kernels (cols / pack); 0: the generic per-element kernel
@@ -2279,6 +2319,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "apply_node_vec") { g_apply_node_vec = static_cast<int>(value); return 0; }
   if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
   if (k == "mm_prefetch") { g_mm_prefetch = static_cast<int>(value); return 0; }
+  if (k == "mm_vstore") { g_mm_vstore = static_cast<int>(value); return 0; }
   if (k == "mm_blocks_per_cu") { g_mm_blocks_per_cu = value; return 0; }
   if (k == "apply_edge_form") { g_apply_edge_form = static_cast<int>(value); return 0; }
   if (k == "esm_lane") { g_esm_lane = static_cast<int>(value); return 0; }
@@ -2886,10 +2927,11 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
 #define GTA_MMR(TA_, WT_, NT_)                                                                                \
   if (pf) k_mm_rows<TA_, WT_, NT_, true><<<gr, dim3(kBlock), 0, S(stream)>>>(                        \
       static_cast<const TA_*>(x), ldx, row_idx, M, static_cast<int>(K), static_cast<const WT_*>(wt), ldwt,        \
-      static_cast<int>(N), sf, out, ldo);                                                                         \
+      static_cast<int>(N), sf, out, ldo, 0, 0, g_mm_vstore);                                                      \
   else k_mm_rows<TA_, WT_, NT_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const TA_*>(x), ldx, row_idx, M, \
                                                                     static_cast<int>(K), static_cast<const WT_*>(wt), \
-                                                                    ldwt, static_cast<int>(N), sf, out, ldo)
+                                                                    ldwt, static_cast<int>(N), sf, out, ldo, 0, 0,  \
+                                                                    g_mm_vstore)
 #define GTA_MMR_NT(TA_, WT_) \
   if (nt == 1) GTA_MMR(TA_, WT_, 1); else if (nt == 2) GTA_MMR(TA_, WT_, 2); else if (nt == 4) GTA_MMR(TA_, WT_, 4); else GTA_MMR(TA_, WT_, 8)
   if (dtype == GTA_F32) { GTA_MMR_NT(float, float); }
@@ -2934,9 +2976,9 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
   hipStream_t s = S(stream);
 #define GTA_MMS(TA_, WT_, NT_)                                                                                    \
   if (pf) k_mm_rows<TA_, WT_, NT_, true><<<gr, dim3(kBlock), 0, s>>>(static_cast<const TA_*>(x), ldx, row_idx, M, ki, \
-      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N);                                 \
+      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N, g_mm_vstore);                                 \
   else k_mm_rows<TA_, WT_, NT_><<<gr, dim3(kBlock), 0, s>>>(static_cast<const TA_*>(x), ldx, row_idx, M, ki,          \
-      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N)
+      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N, g_mm_vstore)
 #define GTA_MMS_NT(TA_, WT_) \
   if (nt == 1) GTA_MMS(TA_, WT_, 1); else if (nt == 2) GTA_MMS(TA_, WT_, 2); else if (nt == 4) GTA_MMS(TA_, WT_, 4); else GTA_MMS(TA_, WT_, 8)
   if (dtype == GTA_F32) { GTA_MMS_NT(float, float); }

@@ -663,3 +663,31 @@ def test_update_mm_split_k(dev, M, K, N, dt, gathered):
     xs = xr[idx.numpy()] if gathered else xr[:M]
     ref = isa_ref.mm(xs, wf, sf_kind="RELU")
     _check(out, ref, np.abs(xs).astype(np.float64) @ np.abs(wf).astype(np.float64), f"split-K {dt}")
+
+
+@pytest.mark.parametrize("M,K,N,dt,gathered", [(5000, 602, 128, "f32", False), (4099, 100, 130, "mixed", True),
+                                                (3001, 128, 8, "bf16", False), (2708, 1433, 128, "f32", False),
+                                                (777, 64, 200, "f32", True)])
+def test_update_mm_vector_store_bitwise(dev, M, K, N, dt, gathered):
+    """k_mm_rows' quad-transposed 16-B row-store epilogue == the four-dword-store epilogue bitwise
+    (row-streaming and split-K forms, column tails, gathered rows)."""
+    rng = np.random.default_rng(M + N)
+    x = torch.from_numpy(rng.standard_normal((M + 3, K)).astype(np.float32))
+    w = torch.from_numpy(rng.standard_normal((K, N)).astype(np.float32))
+    if dt == "bf16":
+        x, w = x.to(torch.bfloat16), w.to(torch.bfloat16)
+    elif dt == "mixed":
+        w = w.to(torch.bfloat16)
+    idx = torch.from_numpy(rng.integers(0, M + 3, M).astype(np.int32)).to(dev) if gathered else None
+    xd, wd = x.to(dev), w.to(dev)
+    outs = []
+    old_min = ops.MM_ROWS_MIN_M
+    try:
+        ops.MM_ROWS_MIN_M = 0
+        for vs in (1, 0):
+            ops.set_debug("mm_vstore", vs)
+            outs.append(ops.update_mm(xd, wd, idx, sf="RELU", m=None if gathered else M))
+    finally:
+        ops.set_debug("mm_vstore", 1)
+        ops.MM_ROWS_MIN_M = old_min
+    assert torch.equal(outs[0], outs[1])
