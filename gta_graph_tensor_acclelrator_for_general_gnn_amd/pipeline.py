@@ -62,8 +62,10 @@ class Layer:
         blocks += [[op.idx] for op in g.ops if op.idx not in used]
         return blocks
 
-    def run(self, tensors, plan_chunk=512, model=None):
-        res, ex = executor.run_stream(self.opgraph, self.stream, self.graph, tensors, self.sem, plan_chunk)
+    def run(self, tensors, plan_chunk=512, model=None, sync=True):
+        """sync=False: no device synchronisation around the stream (res.elapsed_s is then host time
+        only); a multi-layer forward synchronises once at its end instead of twice per layer."""
+        res, ex = executor.run_stream(self.opgraph, self.stream, self.graph, tensors, self.sem, plan_chunk, sync=sync)
         if model:
             executor.attach_model(res, self.stream_records, self.tile_size_list, self.graph, model)
         return res, ex

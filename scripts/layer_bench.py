@@ -26,7 +26,7 @@ def main(names=None, reps=5, trace=False, graphed=False):
             for lay, t in zip(layers, tensors):
                 if x is not None:
                     t["x"] = x
-                res, _ = lay.run(t)
+                res, _ = lay.run(t, sync=False)  # one synchronisation per forward, at its end
                 x = res.outputs[sorted(res.outputs)[-1]]
             torch.cuda.synchronize()
             if r:
