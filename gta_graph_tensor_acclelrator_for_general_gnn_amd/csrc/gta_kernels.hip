@@ -2282,7 +2282,7 @@ int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (
 int g_seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
 int g_apply_node_vec = 1;  // k_apply_node4 (float4, 32-bit index math) for the common apply_node shapes
 int g_seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
-int g_att_direct = 1;      // k_att_h32: a row's only item writes y itself, the reduce skips the row
+int g_att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
 int g_att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
 int g_mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
 int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
@@ -2695,7 +2695,9 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
   if (lean) {
     const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
     const uint32_t rb = static_cast<uint32_t>(ldx * 4), bbytes = static_cast<uint32_t>(ldb * 4);
-    const bool direct = g_att_direct && ldy % 4 == 0 && aligned(y, 16);
+    // single-item rows are common only when few blocks cut the rows (low degree, B <= 2); above
+    // that the row_ptr reads at every item's end cost more than the rare direct writes save
+    const bool direct = (g_att_direct == 2 || (g_att_direct == 1 && B <= 2)) && ldy % 4 == 0 && aligned(y, 16);
     skip_single = direct;
     const int64_t* rp = direct ? v.row_ptr : nullptr;
     if (g_att_lean == 2)
