@@ -1177,8 +1177,11 @@ struct BlockedView {
   int64_t* row_ptr;
   int32_t* cnt;
   int64_t* scan;  // scan scratch (kScanMaxTiles + 1)
+  int32_t* lhist;  // [2][64][kLenBins]: item-length histogram per block, then placement cursors
   SegItem* items;
   int32_t* row_items;
+  int32_t* item_slot;  // position of item k in row_items (for the length sort)
+  SegItem* items_tmp;  // length-sorted items before they are copied back
 };
 
 inline int64_t blocked_max_items(int64_t n_rows, int64_t nnz, int B, int64_t item_edges) {
@@ -1187,9 +1190,12 @@ inline int64_t blocked_max_items(int64_t n_rows, int64_t nnz, int B, int64_t ite
 
 constexpr int64_t kScanMaxTiles = 4096;  // plan-build scan (scan_excl): tile sums kept in the plan
 
+constexpr int kLenBins = 257;  // item length keys 256 - min(len, 256): longest first
+
 inline int64_t blocked_fixed_bytes(int64_t n_rows, int B) {
   return round16(128) + round16(n_rows * 4) + round16(n_rows * (B + 1) * 4) + round16(64 * 4) +
-         round16((n_rows + 1) * 8) + round16(n_rows * B * 4) + round16((kScanMaxTiles + 1) * 8);
+         round16((n_rows + 1) * 8) + round16(n_rows * B * 4) + round16((kScanMaxTiles + 1) * 8) +
+         round16(2 * 64 * kLenBins * 4);
 }
 
 BlockedView blocked_view(void* base, int64_t n_rows, int B, int64_t max_items) {
@@ -1202,13 +1208,17 @@ BlockedView blocked_view(void* base, int64_t n_rows, int B, int64_t max_items) {
   v.row_ptr = reinterpret_cast<int64_t*>(p); p += round16((n_rows + 1) * 8);
   v.cnt = reinterpret_cast<int32_t*>(p); p += round16(n_rows * B * 4);
   v.scan = reinterpret_cast<int64_t*>(p); p += round16((kScanMaxTiles + 1) * 8);
+  v.lhist = reinterpret_cast<int32_t*>(p); p += round16(2 * 64 * kLenBins * 4);
   v.items = reinterpret_cast<SegItem*>(p); p += round16(max_items * 16);
-  v.row_items = reinterpret_cast<int32_t*>(p);
+  v.row_items = reinterpret_cast<int32_t*>(p); p += round16(max_items * 4);
+  v.item_slot = reinterpret_cast<int32_t*>(p); p += round16(max_items * 4);
+  v.items_tmp = reinterpret_cast<SegItem*>(p);
   return v;
 }
 
 int64_t blocked_bytes(int64_t n_rows, int B, int64_t max_items) {
-  return blocked_fixed_bytes(n_rows, B) + round16(max_items * 16) + round16(max_items * 4);
+  return blocked_fixed_bytes(n_rows, B) + round16(max_items * 16) + round16(max_items * 4) + round16(max_items * 4) +
+         round16(max_items * 16);
 }
 
 __device__ __forceinline__ int deg_bucket(int64_t d) {  // 31 = heaviest ... 0 = empty/1
@@ -1422,7 +1432,39 @@ __global__ void k_blocked_items(const int64_t* __restrict__ indptr, int64_t n_ro
     it.len = static_cast<int32_t>(max<int64_t>(0, min<int64_t>(part, len - j * part)));
     v.items[id0 + j] = it;
     v.row_items[slot0 + j] = static_cast<int32_t>(id0 + j);
+    v.item_slot[id0 + j] = static_cast<int32_t>(slot0 + j);
+    atomicAdd(&v.lhist[b * kLenBins + 256 - min(it.len, 256)], 1);
   }
+}
+
+// length sort of each block's items (longest first), so the two half-wave items of a wave
+// hold about the same number of edges and finish together.  Only item ids move: each row's
+// row_items keep their (block, part) order, so the reduce -- and every result -- is unchanged.
+__device__ __forceinline__ int len_key(int len) { return 256 - min(len, 256); }
+
+__global__ void k_items_len_scan(BlockedView v, int64_t n_rows, int B) {
+  const int b = threadIdx.x;
+  if (b >= B) return;
+  int run = v.cnt[static_cast<int64_t>(b) * n_rows];  // first item id of block b
+  for (int key = 0; key < kLenBins; ++key) {
+    const int c = v.lhist[b * kLenBins + key];
+    v.lhist[64 * kLenBins + b * kLenBins + key] = run;
+    run += c;
+  }
+}
+
+__global__ void k_items_permute(BlockedView v, int64_t n_rows, int B) {
+  const int64_t id = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  if (id >= v.hdr[4]) return;
+  int lo = 0, hi = B - 1;  // the block holding item id: last b with first id <= id
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (v.cnt[static_cast<int64_t>(mid) * n_rows] <= id) lo = mid; else hi = mid - 1;
+  }
+  const SegItem it = v.items[id];
+  const int nid = atomicAdd(&v.lhist[64 * kLenBins + lo * kLenBins + len_key(it.len)], 1);
+  v.items_tmp[nid] = it;
+  v.row_items[v.item_slot[id]] = nid;
 }
 
 // sum the chunk partials of split rows, in chunk order
@@ -2282,6 +2324,7 @@ int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (
 int g_seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
 int g_apply_node_vec = 1;  // k_apply_node4 (float4, 32-bit index math) for the common apply_node shapes
 int g_seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
+int g_plan_len_sort = 1;   // blocked plan: each block's items sorted by length (matched half-wave pairs)
 int g_att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
 int g_att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
 int g_mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
@@ -2315,6 +2358,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "seg_lean") { g_seg_lean = static_cast<int>(value); return 0; }
   if (k == "att_lean") { g_att_lean = static_cast<int>(value); return 0; }
   if (k == "att_direct") { g_att_direct = static_cast<int>(value); return 0; }
+  if (k == "plan_len_sort") { g_plan_len_sort = static_cast<int>(value); return 0; }
   if (k == "seg_lean_w1") { g_seg_lean_w1 = static_cast<int>(value); return 0; }
   if (k == "apply_node_vec") { g_apply_node_vec = static_cast<int>(value); return 0; }
   if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
@@ -2495,8 +2539,16 @@ int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indic
   GTA_LAUNCHED("k_blocked_cnt");
   scan_excl<int32_t>(v.cnt, n_rows * B, 0, &v.hdr[4], v.scan, s);  // -> first item id, n_items
   GTA_LAUNCHED("scan_excl");
+  GTA_HIP(hipMemsetAsync(v.lhist, 0, 64 * kLenBins * 4, s));
   k_blocked_items<<<gk, dim3(256), 0, s>>>(indptr, n_rows, B, item_edges, row_edges, v);
   GTA_LAUNCHED("k_blocked_items");
+  if (g_plan_len_sort) {
+    k_items_len_scan<<<1, 64, 0, s>>>(v, n_rows, B);
+    GTA_LAUNCHED("k_items_len_scan");
+    k_items_permute<<<dim3(static_cast<unsigned>((mi + 255) / 256)), dim3(256), 0, s>>>(v, n_rows, B);
+    GTA_LAUNCHED("k_items_permute");
+    GTA_HIP(hipMemcpyAsync(v.items, v.items_tmp, mi * sizeof(SegItem), hipMemcpyDeviceToDevice, s));
+  }
   return GTA_OK;
 }
 

@@ -691,3 +691,29 @@ def test_update_mm_vector_store_bitwise(dev, M, K, N, dt, gathered):
         ops.set_debug("mm_vstore", 1)
         ops.MM_ROWS_MIN_M = old_min
     assert torch.equal(outs[0], outs[1])
+
+
+@pytest.mark.parametrize("blocks,item_edges,heads", [(1, 256, 8), (7, 64, 8), (20, 256, 1), (16, 1 << 30, 0)])
+def test_blocked_plan_length_sort_bitwise(dev, blocks, item_edges, heads):
+    """Sorting each block's items by length (matched half-wave pairs) moves only item ids: the
+    metric aggregate and the fused attention aggregate are bitwise unchanged."""
+    n, e, F = 4000, 120000, 128
+    g0 = G.synthetic(n, e, seed=blocks + heads, device="cpu")
+    ip, ix = g0.numpy()
+    rng = np.random.default_rng(blocks)
+    x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
+    w = torch.from_numpy(rng.random((len(ix), heads)).astype(np.float32)).to(dev) if heads else None
+    a = torch.from_numpy(rng.standard_normal((n, 8)).astype(np.float32)).to(dev)
+    b = torch.from_numpy(rng.standard_normal((n, 8)).astype(np.float32)).to(dev)
+    outs = {}
+    try:
+        for srt in (0, 1):
+            ops.set_debug("plan_len_sort", srt)
+            g = G.from_numpy(ip, ix, device=dev)  # a fresh graph: plans are cached per graph
+            plan = g.blocked_plan(blocks, item_edges)
+            outs[srt] = (ops.aggregate_blocked(g, x, w, plan=plan, blocks=blocks),
+                         ops.gat_aggregate_blocked(g, x, a, b, want_sums=True, plan=plan))
+    finally:
+        ops.set_debug("plan_len_sort", 1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1][0], outs[1][1][0]) and torch.equal(outs[0][1][1], outs[1][1][1])
