@@ -2542,7 +2542,7 @@ int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indic
   GTA_HIP(hipMemsetAsync(v.lhist, 0, 64 * kLenBins * 4, s));
   k_blocked_items<<<gk, dim3(256), 0, s>>>(indptr, n_rows, B, item_edges, row_edges, v);
   GTA_LAUNCHED("k_blocked_items");
-  if (g_plan_len_sort) {
+  if (g_plan_len_sort && mi > 0) {
     k_items_len_scan<<<1, 64, 0, s>>>(v, n_rows, B);
     GTA_LAUNCHED("k_items_len_scan");
     k_items_permute<<<dim3(static_cast<unsigned>((mi + 255) / 256)), dim3(256), 0, s>>>(v, n_rows, B);
