@@ -16,6 +16,13 @@ the one exchange step of GCN / GraphSAGE / GIN layers: half the bytes of an
 all-reduce, and the next layer's scatter C reads the block the rank now owns.
 A scatter R (destination side, GAT's scores) needs every row: one all-gather
 of the [n_p, F] blocks.
+
+RowShard is the other layout (the metric aggregate's default, bench.py): rank p
+owns the destination rows [r_p, r_{p+1}) (nnz-balanced) with all their in-edges.
+A gather lands on the rank's own rows, a destination-side scatter reads them as
+they are, per-row sums (GAT's softmax) stay on one rank, so the executor keeps
+its fusions; the exchange is one all-gather of each source-side table, after
+the node-side GEMM that feeds it (x W, 128 columns, not x, 602).
 """
 import torch
 import torch.distributed as dist
@@ -24,8 +31,17 @@ from . import partition
 from .graph import Graph
 
 
+def row_cuts(graph, world):
+    """Destination-row cut points [world+1] balancing nnz (the indptr itself is the prefix sum)."""
+    ip = graph.indptr
+    targets = torch.arange(1, world, device=ip.device, dtype=torch.float64) * (graph.nnz / world)
+    inner = torch.searchsorted(ip[1:].to(torch.float64), targets) + 1
+    return [0] + [min(int(v), graph.n_rows) for v in inner.cpu()] + [graph.n_rows]
+
+
 class DistShard:
     """Rank `rank`'s part of `graph` (see module docstring)."""
+    local_rows = False  # gathers are partial sums over this rank's source columns
 
     def __init__(self, graph, rank, world, cuts=None, chunks=1):
         """chunks > 1: the padded rows are laid out chunk-major -- row j of chunk k of block q at
@@ -91,14 +107,90 @@ class DistShard:
         return out
 
 
+class RowShard:
+    """Rank `rank` owns destination rows [r0, r1) of `graph` (nnz-balanced cuts of the reference's
+    row-tile axis, code/preprocessing.py:26-38) and all their in-edges: its CSR is the contiguous
+    slice indptr[r0:r1+1], edges [e0, e1).  Node tensors are [n_p, F] row blocks, so the rank's
+    gathers are complete rows and its destination-side scatters read its own block.  Source
+    tables are all-gathered into the padded [world*m, F] layout (block q at rows [q*m, q*m + n_q),
+    m = max n_q), so the column ids are remapped once here: column c of block q -> q*m + c - r_q.
+
+    replicate_inputs: the layer's model inputs (node tensors handed in whole) are kept whole, in
+    the padded layout, so a scatter C of one needs no exchange -- the metric's replicated X
+    (bench.py); tables the layer computes are still all-gathered."""
+    local_rows = True
+    chunks = 1
+
+    def __init__(self, graph, rank, world, cuts=None, replicate_inputs=True):
+        self.cuts = row_cuts(graph, world) if cuts is None else [int(c) for c in cuts]
+        self.rank, self.world = rank, world
+        self.r0, self.r1 = self.cuts[rank], self.cuts[rank + 1]
+        self.c0, self.c1 = self.r0, self.r1  # its node rows (DistShard's naming)
+        self.n_local = self.r1 - self.r0
+        self.m = max(1, max(self.cuts[q + 1] - self.cuts[q] for q in range(world)))
+        self.n_global, self.e_global = graph.n_rows, graph.nnz
+        ip = graph.indptr
+        self.e0, self.e1 = int(ip[self.r0]), int(ip[self.r1])
+        col = graph.indices[self.e0:self.e1].long()
+        cuts_t = torch.tensor(self.cuts, device=col.device, dtype=torch.int64)
+        blk = torch.searchsorted(cuts_t, col, right=True) - 1
+        pcol = (blk * self.m + col - cuts_t[blk]).to(torch.int32)
+        self.graph = Graph((ip[self.r0:self.r1 + 1] - ip[self.r0]).contiguous(), pcol, n_cols=world * self.m)
+        self.replicate_inputs = replicate_inputs
+        self.inputs_full = {}
+        self._padded = {}
+
+    def padded(self, t):
+        """Global node tensor [N, *] -> the padded table layout [world*m, *] (cached per tensor)."""
+        key = (t.data_ptr(), tuple(t.shape), t._version)
+        hit = self._padded.get(key)
+        if hit is None:
+            full = t.new_zeros(self.world * self.m, *t.shape[1:])
+            for q in range(self.world):
+                a, b = self.cuts[q], self.cuts[q + 1]
+                full[q * self.m: q * self.m + b - a] = t[a:b]
+            hit = self._padded[key] = (t, full)  # holds t: its storage (and key) stay valid
+        return hit[1]
+
+    @property
+    def edge_ids(self):
+        return torch.arange(self.e0, self.e1, device=self.graph.device)
+
+    def local_tensors(self, tensors):
+        """Global layer tensors -> this rank's: node tensors [N, *] -> rows [r0, r1), edge tensors
+        [E, *] -> edges [e0, e1), weights / broadcast rows unchanged."""
+        out = {}
+        self.inputs_full = {}  # this layer's whole inputs only (a later layer's x is a row block)
+        for k, t in tensors.items():
+            rows = t.shape[0] if t.dim() else 0
+            if k.startswith("w:"):
+                out[k] = t
+            elif k == "x_edge" or (rows == self.e_global and rows != self.n_global):
+                out[k] = t[self.e0:self.e1].contiguous()
+            elif rows == self.n_global:
+                out[k] = t[self.r0:self.r1].contiguous()
+                self.inputs_full[k] = t
+            else:
+                out[k] = t
+        return out
+
+
 class Comm:
-    """The executor's exchange hooks over torch.distributed (RCCL "nccl" or gloo)."""
+    """The executor's exchange hooks over torch.distributed (RCCL "nccl" or gloo).
+
+    DistShard (source-column shards): gathers reduce-scatter (reduce_rows), dst-side scatters
+    all-gather (gather_rows), source tables are local.  RowShard (destination-row shards):
+    gathers and dst-side scatters are local, source tables all-gather (src_fill)."""
 
     def __init__(self, shard, group=None):
         self.s, self.group = shard, group
         self.on = dist.is_available() and dist.is_initialized() and shard.world > 1
         self.nccl = self.on and dist.get_backend(group) == "nccl"
+        self.local_rows = shard.local_rows
+        self.src_fill = self.src_rows if self.local_rows else None
+        self.replicated_bytes = 0
         self.bytes = 0
+        self._filled = {}
 
     @property
     def n_local(self):
@@ -107,6 +199,8 @@ class Comm:
     def reduce_rows(self, y):
         """Partial aggregate over padded rows [world*m, F] -> this rank's summed block [n_p, F]."""
         s = self.s
+        if self.local_rows:  # the rank's CSR holds whole rows
+            return y
         assert s.chunks == 1, "layer execution uses the one-chunk layout"
         if not self.on:
             return y[s.rank * s.m: s.rank * s.m + s.n_local]
@@ -119,7 +213,34 @@ class Comm:
         return y[s.rank * s.m: s.rank * s.m + s.n_local]
 
     def gather_rows(self, x):
-        """This rank's block [n_p, F] -> every block, padded: [world*m, F] (dst-side scatters)."""
+        """Dst-side scatter table: column shards all-gather the blocks; row shards own the rows."""
+        return x if self.local_rows else self._all_blocks(x)
+
+    def src_rows(self, x):
+        """Source-side table of a row shard: every rank's block, padded [world*m, F] (one all-gather
+        per distinct tensor; the padded column ids of RowShard index it)."""
+        key = (x.data_ptr(), tuple(x.shape), tuple(x.stride()), x._version)
+        hit = self._filled.get(key)  # holds x, so its storage (and key) cannot be reused meanwhile
+        if hit is None:
+            hit = self._filled[key] = (x, self._all_blocks(x))
+        return hit[1]
+
+    def replicated(self, key):
+        """A getter of the whole padded table of model input `key` when the row shard keeps inputs
+        replicated (None: all-gather it like any other table)."""
+        s = self.s
+        if not (self.local_rows and s.replicate_inputs) or key not in s.inputs_full:
+            return None
+        t = s.inputs_full[key]
+
+        def get():
+            full = s.padded(t)
+            self.replicated_bytes = max(self.replicated_bytes, full.numel() * full.element_size())
+            return full
+        return get
+
+    def _all_blocks(self, x):
+        """This rank's block [n_p, F] -> every block, padded: [world*m, F]."""
         s = self.s
         buf = torch.zeros(s.m, x.shape[1], dtype=x.dtype, device=x.device)
         buf[:s.n_local] = x
@@ -139,7 +260,7 @@ class Comm:
     def full_rows(self, x):
         """[n_p, F] blocks of every rank -> the unpadded global [N, F] (for results/tests)."""
         s = self.s
-        full = self.gather_rows(x)
+        full = self._all_blocks(x)
         return torch.cat([full[q * s.m: q * s.m + s.cuts[q + 1] - s.cuts[q]] for q in range(s.world)])
 
 

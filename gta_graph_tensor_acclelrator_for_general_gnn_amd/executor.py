@@ -43,11 +43,25 @@ class EdgeT:
 
 
 class Scat:
-    """A scatter kept virtual: edge e reads row idx(e) of node tensor t (mode 'src' or 'dst')."""
-    __slots__ = ("t", "mode")
+    """A scatter kept virtual: edge e reads row idx(e) of node tensor t (mode 'src' or 'dst').
 
-    def __init__(self, t, mode):
-        self.t, self.mode = t, mode
+    On a destination-row shard (distributed.RowShard) a source-side table is first this rank's
+    row block `local`; `fill` exchanges it into the full table (one all-gather) the first time a
+    kernel indexes it through `t`.  Node-side GEMMs of the scatter run on `local` and keep `fill`,
+    so the exchange carries the GEMM's output, not its input.  `own` (a replicated model input)
+    returns this scatter's whole table without an exchange; derived scatters do not inherit it."""
+    __slots__ = ("local", "mode", "fill", "own", "_full")
+
+    def __init__(self, t, mode, fill=None, own=None):
+        self.local, self.mode, self.fill, self.own, self._full = t, mode, fill, own, None
+
+    @property
+    def t(self):
+        if self.fill is None and self.own is None:
+            return self.local
+        if self._full is None:
+            self._full = self.own() if self.own is not None else self.fill(self.local)
+        return self._full
 
 
 class Deferred:
@@ -130,7 +144,8 @@ class Executor:
                     self.consumers[src.op].append(i)
         #   fuse_softmax: GAT's score -> SF -> per-row sum (-> divide) chain runs as one
         #   gta_edge_softmax launch (results equal to fp32 rounding, not bitwise)
-        self.fuse_softmax = dist is None or not dist.on  # per-row sums span ranks: unfused ops + exchanges
+        # column shards: per-row sums span ranks (unfused ops + exchanges); row shards own whole rows
+        self.fuse_softmax = dist is None or dist.local_rows or dist.s.world == 1
         self.softmax = self._match_softmax()
         #   fuse_attention: the softmax chain's alpha (or v) * scatter_C(x) -> gather runs as one
         #   column-blocked gta_gat_aggregate_blocked (no [E, heads] tensor); attention_blocks
@@ -159,7 +174,7 @@ class Executor:
         #   agg + (1+eps) x), runs as the aggregate accumulating into T's fresh output buffer:
         #   T + sum == sum + T bitwise, and the ADD pass over [N, F] disappears.  G and T stay
         #   available (recomputed on demand).
-        self.gather_acc = dist is None or not dist.on
+        self.gather_acc = dist is None or dist.local_rows or dist.s.world == 1
         self.gacc = self._match_gather_acc()
 
     # ---------------------------------------------------------------- inputs
@@ -368,12 +383,12 @@ class Executor:
     def _node_mm(self, op, v, post_sf=None):
         """applyedge MM of a virtual scatter: the GEMM runs over the node rows, the result stays virtual."""
         W = self.tensors[f"w:{op.idx}"]
-        x, W = self._mm_dtypes(v.t, W)
+        x, W = self._mm_dtypes(v.local, W)
         if W.shape[0] != x.shape[1]:
             raise ValueError(f"op {op.idx}: weight rows {W.shape[0]} != feature width {x.shape[1]}")
         xw = ops.update_mm(x, W, sf=post_sf)
         self._count(x.shape[0] * (x.shape[1] * x.element_size() + W.shape[1] * 4) + W.numel() * W.element_size())
-        return Scat(xw, v.mode)
+        return Scat(xw, v.mode, v.fill)
 
     def _pushdown_mm(self, op, add_idx, post_sf=None):
         """MM(scatter a + scatter b) as (a W)[r_a(e)] + (b W)[r_b(e)]."""
@@ -464,7 +479,7 @@ class Executor:
             ws = [z for z in pins if not (isinstance(z, Scat) and z.mode == "src")]
             if len(xs) != 1 or len(ws) > 1:
                 return None
-            x, w = xs[0].t, None
+            x, w, fill = xs[0].local, None, xs[0].fill
             if ws:
                 if isinstance(ws[0], tuple) or ws[0] is None:
                     return None
@@ -472,13 +487,15 @@ class Executor:
                 if w.shape[1] != 1:
                     return None
         elif isinstance(v, Scat) and v.mode == "src":
-            x, w = v.t, None
+            x, w, fill = v.local, None, v.fill
         else:
             return None
         W = self.tensors[f"w:{M.idx}"]
         if W.shape[0] != x.shape[1]:
             return None
         xw = self._node_gemm(x, M.idx, W).contiguous()
+        if fill is not None:  # row shards: exchange x W (narrower than x)
+            xw = fill(xw)
         n, E, F = self.graph.n_rows, self.graph.nnz, xw.shape[1]
         y = self._spmm(xw, "src", w)
         self._count(E * (4 + (4 if w is not None else 0) + 4 * F) + n * (8 + 4 * F))
@@ -783,10 +800,16 @@ class Executor:
                 v = NodeT(self._node(v))
             if not isinstance(v, NodeT):
                 raise TypeError(f"scatter op {op.idx} needs a node tensor")
-            t = v.t
-            if op.order != "C" and self.dist is not None:
-                t = self.dist.gather_rows(t)
-            s = Scat(t, "src" if op.order == "C" else "dst")
+            t, fill, own = v.t, None, None
+            if self.dist is not None:  # row shards fill source tables lazily; column shards gather dst rows
+                if op.order == "C":
+                    fill = self.dist.src_fill
+                    if src.kind != "op":  # a model input the rank may hold whole
+                        key = f"ext:{op.idx}:0"
+                        own = self.dist.replicated(key if key in self.tensors else "x")
+                else:
+                    t = self.dist.gather_rows(t)
+            s = Scat(t, "src" if op.order == "C" else "dst", fill, own)
             # a STORE_E'd scatter is only materialised when nothing reads it back (a sink):
             # every consumer kernel gathers by index, which is the same bytes
             if op.idx in block.stored and not (self.elide_scatter_stores and self.consumers[op.idx]):

@@ -1,11 +1,12 @@
-"""Full BASELINE-config layers on N GPUs (one process per GPU, node-range shards, distributed.py).
+"""Full BASELINE-config layers on N GPUs (one process per GPU, distributed.py).
 
   python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
-      --master-port P scripts/dist_layers.py [config ...] [--reps R]
+      --master-port P scripts/dist_layers.py [config ...] [--reps R] [--layout rows|cols]
 
 Each rank builds the same compiled layer (front end -> search -> stream, on the
-global graph), keeps its shard, and executes the stream with reduce-scatter /
-all-gather exchanges.  Rank 0 prints one JSON line per config: ms per forward
+global graph), keeps its shard, and executes the stream.  --layout rows (default):
+destination-row shards, one all-gather per source table; cols: source-column
+shards, reduce-scatter per gather and all-gather per dst-side scatter.  Rank 0 prints one JSON line per config: ms per forward
 (max over ranks), edges/s, exchanged bytes, and the max normalised difference
 of the re-assembled output vs a 1-device execution of the same stream.
 GTA_DIST_BACKEND=gloo GTA_SINGLE_DEVICE=1 rehearses several ranks on one GPU.
@@ -30,6 +31,18 @@ def main():
         i = args.index("--reps")
         reps = int(args[i + 1])
         del args[i:i + 2]
+    layout = "rows"
+    if "--layout" in args:
+        i = args.index("--layout")
+        layout = args[i + 1]
+        del args[i:i + 2]
+    probe = 0  # --probe W: one process times rank 0's shard of a W-way cut (compute only, no exchange)
+    if "--probe" in args:
+        i = args.index("--probe")
+        probe = int(args[i + 1])
+        del args[i:i + 2]
+    replicate = "--no-replicate" not in args  # rows: keep model inputs whole (no exchange of x)
+    args = [a for a in args if a != "--no-replicate"]
     names = args or ["sage-reddit", "gin-products"]
     rank, world = int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1))
     local = int(os.environ.get("LOCAL_RANK", 0))
@@ -41,8 +54,11 @@ def main():
     out = {}
     for name in names:
         layers, g, tensors = configs.build(name, dev)
-        shard = distributed.DistShard(g, rank, world)
-        times, comm_bytes = [], 0
+        if layout == "rows":
+            shard = distributed.RowShard(g, rank, probe or world, replicate_inputs=replicate)
+        else:
+            shard = distributed.DistShard(g, rank, probe or world)
+        times, comm_bytes, rep_bytes = [], 0, 0
         for r in range(reps + 1):
             if world > 1:
                 dist.barrier()
@@ -57,6 +73,7 @@ def main():
                 x = res.outputs[sorted(res.outputs)[-1]]
                 if r == 0:
                     comm_bytes += ex.dist.bytes
+                    rep_bytes += ex.dist.replicated_bytes
             torch.cuda.synchronize(dev)
             dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev if backend == "nccl"
                               else "cpu")
@@ -66,7 +83,7 @@ def main():
                 times.append(float(dt))
         full = ex.dist.full_rows(x) if world > 1 else x
         err = None
-        if rank == 0:  # the same stream on one device, same inputs
+        if rank == 0 and not probe:  # the same stream on one device, same inputs
             y = None
             for lay, t in zip(layers, tensors):
                 t = dict(t)
@@ -79,7 +96,7 @@ def main():
         ms = 1e3 * sorted(times)[len(times) // 2]
         rec = {"config": name, "n_gpus": world, "N": g.n_rows, "E": g.nnz, "shard_edges": shard.graph.nnz,
                "ms_per_forward": ms, "edges_per_s": g.nnz * len(layers) / (ms / 1e3),
-               "exchanged_bytes_per_rank": comm_bytes, "backend": backend if world > 1 else None,
+               "exchanged_bytes_per_rank": comm_bytes, "replicated_input_bytes": rep_bytes, "layout": layout, "probe_world": probe or None, "backend": backend if world > 1 else None,
                "max_norm_diff_vs_1dev": err}
         out[name] = rec
         if rank == 0:
@@ -88,7 +105,7 @@ def main():
         torch.cuda.empty_cache()
     if rank == 0:
         os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-        with open(os.path.join(ROOT, "gpurun_out", f"dist_layers_{world}.json"), "w") as f:
+        with open(os.path.join(ROOT, "gpurun_out", f"dist_layers_{layout}_{world}{f'_probe{probe}' if probe else ''}.json"), "w") as f:
             json.dump(out, f, indent=1)
     if world > 1:
         dist.barrier()

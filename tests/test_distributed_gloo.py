@@ -28,7 +28,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, golden_dir, q):
+def _worker(rank, world, port, golden_dir, q, layout="cols"):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -52,7 +52,10 @@ def _worker(rank, world, port, golden_dir, q):
             og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
             st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
             tensors = workloads.make_tensors(og, g, net, seed=3)
-            shard = distributed.DistShard(g, rank, world)
+            if layout == "cols":
+                shard = distributed.DistShard(g, rank, world)
+            else:  # "rows": model inputs replicated; "rows-allgather": every source table exchanged
+                shard = distributed.RowShard(g, rank, world, replicate_inputs=layout == "rows")
             res, ex = distributed.run_stream(og, st, shard, tensors, sem)
             full = {k: ex.dist.full_rows(v) for k, v in res.outputs.items()}
             nnz = torch.tensor([shard.graph.nnz])
@@ -61,7 +64,7 @@ def _worker(rank, world, port, golden_dir, q):
                 ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
                 compare(full, ref, full.keys(), rtol=1e-4)
                 assert int(nnz) == g.nnz
-                report.append((rec["file"], ex.dist.bytes))
+                report.append((rec["file"], ex.dist.bytes + ex.dist.replicated_bytes))
         if rank == 0:
             q.put(("ok", report))
     except Exception as e:  # report to the parent instead of hanging the other rank
@@ -71,12 +74,14 @@ def _worker(rank, world, port, golden_dir, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_layer_streams_distributed_gloo(golden_dir, world):
+@pytest.mark.parametrize("world,layout", [(2, "cols"), (3, "cols"), (2, "rows"), (3, "rows"), (2, "rows-allgather")])
+def test_layer_streams_distributed_gloo(golden_dir, world, layout):
+    """layout "cols": source-column shards (reduce-scatter per gather); "rows": destination-row
+    shards (all-gather per source table, fusions on)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, golden_dir, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, golden_dir, q, layout)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
@@ -85,6 +90,32 @@ def test_layer_streams_distributed_gloo(golden_dir, world):
     assert status == "ok", info
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     assert len(info) == len(STREAMS) and all(b > 0 for _, b in info)
+
+
+def test_row_shard_layout_single_process():
+    """Row shards: contiguous CSR slices with padded column ids; the padded table gathers back to x."""
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, graph as G
+    g = G.synthetic(1000, 20000, seed=2)
+    world = 3
+    ip, ix = g.numpy()
+    x = torch.randn(g.n_rows, 5)
+    shards = [distributed.RowShard(g, r, world) for r in range(world)]
+    m = shards[0].m
+    full = torch.zeros(world * m, 5)
+    for s in shards:
+        full[s.rank * m: s.rank * m + s.n_local] = x[s.r0:s.r1]
+    assert [s.r0 for s in shards] + [shards[-1].r1] == shards[0].cuts and shards[-1].r1 == g.n_rows
+    for s in shards:
+        sip, six = s.graph.numpy()
+        assert s.graph.n_rows == s.n_local and s.graph.n_cols == world * m
+        np.testing.assert_array_equal(sip, ip[s.r0:s.r1 + 1] - ip[s.r0])
+        # every padded column id reads the global source row
+        torch.testing.assert_close(full[torch.as_tensor(six).long()], x[torch.as_tensor(ix[s.e0:s.e1]).long()])
+        same_row = np.diff(np.repeat(np.arange(s.n_local), np.diff(sip))) == 0
+        assert np.all(np.diff(six.astype(np.int64))[same_row] >= 0)  # the remap keeps rows sorted
+    assert sum(s.e1 - s.e0 for s in shards) == g.nnz
+    # nnz balance: no shard holds more than its share plus one row
+    assert max(s.e1 - s.e0 for s in shards) <= g.nnz / world + int(np.diff(ip).max())
 
 
 def test_shard_layout_single_process():
