@@ -363,7 +363,8 @@ def main():
                 "alpha=per-head softmax over in-edges",
         "config": {"workload": "GAT layer-1 aggregate block [3,11,12] (scatter C -> applyedge MUL -> gather ADD)",
                    "graph": "reddit-shaped", "N": args.n, "E": nnz_total, "F": F, "heads": HEADS,
-                   "parallelism": (f"destination-row tiles x{pr} (X replicated, no data-path collective)"
+                   "parallelism": ("one GPU, whole graph" if world == 1 else
+                                   f"destination-row tiles x{pr} (X replicated, no data-path collective)"
                                    if grid and pc == 1 else
                                    f"2-D edge tiles {pr}x{pc} (row groups x source-column groups), RCCL reduce-scatter "
                                    f"of the partial aggregates inside each row group" if grid else
@@ -378,6 +379,9 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": PEAK_HBM_GBS, "unit": "GB/s",
                      "frac": achieved / PEAK_HBM_GBS, "traffic": traffic,
                      "kernel_ms": kern_ms, "alg_bytes_per_launch": ab,
+                     # PMC bytes (L2 <-> fabric, incl. Infinity-Cache hits) per launch over the same time
+                     "traffic_GBps": traffic and traffic / (kern_ms / 1e3) / 1e9,
+                     "traffic_frac": traffic and traffic / (kern_ms / 1e3) / 1e9 / PEAK_HBM_GBS,
                      "kernels": ("k_agg_h32 + k_seg_reduce" if impl == "blocked" else "k_aggregate + combine")},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
