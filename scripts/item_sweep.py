@@ -56,7 +56,7 @@ def main():
         g = G.Graph(g.indptr, cols[order].to(torch.int32).contiguous())
         alpha = alpha[order].contiguous()
     print(f"inputs {time.time() - t0:.1f} s", flush=True)
-    defaults = {"seg_lean": 1, "seg_lanes": 32, "seg_u": 8, "seg_nt": 2, "seg_quarter": 1, "seg_lean_w1": 1}
+    defaults = {"seg_lean": 1, "seg_lanes": 32, "seg_u": 8, "seg_nt": 2, "seg_quarter": 1, "seg_lean_w1": 1, "slab_rows": 0}
     out = {}
     for grid in args.grids.split(","):
         pr, pc = map(int, grid.lower().split("x"))
@@ -104,6 +104,7 @@ def main():
                         ref[key] = y.clone()
                     else:
                         d = (y - ref[key]).abs().max().item()
+                        print(f"  {name}: max |y - first variant| = {d}", flush=True)
                         assert d < 1e-3, f"variant {name} differs from the first by {d}"
                 for k_ in kv:
                     ops.set_debug(k_, defaults[k_])
