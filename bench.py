@@ -113,8 +113,8 @@ def cpu_baseline(g, x, alpha, target_s=12.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--chunk", type=int, default=512, help="aggregate plan row-chunk (edges)")
     ap.add_argument("--row-chunks", type=int, default=0, help="row chunks for comm overlap (0 = auto)")
     ap.add_argument("--lpe", type=int, default=0, help="force lanes-per-edge variant (32 or 64)")
