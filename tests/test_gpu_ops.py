@@ -627,10 +627,12 @@ def test_update_mm_prefetch_forms(dev, pf, M, K, N, dt):
     elif dt == "mixed":
         w = w.to(torch.bfloat16)
     ops.set_debug("mm_prefetch", pf)
+    ops.set_debug("mm_blaslt", 0)  # the hand-written row kernel, not the library path
     try:
         out = ops.update_mm(x.to(dev), w.to(dev))
     finally:
         ops.set_debug("mm_prefetch", 1)
+        ops.set_debug("mm_blaslt", 1)
     xr = x.float().numpy().astype(np.float64)
     if dt != "f32":
         xr = torch.from_numpy(xr).to(torch.bfloat16).double().numpy()
@@ -663,6 +665,28 @@ def test_update_mm_split_k(dev, M, K, N, dt, gathered):
     xs = xr[idx.numpy()] if gathered else xr[:M]
     ref = isa_ref.mm(xs, wf, sf_kind="RELU")
     _check(out, ref, np.abs(xs).astype(np.float64) @ np.abs(wf).astype(np.float64), f"split-K {dt}")
+
+
+@pytest.mark.parametrize("M,K,N,ldx_pad", [(40000, 602, 128, 0), (40000, 602, 256, 3), (33000, 37, 200, 1),
+                                           (89250, 500, 128, 0)])
+def test_update_mm_plain_f32_library_path(dev, M, K, N, ldx_pad):
+    """Plain fp32 UPDATE with M >= 32768 runs on hipBLASLt inside libgta (gta_update_mm_t): fp64 bound,
+    strided x, and within the fp32 bound of the hand-written k_mm_rows on the same operands."""
+    rng = np.random.default_rng(M + K + N)
+    x = torch.from_numpy(rng.standard_normal((M, K + ldx_pad)).astype(np.float32))[:, :K]
+    w = torch.from_numpy((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32))
+    xd, wd = x.to(dev), w.to(dev)
+    out = ops.update_mm(xd, wd)
+    ops.set_debug("mm_blaslt", 0)
+    try:
+        own = ops.update_mm(xd, wd)
+    finally:
+        ops.set_debug("mm_blaslt", 1)
+    xr, wf = x.numpy().astype(np.float64), w.numpy().astype(np.float64)
+    scale = np.abs(xr) @ np.abs(wf)
+    _check(out, xr @ wf, scale, "update_mm hipBLASLt")
+    _check(own, xr @ wf, scale, "update_mm k_mm_rows")
+    assert torch.equal(out, ops.update_mm(xd, wd))  # deterministic
 
 
 @pytest.mark.parametrize("M,K,N,dt,gathered", [(5000, 602, 128, "f32", False), (4099, 100, 130, "mixed", True),
