@@ -2333,7 +2333,8 @@ int g_plan_len_sort = 1;   // blocked plan: each block's items sorted by length 
 int g_att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
 int g_att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
 int g_mm_blaslt = 1;        // plain fp32 UPDATE with M >= g_mm_blaslt_min_m on hipBLASLt (gta_update_mm_t)
-int64_t g_mm_blaslt_min_m = 32768;
+int64_t g_mm_blaslt_min_m = 1024;
+int g_mm_blaslt_tune = 1;  // time the heuristic's top candidates at a shape's first use
 int g_mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
 int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
 int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
@@ -2372,6 +2373,7 @@ int gta_debug_set(const char* key, int64_t value) {
   if (k == "mm_prefetch") { g_mm_prefetch = static_cast<int>(value); return 0; }
   if (k == "mm_blaslt") { g_mm_blaslt = static_cast<int>(value); return 0; }
   if (k == "mm_blaslt_min_m") { g_mm_blaslt_min_m = value; return 0; }
+  if (k == "mm_blaslt_tune") { g_mm_blaslt_tune = static_cast<int>(value); return 0; }
   if (k == "mm_vstore") { g_mm_vstore = static_cast<int>(value); return 0; }
   if (k == "mm_blocks_per_cu") { g_mm_blocks_per_cu = value; return 0; }
   if (k == "apply_edge_form") { g_apply_edge_form = static_cast<int>(value); return 0; }
@@ -2968,7 +2970,8 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
   return GTA_OK;
 }
 
-// Plain fp32 UPDATE (no row gather, no SF epilogue, M >= g_mm_blaslt_min_m) on hipBLASLt, the
+// Plain fp32 UPDATE (no row gather, no SF epilogue, M >= g_mm_blaslt_min_m; the row-streaming and
+// split-K entry points) on hipBLASLt, the
 // vendor's tuned fp32 MFMA GEMM: measured faster than k_mm_rows on the layer shapes (Reddit
 // x.W 602 -> 128: 0.37 vs 0.58 ms; Flickr 500 -> 128: 0.12 vs 0.145 ms;
 // profiles/r01_mm_vs_library.json) -- k_mm_rows keeps the gather-GEMM, the SF epilogues, bf16 and
@@ -2984,6 +2987,7 @@ struct BlasLtShape {
   bool ok = false;
 };
 constexpr uint64_t kBlasLtWorkspace = 32ull << 20;
+constexpr int kBlasLtCandidates = 8;
 
 bool blaslt_f32(const float* x, int64_t ldx, int64_t M, int64_t K, const float* wt, int64_t ldwt, int64_t N,
                 float* out, int64_t ldo, hipStream_t s) {
@@ -3020,16 +3024,49 @@ bool blaslt_f32(const float* x, int64_t ldx, int64_t M, int64_t K, const float* 
     if (ok) {
       hipblasLtMatmulPreference_t pref = nullptr;
       uint64_t wsb = kBlasLtWorkspace;
-      hipblasLtMatmulHeuristicResult_t res{};
+      hipblasLtMatmulHeuristicResult_t res[kBlasLtCandidates];
       int nres = 0;
       ok = hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS &&
            hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
                                                  sizeof(wsb)) == HIPBLAS_STATUS_SUCCESS &&
-           hipblasLtMatmulAlgoGetHeuristic(h->second.first, sh.md, sh.la, sh.lb, sh.lc, sh.lc, pref, 1, &res,
-                                           &nres) == HIPBLAS_STATUS_SUCCESS &&
-           nres > 0 && res.state == HIPBLAS_STATUS_SUCCESS;
+           hipblasLtMatmulAlgoGetHeuristic(h->second.first, sh.md, sh.la, sh.lb, sh.lc, sh.lc, pref,
+                                           g_mm_blaslt_tune ? kBlasLtCandidates : 1, res, &nres) ==
+               HIPBLAS_STATUS_SUCCESS &&
+           nres > 0 && res[0].state == HIPBLAS_STATUS_SUCCESS;
       if (pref) hipblasLtMatmulPreferenceDestroy(pref);
-      if (ok) sh.algo = res.algo;
+      if (ok) {
+        sh.algo = res[0].algo;
+        // first use of the shape: time the heuristic's candidates on the real operands and keep the
+        // fastest (not while a HIP graph is being captured: the heuristic's first choice then)
+        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+        if (nres > 1 && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+          hipEvent_t e0, e1;
+          if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
+            const float alpha = 1.f, beta = 0.f;
+            float best = 1e30f;
+            for (int i = 0; i < nres; ++i) {
+              if (res[i].state != HIPBLAS_STATUS_SUCCESS) continue;
+              bool run_ok = true;
+              for (int rep = 0; rep < 3 && run_ok; ++rep) {  // rep 0 warms up
+                if (rep == 1) (void)hipEventRecord(e0, s);
+                run_ok = hipblasLtMatmul(h->second.first, sh.md, &alpha, wt, sh.la, x, sh.lb, &beta, out, sh.lc,
+                                         out, sh.lc, &res[i].algo, h->second.second, kBlasLtWorkspace, s) ==
+                         HIPBLAS_STATUS_SUCCESS;
+              }
+              if (!run_ok) continue;
+              (void)hipEventRecord(e1, s);
+              float ms = 0.f;
+              if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess &&
+                  ms < best) {
+                best = ms;
+                sh.algo = res[i].algo;
+              }
+            }
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+          }
+        }
+      }
     }
     sh.ok = ok;
     it = shapes.emplace(key, sh).first;
@@ -3109,6 +3146,11 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
     return fail(GTA_ERR_ARG, "update_mm_t_split: workspace too small");
   if (nsl > 65535) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t_split: too many slices");
   float* ws = static_cast<float*>(workspace);
+  if (g_mm_blaslt && dtype == GTA_F32 && !row_idx && sf == GTA_SF_NONE && M >= g_mm_blaslt_min_m &&
+      blaslt_f32(static_cast<const float*>(x), ldx, M, K, static_cast<const float*>(wt), ldwt, N, out, ldo, S(stream))) {
+    GTA_LAUNCHED("hipblaslt_matmul");
+    return GTA_OK;
+  }
   const int nt = N <= 16 ? 1 : N <= 32 ? 2 : N <= 64 ? 4 : 8;
   const int64_t groups = (M + 127) / 128;
   const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);

@@ -440,10 +440,12 @@ def test_update_mm_both_forms(dev, form, M, K, N, dt):
         w = w.to(torch.bfloat16)
     old = ops.MM_FORM, ops.MM_ROWS_MIN_M
     ops.MM_FORM, ops.MM_ROWS_MIN_M = form, 0
+    ops.set_debug("mm_blaslt", 0)  # the hand-written kernels, not the library path
     try:
         out = ops.update_mm(xs.to(dev), w.to(dev))
     finally:
         ops.MM_FORM, ops.MM_ROWS_MIN_M = old
+        ops.set_debug("mm_blaslt", 1)
     xr = xs.float().numpy().astype(np.float64)
     if dt != "f32":
         xr = torch.from_numpy(xr).to(torch.bfloat16).double().numpy()
@@ -668,7 +670,7 @@ def test_update_mm_split_k(dev, M, K, N, dt, gathered):
 
 
 @pytest.mark.parametrize("M,K,N,ldx_pad", [(40000, 602, 128, 0), (40000, 602, 256, 3), (33000, 37, 200, 1),
-                                           (89250, 500, 128, 0)])
+                                           (89250, 500, 128, 0), (2708, 1433, 128, 0), (3000, 602, 128, 2)])
 def test_update_mm_plain_f32_library_path(dev, M, K, N, ldx_pad):
     """Plain fp32 UPDATE with M >= 32768 runs on hipBLASLt inside libgta (gta_update_mm_t): fp64 bound,
     strided x, and within the fp32 bound of the hand-written k_mm_rows on the same operands."""
