@@ -3038,8 +3038,17 @@ bool blaslt_f32(const float* x, int64_t ldx, int64_t M, int64_t K, const float* 
         sh.algo = res[0].algo;
         // first use of the shape: time the heuristic's candidates on the real operands and keep the
         // fastest (not while a HIP graph is being captured: the heuristic's first choice then)
+        // (nor when out overlaps an operand: the trial runs write out)
+        const auto span = [](const float* p, int64_t rows, int64_t ld, int64_t cols) {
+          return std::make_pair(reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(p + (rows - 1) * ld + cols));
+        };
+        const auto overlap = [](std::pair<uintptr_t, uintptr_t> a, std::pair<uintptr_t, uintptr_t> b) {
+          return a.first < b.second && b.first < a.second;
+        };
+        const auto so = span(out, M, ldo, N);
+        const bool disjoint = !overlap(so, span(x, M, ldx, K)) && !overlap(so, span(wt, N, ldwt, K));
         hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        if (nres > 1 && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+        if (nres > 1 && disjoint && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
           hipEvent_t e0, e1;
           if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
             const float alpha = 1.f, beta = 0.f;
