@@ -192,9 +192,9 @@ class Executor:
         if src.kind == "ext":
             if t is None:
                 raise KeyError(f"op {op.idx} slot {slot}: external input 'ext:{op.idx}:{slot}' not given")
-            return self._wrap_ext(t)
+            return self._wrap_ext(t, op)
         if t is not None:  # explicit override of the model input for this slot
-            return self._wrap_ext(t)
+            return self._wrap_ext(t, op)
         if op.type == "applyedge":
             t = self.tensors.get("x_edge")
             if t is None:
@@ -202,9 +202,12 @@ class Executor:
             return EdgeT(t)
         return NodeT(self.tensors["x"])
 
-    def _wrap_ext(self, t):
+    def _wrap_ext(self, t, op=None):
         if t.dim() == 1:
             t = t.view(-1, 1)
+        if op is not None and op.type in ("scatter", "applynode") and t.shape[0] == self.n_nodes \
+                and t.shape[0] != 1:  # N == E (e.g. an empty row shard): these ops read node rows
+            return NodeT(t)
         if t.shape[0] == self.graph.nnz and t.shape[0] != self.n_nodes:
             return EdgeT(t)
         if t.shape[0] == 1:

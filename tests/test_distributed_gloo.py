@@ -118,6 +118,33 @@ def test_row_shard_layout_single_process():
     assert max(s.e1 - s.e0 for s in shards) <= g.nnz / world + int(np.diff(ip).max())
 
 
+def test_row_shards_with_empty_ranks(golden_dir):
+    """More ranks than rows: the empty row shards run every network's stream (no process group;
+    tests/fake_ops kernels) and return [0, F] blocks."""
+    import json
+
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, executor, graph as G, ir, workloads
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd.semantics import Semantics
+    from tests import fake_ops
+    old_ops, executor.ops = executor.ops, fake_ops
+    try:
+        man = json.load(open(os.path.join(golden_dir, "manifest.json")))
+        g = G.from_numpy(np.array([0, 2, 2, 5]), np.array([1, 2, 0, 1, 2], dtype=np.int32))
+        for net, reorder in STREAMS:
+            rec = [s for s in man["streams"] if "file" in s and s["dataset"] == "cora" and s["network"] == net
+                   and s["reorder"] == reorder][0]
+            sem = Semantics.for_network(net, reorder)
+            og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+            st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+            tensors = workloads.make_tensors(og, g, net, seed=3)
+            for r in range(5):
+                shard = distributed.RowShard(g, r, 5)
+                res, _ = distributed.run_stream(og, st, shard, tensors, sem)
+                assert all(v.shape[0] == shard.n_local for v in res.outputs.values()), (net, reorder, r)
+    finally:
+        executor.ops = old_ops
+
+
 def test_shard_layout_single_process():
     """Padded destination rows, local column ids, and the edge set partition (no process group)."""
     from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, graph as G
