@@ -219,7 +219,9 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
  * is staged into LDS with 16-B copies.  The contraction order differs from
  * gta_update_mm (fp32 rounding only).  A plain fp32 product (GTA_F32, row_idx NULL,
  * GTA_SF_NONE, M >= 1024) runs on hipBLASLt instead (the algorithm timed fastest at the
- * shape's first use; deterministic per shape); this also applies to gta_update_mm_t_split. */
+ * shape's first use in the process: repeat calls are bitwise equal, separate processes may
+ * pick another algorithm and differ by fp32 rounding); this also applies to
+ * gta_update_mm_t_split. */
 int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                     int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream);
 
