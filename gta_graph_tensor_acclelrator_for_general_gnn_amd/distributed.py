@@ -284,16 +284,33 @@ def run_stream(opgraph, stream, shard, tensors, semantics=None, group=None, plan
     return res, ex
 
 
-def grid_shape(world):
-    """Default rank grid (row groups pr x column groups pc) for the aggregate benchmark: pr = world,
-    pc = 1, i.e. destination-row tiles of the reference's row-tile blocking
-    (code/preprocessing.py:26-38) with X replicated.  Measured per-rank compute of one launch on
-    one GPU (profiles/r01_grid_sweep.json) is the same for row tiles and 2-D tiles of equal edge
-    count (8x1 0.665 ms vs 4x2 0.645; 4x1 1.274 vs 2x2 1.273; 2x1 2.494 vs 1x2 2.544), so column
-    groups only add the reduce-scatter of partial aggregates (60 MB per rank at 1x2).  Row tiles
-    are independent: no data-path collective.  --grid PRxPC selects the 2-D form with its RCCL
-    reduce-scatter."""
-    return world, 1
+def grid_shape(world, mode="edges"):
+    """Default rank grid (row groups pr x column groups pc) of the metric aggregate.
+
+    mode "edges" (the north-star form, bench.py's default): an edge partition of the reference's
+    T-row x column tiles (code/preprocessing.py:26-38) whose partial vertex aggregates are summed
+    over xGMI by RCCL -- 1x2, 2x2, 4x2, 4x4 ...: pc = 2 column groups once world >= 4 keeps the
+    reduce-scatter between pairs of GPUs (15 MB per rank at 8 GPUs on Reddit), pc = world below.
+    mode "rows": destination-row tiles (pc = 1), whose outputs are complete rows (the exchange
+    is then the all-gather of Y for the next layer)."""
+    if mode == "rows" or world == 1:
+        return world, 1
+    if world < 4:
+        return 1, world
+    pc = 2 if world <= 8 else 4
+    while world % pc:
+        pc //= 2
+    return world // pc, pc
+
+
+def row_cuts_ip(indptr, world):
+    """Destination-row cut points [world+1] balancing nnz, from an indptr tensor alone."""
+    ip = indptr
+    n = ip.numel() - 1
+    nnz = int(ip[-1])
+    targets = torch.arange(1, world, device=ip.device, dtype=torch.float64) * (nnz / world)
+    inner = torch.searchsorted(ip[1:].to(torch.float64), targets) + 1
+    return [0] + [min(int(v), n) for v in inner.cpu()] + [n]
 
 
 class GridShard:
@@ -307,35 +324,52 @@ class GridShard:
     row R_i + j*m + c*mk + v (mk = ceil(m / C)) sits at padded row c*pc*mk + j*mk + v, so chunk c
     is the contiguous [pc*mk] range holding one mk-row part per rank of the group -- one
     reduce-scatter per chunk, issued while chunk c+1 aggregates.  Rank j's output is then
-    [C*mk] rows, part c at c*mk (owned_rows gives their global ids)."""
+    [C*mk] rows, part c at c*mk (owned_rows gives their global ids).
+
+    Built from a whole graph (GridShard(graph, ...)) or from the rank's row group alone
+    (GridShard.from_rows: the multi-GPU bench, where no rank holds the whole graph)."""
 
     def __init__(self, graph, rank, pr, pc, chunks=1):
+        ip = graph.indptr
+        rcuts = row_cuts_ip(ip, pr)
+        ccuts = [int(c) for c in partition.column_cuts(graph, pc)]
+        i = rank // pc
+        r0, r1 = rcuts[i], rcuts[i + 1]
+        e0, e1 = int(ip[r0]), int(ip[r1])
+        self._build(rcuts, ccuts, rank, pr, pc, chunks, (ip[r0:r1 + 1] - e0).contiguous(),
+                    graph.indices[e0:e1].long(), e0)
+
+    @classmethod
+    def from_rows(cls, rcuts, ccuts, rank, pr, pc, row_indptr, row_src, chunks=1, e0=0):
+        """The shard from its row group only: row_indptr [n_i + 1] (local, from 0) and row_src (int64
+        source column of each of the group's edges, columns sorted within rows); e0 = the group's
+        first global edge id (edge_ids are global CSR ids, local_edge_ids index the group's edges)."""
+        self = cls.__new__(cls)
+        self._build(list(rcuts), list(ccuts), rank, pr, pc, chunks, row_indptr, row_src, e0)
+        return self
+
+    def _build(self, rcuts, ccuts, rank, pr, pc, chunks, lip, src, e0):
         self.pr, self.pc, self.rank = pr, pc, rank
         self.i, self.j = divmod(rank, pc)
-        dev = graph.device
-        ip = graph.indptr
-        targets = torch.arange(1, pr, device=dev, dtype=torch.float64) * (graph.nnz / pr)
-        inner = torch.searchsorted(ip[1:].to(torch.float64), targets) + 1
-        self.rcuts = [0] + [int(v) for v in inner.cpu()] + [graph.n_rows]
-        self.ccuts = [int(c) for c in partition.column_cuts(graph, pc)]
-        r0, r1 = self.rcuts[self.i], self.rcuts[self.i + 1]
-        c0, c1 = self.ccuts[self.j], self.ccuts[self.j + 1]
+        self.rcuts, self.ccuts = rcuts, ccuts
+        dev = lip.device
+        r0, r1 = rcuts[self.i], rcuts[self.i + 1]
+        c0, c1 = ccuts[self.j], ccuts[self.j + 1]
         self.r0, self.r1, self.c0, self.c1 = r0, r1, c0, c1
-        self.m = -(-(r1 - r0) // pc)
+        self.m = max(1, -(-(r1 - r0) // pc))
         self.chunks = max(1, int(chunks))
         self.mk = -(-self.m // self.chunks)
-        e0, e1 = int(ip[r0]), int(ip[r1])
-        src = graph.indices[e0:e1]
         keep = (src >= c0) & (src < c1)
-        deg = ip[r0 + 1:r1 + 1] - ip[r0:r1]
+        deg = lip[1:] - lip[:-1]
         rows = torch.repeat_interleave(torch.arange(r1 - r0, device=dev), deg)[keep]
-        local_src = (src[keep].long() - c0).to(torch.int32)
-        self.edge_ids = torch.nonzero(keep, as_tuple=False).flatten() + e0
+        local_src = (src[keep] - c0).to(torch.int32)
+        self.local_edge_ids = torch.nonzero(keep, as_tuple=False).flatten()
         if self.chunks > 1:  # chunk-major padded rows; a stable sort keeps each row's edge order
             jj, u = rows // self.m, rows % self.m
             rows = (u // self.mk) * (pc * self.mk) + jj * self.mk + u % self.mk
             order = torch.sort(rows, stable=True).indices
-            rows, local_src, self.edge_ids = rows[order], local_src[order], self.edge_ids[order]
+            rows, local_src, self.local_edge_ids = rows[order], local_src[order], self.local_edge_ids[order]
+        self.edge_ids = self.local_edge_ids + e0
         n_pad = self.chunks * pc * self.mk
         counts = torch.bincount(rows, minlength=n_pad)
         indptr = torch.zeros(n_pad + 1, dtype=torch.int64, device=dev)
@@ -355,7 +389,7 @@ class GridShard:
         """Global row ids of `rank`'s reduce-scatter output ([out_rows] rows; -1 = padding)."""
         i, j = divmod(rank, self.pc)
         r0, r1 = self.rcuts[i], self.rcuts[i + 1]
-        m = -(-(r1 - r0) // self.pc)
+        m = max(1, -(-(r1 - r0) // self.pc))
         if self.chunks == 1:
             t = torch.arange(m) + r0 + j * m
             return torch.where(t < r1, t, torch.full_like(t, -1))

@@ -148,6 +148,98 @@ def synthetic(n, e, seed=0, kind="lognormal", sigma=1.0, device="cpu", sort_cols
     return Graph(indptr, cols.to(torch.int32))
 
 
+M32 = 0xFFFFFFFF
+
+
+def _mulmod32(x, c):
+    """(x * c) mod 2^32 for uint32 values held in int64 tensors, without int64 overflow."""
+    lo = (x * (c & 0xFFFF)) & M32
+    hi = ((x * (c >> 16)) & 0xFFFF) << 16
+    return (lo + hi) & M32
+
+
+def mix32(x):
+    """lowbias32 integer hash of uint32 values in an int64 tensor: exact (bitwise equal) on CPU and GPU."""
+    x = x & M32
+    x = x ^ (x >> 16)
+    x = _mulmod32(x, 0x7FEB352D)
+    x = x ^ (x >> 15)
+    x = _mulmod32(x, 0x846CA68B)
+    return x ^ (x >> 16)
+
+
+def hash32(idx, seed, stream):
+    """Counter-based 32-bit hash of (seed, stream, idx) for idx < 2^32 (int64 tensor)."""
+    key = mix32(torch.tensor((seed * 0x9E3779B9 + stream * 0x85EBCA6B + 0x27D4EB2F) & M32, dtype=torch.int64))
+    return mix32(mix32(idx ^ int(key)) + int(stream))
+
+
+def hash_normal(idx, seed, stream, dtype=torch.float32):
+    """N(0, 1) values keyed by idx (Box-Muller on two counter hashes): any subset of a table can be
+    generated on its own, on any device, in any order."""
+    u1 = (hash32(idx, seed, 2 * stream).to(torch.float64) + 0.5) * (1.0 / 4294967296.0)
+    u2 = hash32(idx, seed, 2 * stream + 1).to(torch.float64) * (1.0 / 4294967296.0)
+    return (torch.sqrt(-2.0 * torch.log(u1)) * torch.cos(6.283185307179586 * u2)).to(dtype)
+
+
+def lognormal_degrees_host(n, e, seed=0, sigma=1.0):
+    """lognormal_degrees on the host (numpy, fp64): the same int64 [n] on every rank and device."""
+    import numpy as np
+    z = np.random.default_rng(seed).standard_normal(n)
+    raw = np.exp(sigma * z)
+    scaled = raw * (e / raw.sum())
+    deg = np.floor(scaled).astype(np.int64)
+    rem = int(e - int(deg.sum()))
+    if rem > 0:
+        frac = scaled - deg
+        top = np.argsort(-frac, kind="stable")[:rem]
+        deg[top] += 1
+    return deg
+
+
+class CounterCSR:
+    """A synthetic destination-sorted CSR whose every edge is a pure function of (seed, edge id).
+
+    Same shape model as synthetic() (lognormal degrees scaled to exactly e edges, uniform random
+    sources, columns sorted within each row), but the sources come from a counter
+    hash instead of a sequential generator, so a rank builds only its own rows -- and, after the
+    column filter, only its own (row group x column group) tile -- with no global pass
+    (multi-GPU bench, distributed.GridShard.from_rows).  Edge ids are generation order: edge e of
+    row r lies in [indptr[r], indptr[r+1]); per-edge data (GAT logits) are keyed by that id, so
+    sorting a row's columns moves nothing it depends on."""
+
+    def __init__(self, n, e, seed=0, sigma=1.0):
+        import numpy as np
+        self.n, self.e, self.seed = int(n), int(e), int(seed)
+        deg = lognormal_degrees_host(self.n, self.e, seed, sigma)
+        self.indptr_np = np.zeros(self.n + 1, np.int64)
+        np.cumsum(deg, out=self.indptr_np[1:])
+
+    def indptr(self, device):
+        return torch.from_numpy(self.indptr_np).to(device)
+
+    def sources(self, e0, e1, device):
+        """int64 source column of edges [e0, e1) in generation order."""
+        idx = torch.arange(e0, e1, device=device, dtype=torch.int64)
+        return (hash32(idx, self.seed, 1) * self.n) >> 32
+
+    def rows(self, r0, r1, device):
+        """Rows [r0, r1): (local indptr int64 [r1-r0+1], sources int64 in CSR order (sorted within
+        each row), gen int64 = the generation id of each CSR edge)."""
+        ip = self.indptr(device)
+        e0, e1 = int(self.indptr_np[r0]), int(self.indptr_np[r1])
+        src = self.sources(e0, e1, device)
+        lip = (ip[r0:r1 + 1] - e0).contiguous()
+        row = torch.repeat_interleave(torch.arange(r1 - r0, device=device, dtype=torch.int64), lip[1:] - lip[:-1])
+        order = torch.sort(row * self.n + src, stable=True).indices  # duplicates keep generation order
+        del row
+        return lip, src[order].contiguous(), order + e0
+
+    def graph(self, device):
+        lip, src, _ = self.rows(0, self.n, device)
+        return Graph(lip, src.to(torch.int32))
+
+
 def dataset_graph(name, seed=0, device="cpu", **kw):
     n, e = SHAPES[name]
     return synthetic(n, e, seed=seed, device=device, **kw)

@@ -18,13 +18,20 @@ from .graph import Graph
 
 def column_cuts(graph, world):
     """Source-column cut points [world+1] balancing nnz (prefix sum of per-column counts)."""
-    counts = torch.bincount(graph.indices.long(), minlength=graph.n_cols)
+    return cuts_from_counts(torch.bincount(graph.indices.long(), minlength=graph.n_cols), world)
+
+
+def cuts_from_counts(counts, world):
+    """Cut points [world+1] of a per-column nnz histogram (the column sums of the reference's tile
+    metadata, code/preprocessing.py:26-38) so every part holds ~nnz/world edges."""
+    n_cols = counts.numel()
+    nnz = float(counts.sum())
     csum = torch.cumsum(counts, 0)
-    targets = torch.arange(1, world, device=csum.device, dtype=torch.float64) * (graph.nnz / world)
+    targets = torch.arange(1, world, device=csum.device, dtype=torch.float64) * (nnz / world)
     inner = torch.searchsorted(csum.to(torch.float64), targets, right=False) + 1
     cuts = torch.cat([torch.zeros(1, dtype=torch.int64, device=csum.device), inner.to(torch.int64),
-                      torch.full((1,), graph.n_cols, dtype=torch.int64, device=csum.device)])
-    return torch.clamp(cuts, 0, graph.n_cols).cpu()
+                      torch.full((1,), n_cols, dtype=torch.int64, device=csum.device)])
+    return torch.clamp(cuts, 0, n_cols).cpu()
 
 
 class Shard:

@@ -16,12 +16,12 @@ for s in $STEPS; do
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
       rc=$?; echo "smoke rc=$rc"; tail -3 gpurun_out/smoke.log; stop_if_fatal $rc smoke ;;
     bench)
-      timeout -k 10 ${T_BENCH:-600} python bench.py ${BENCH_ARGS} > gpurun_out/bench.log 2>&1
+      timeout -k 10 ${T_BENCH:-600} python bench.py --pmc-dir gpurun_out/pmc ${BENCH_ARGS} > gpurun_out/bench.log 2>&1
       rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log; stop_if_fatal $rc bench ;;
     prof)
       export TMPDIR=/tmp
       timeout -k 10 ${T_PROF:-600} rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
-        -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/prof.log 2>&1
+        -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-pmc ${BENCH_ARGS} > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.log; stop_if_fatal $rc prof ;;
     pmc)
       export TMPDIR=/tmp
@@ -32,10 +32,12 @@ for s in $STEPS; do
         -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS} > gpurun_out/pmc_write.log 2>&1
       rc=$?; echo "pmc write rc=$rc"; stop_if_fatal $rc pmc ;;
     bench2)
-      GTA_DIST_BACKEND=gloo GTA_SINGLE_DEVICE=1 timeout -k 10 ${T_BENCH:-600} python -m torch.distributed.run \
-        --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --steps 3 --warmup 1 \
-        > gpurun_out/bench2.log 2>&1
-      rc=$?; echo "bench2 rc=$rc"; grep '^{' gpurun_out/bench2.log | tail -1; stop_if_fatal $rc bench2 ;;
+      for m in ${BENCH2_MODES:-edges rows}; do
+        GTA_DIST_BACKEND=gloo GTA_SINGLE_DEVICE=1 timeout -k 10 ${T_BENCH:-600} python -m torch.distributed.run \
+          --nnodes=1 --nproc-per-node ${BENCH2_RANKS:-2} --master-addr 127.0.0.1 --master-port 29511 bench.py \
+          --gpus ${BENCH2_RANKS:-2} --steps 3 --warmup 1 --mode $m ${BENCH2_ARGS} > gpurun_out/bench2_$m.log 2>&1
+        rc=$?; echo "bench2 $m rc=$rc"; grep '^{' gpurun_out/bench2_$m.log | tail -1; stop_if_fatal $rc bench2
+      done ;;
     layers)
       timeout -k 10 ${T_LAYERS:-600} python scripts/layer_bench.py ${LAYER_ARGS} > gpurun_out/layers.log 2>&1
       rc=$?; echo "layers rc=$rc"; tail -6 gpurun_out/layers.log; stop_if_fatal $rc layers ;;

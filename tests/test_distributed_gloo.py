@@ -256,13 +256,13 @@ def test_grid_tiles_reduce_scatter_gloo(pr, pc, chunks):
     assert q.get(timeout=10) < 1e-5
 
 
-def test_default_grid_is_row_tiles():
-    """bench.py --gpus N defaults to N destination-row tiles (no data-path collective); the row
-    tiles of a 1-column grid cover every edge exactly once and each rank owns its rows."""
+def test_row_tile_grid_covers_every_edge_once():
+    """--mode rows: N destination-row tiles (a 1-column grid) cover every edge exactly once and each
+    rank owns its rows."""
     from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, graph as G
     g = G.synthetic(500, 9000, seed=4)
     for world in (1, 2, 4, 8):
-        assert distributed.grid_shape(world) == (world, 1)
+        assert distributed.grid_shape(world, "rows") == (world, 1)
         shards = [distributed.GridShard(g, r, world, 1) for r in range(world)]
         assert sum(s.graph.nnz for s in shards) == g.nnz
         owned = torch.cat([s.owned_rows(r) for r, s in enumerate(shards)])
