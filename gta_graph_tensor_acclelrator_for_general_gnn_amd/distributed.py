@@ -39,6 +39,36 @@ def row_cuts(graph, world):
     return [0] + [min(int(v), graph.n_rows) for v in inner.cpu()] + [graph.n_rows]
 
 
+
+NODE_OPS = ("scatter", "applynode")   # their external inputs are node rows
+EDGE_OPS = ("applyedge", "gather")    # theirs are edge rows
+
+
+def tensor_kind(key, rows, n_global, e_global, opgraph=None):
+    """"w" (weights, broadcast rows: unchanged), "node" ([N, *]) or "edge" ([E, *]) for a layer
+    tensor.  'ext:<op>:<slot>' inputs are classified by their op's type when the op graph is given,
+    so the ambiguous N == E case (and an edge input of an applyedge op) is sliced correctly; other
+    keys and calls without the op graph fall back to the row count."""
+    if key.startswith("w:"):
+        return "w"
+    if key == "x_edge":
+        return "edge"
+    if opgraph is not None and key.startswith("ext:"):
+        try:
+            op = opgraph.ops[int(key.split(":")[1])]
+        except (ValueError, IndexError):
+            op = None
+        if op is not None and rows not in (0, 1):
+            if op.type in NODE_OPS and rows == n_global:
+                return "node"
+            if op.type in EDGE_OPS and rows == e_global:
+                return "edge"
+    if rows == e_global and rows != n_global:
+        return "edge"
+    if rows == n_global:
+        return "node"
+    return "w"
+
 class DistShard:
     """Rank `rank`'s part of `graph` (see module docstring)."""
     local_rows = False  # gathers are partial sums over this rank's source columns
@@ -90,17 +120,20 @@ class DistShard:
         j = torch.arange(self.chunks * self.mk)
         return torch.where(j < n_q, self.cuts[q] + j, torch.full_like(j, -1))
 
-    def local_tensors(self, tensors):
+    def local_tensors(self, tensors, opgraph=None):
         """Global layer tensors -> this rank's: node tensors [N, *] -> row block, edge tensors
-        [E, *] -> the shard's edges (CSR order kept), weights / broadcast rows unchanged."""
+        [E, *] -> the shard's edges (CSR order kept), weights / broadcast rows unchanged.
+        With the op graph, an 'ext:op:slot' input is classified by its op's type (tensor_kind),
+        which settles N == E."""
         out = {}
         for k, t in tensors.items():
             rows = t.shape[0] if t.dim() else 0
-            if k.startswith("w:"):
+            kind = tensor_kind(k, rows, self.n_global, self.e_global, opgraph)
+            if kind == "w":
                 out[k] = t
-            elif k == "x_edge" or (rows == self.e_global and rows != self.n_global):
+            elif kind == "edge":
                 out[k] = t[self.edge_ids.to(t.device)].contiguous()
-            elif rows == self.n_global:
+            elif kind == "node":
                 out[k] = t[self.c0:self.c1].contiguous()
             else:
                 out[k] = t
@@ -142,32 +175,33 @@ class RowShard:
 
     def padded(self, t):
         """Global node tensor [N, *] -> the padded table layout [world*m, *] (cached per tensor)."""
-        key = (t.data_ptr(), tuple(t.shape), t._version)
+        key = (id(t), t._version)  # the entry holds t, so its id stays unique (data_ptr is 0 for every empty tensor)
         hit = self._padded.get(key)
         if hit is None:
             full = t.new_zeros(self.world * self.m, *t.shape[1:])
             for q in range(self.world):
                 a, b = self.cuts[q], self.cuts[q + 1]
                 full[q * self.m: q * self.m + b - a] = t[a:b]
-            hit = self._padded[key] = (t, full)  # holds t: its storage (and key) stay valid
+            hit = self._padded[key] = (t, full)
         return hit[1]
 
     @property
     def edge_ids(self):
         return torch.arange(self.e0, self.e1, device=self.graph.device)
 
-    def local_tensors(self, tensors):
+    def local_tensors(self, tensors, opgraph=None):
         """Global layer tensors -> this rank's: node tensors [N, *] -> rows [r0, r1), edge tensors
-        [E, *] -> edges [e0, e1), weights / broadcast rows unchanged."""
+        [E, *] -> edges [e0, e1), weights / broadcast rows unchanged (classified by tensor_kind)."""
         out = {}
         self.inputs_full = {}  # this layer's whole inputs only (a later layer's x is a row block)
         for k, t in tensors.items():
             rows = t.shape[0] if t.dim() else 0
-            if k.startswith("w:"):
+            kind = tensor_kind(k, rows, self.n_global, self.e_global, opgraph)
+            if kind == "w":
                 out[k] = t
-            elif k == "x_edge" or (rows == self.e_global and rows != self.n_global):
+            elif kind == "edge":
                 out[k] = t[self.e0:self.e1].contiguous()
-            elif rows == self.n_global:
+            elif kind == "node":
                 out[k] = t[self.r0:self.r1].contiguous()
                 self.inputs_full[k] = t
             else:
@@ -219,8 +253,11 @@ class Comm:
     def src_rows(self, x):
         """Source-side table of a row shard: every rank's block, padded [world*m, F] (one all-gather
         per distinct tensor; the padded column ids of RowShard index it)."""
-        key = (x.data_ptr(), tuple(x.shape), tuple(x.stride()), x._version)
-        hit = self._filled.get(key)  # holds x, so its storage (and key) cannot be reused meanwhile
+        # keyed on the tensor object: the entry holds x, so id(x) cannot be reused meanwhile.  A key on
+        # data_ptr() would merge distinct zero-element tensors (data_ptr 0) on an empty shard, which
+        # would then skip an all-gather its peers run (a collective mismatch)
+        key = (id(x), x._version)
+        hit = self._filled.get(key)
         if hit is None:
             hit = self._filled[key] = (x, self._all_blocks(x))
         return hit[1]
@@ -271,7 +308,7 @@ def run_stream(opgraph, stream, shard, tensors, semantics=None, group=None, plan
 
     from . import executor
     comm = Comm(shard, group)
-    ex = executor.Executor(opgraph, stream, shard.graph, shard.local_tensors(tensors), semantics, plan_chunk,
+    ex = executor.Executor(opgraph, stream, shard.graph, shard.local_tensors(tensors, opgraph), semantics, plan_chunk,
                            dist=comm)
     cuda = shard.graph.device.type == "cuda"
     if cuda:

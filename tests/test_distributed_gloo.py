@@ -54,6 +54,9 @@ def _worker(rank, world, port, golden_dir, q, layout="cols"):
             tensors = workloads.make_tensors(og, g, net, seed=3)
             if layout == "cols":
                 shard = distributed.DistShard(g, rank, world)
+            elif layout == "rows-empty":  # rank 1 owns no row; every source table is all-gathered
+                cuts = [0, g.n_rows // 2, g.n_rows // 2] + [g.n_rows] * (world - 2)
+                shard = distributed.RowShard(g, rank, world, cuts=cuts, replicate_inputs=False)
             else:  # "rows": model inputs replicated; "rows-allgather": every source table exchanged
                 shard = distributed.RowShard(g, rank, world, replicate_inputs=layout == "rows")
             res, ex = distributed.run_stream(og, st, shard, tensors, sem)
@@ -74,10 +77,13 @@ def _worker(rank, world, port, golden_dir, q, layout="cols"):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,layout", [(2, "cols"), (3, "cols"), (2, "rows"), (3, "rows"), (2, "rows-allgather")])
+@pytest.mark.parametrize("world,layout", [(2, "cols"), (3, "cols"), (2, "rows"), (3, "rows"), (2, "rows-allgather"),
+                                          (3, "rows-empty")])
 def test_layer_streams_distributed_gloo(golden_dir, world, layout):
     """layout "cols": source-column shards (reduce-scatter per gather); "rows": destination-row
-    shards (all-gather per source table, fusions on)."""
+    shards (all-gather per source table, fusions on); "rows-empty": a live group in which rank 1
+    owns no row (repeated cut), so its distinct same-width source tables are all zero-element --
+    each must still join every all-gather its peers run, and the values must match the oracle."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
@@ -267,3 +273,66 @@ def test_row_tile_grid_covers_every_edge_once():
         assert sum(s.graph.nnz for s in shards) == g.nnz
         owned = torch.cat([s.owned_rows(r) for r, s in enumerate(shards)])
         assert torch.equal(torch.sort(owned[owned >= 0]).values, torch.arange(g.n_rows))
+
+
+def _src_rows_worker(rank, world, port, q):
+    import datetime
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=30))
+    try:
+        from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, graph as G
+        g = G.synthetic(12, 60, seed=4)
+        cuts = [0, 6, 6, 12]  # rank 1 owns no row
+        shard = distributed.RowShard(g, rank, world, cuts=cuts, replicate_inputs=False)
+        comm = distributed.Comm(shard)
+        assert comm.on
+        tabs = [torch.arange(g.n_rows * 4, dtype=torch.float32).view(g.n_rows, 4) * (t + 1) for t in range(3)]
+        for t, full_t in enumerate(tabs):  # three distinct same-width tables; rank 1's blocks are all [0, 4]
+            mine = full_t[shard.r0:shard.r1].clone()
+            got = comm.src_rows(mine)
+            for qq in range(world):
+                a, b = cuts[qq], cuts[qq + 1]
+                torch.testing.assert_close(got[qq * shard.m: qq * shard.m + b - a], full_t[a:b])
+            assert comm.src_rows(mine) is got  # a repeated table is not exchanged again
+        q.put(("ok", rank))
+    except Exception as e:
+        q.put(("fail", f"rank {rank}: {type(e).__name__}: {e}"))
+        raise
+    finally:
+        dist.destroy_process_group()
+
+
+def test_src_rows_distinct_tables_on_an_empty_rank():
+    """Comm.src_rows' cache must tell distinct zero-element blocks apart (their
+    data_ptr is 0), or the empty rank skips an all-gather its peers run."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_src_rows_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+    res = [q.get(timeout=10) for _ in range(3)]
+    assert all(s == "ok" for s, _ in res), res
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+
+
+def test_tensor_kind_uses_the_op_type_when_n_equals_e():
+    """with N == E the row count cannot tell node from edge inputs; the op graph can."""
+    from types import SimpleNamespace as NS
+
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, graph as G
+    og = NS(ops=[NS(type="scatter"), NS(type="applyedge"), NS(type="gather"), NS(type="applynode")])
+    kind = lambda k, rows: distributed.tensor_kind(k, rows, 10, 10, og)  # noqa: E731
+    assert [kind(f"ext:{i}:1", 10) for i in range(4)] == ["node", "edge", "edge", "node"]
+    assert kind("x_edge", 10) == "edge" and kind("w:3", 10) == "w" and kind("ext:1:1", 1) == "w"
+    assert distributed.tensor_kind("ext:1:1", 10, 10, 10) == "node"  # without the op graph: row count
+    # a RowShard slices an applyedge input of an N == E graph as edges [e0, e1)
+    ip = np.array([0, 0, 0, 3, 3, 4, 5, 5, 8, 9, 10])
+    g = G.from_numpy(ip, np.arange(10, dtype=np.int32) % 10)
+    s = distributed.RowShard(g, 1, 2)
+    t = torch.arange(10, dtype=torch.float32).view(10, 1)
+    out = s.local_tensors({"ext:1:1": t, "ext:0:0": t}, og)
+    torch.testing.assert_close(out["ext:1:1"], t[s.e0:s.e1])
+    torch.testing.assert_close(out["ext:0:0"], t[s.r0:s.r1])

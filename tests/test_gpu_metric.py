@@ -1,0 +1,58 @@
+"""The exact timed kernel of bench.py at FULL size, against the fp64 oracle.
+
+The metric block is Inst_fused [applyedge, gather][MUL, ADD] of GAT layer 1
+(`FinalVersion For Paper/hardware_info.yaml:35-38`, lowered by inst_fusion_x2
+`code/interpreter.py:575-636`):  Y[i] = sum_{e -> i} alpha[e, head(c)] * X1[src(e)].
+bench.py runs it on the Reddit-shaped counter CSR (N = 232,965, E = 114,615,892, F = 128, H = 8)
+through ops.aggregate_blocked at the auto block count (B = 20).  This test builds the same inputs
+(metric.Shard on one rank), runs the same call, and re-derives sampled rows -- the heaviest and
+the lightest row included -- in fp64 with oracle/isa_ref.aggregate.
+Tolerance: |err| <= 1e-5 * sum|terms| + 1e-6 per element.
+Also checked: two launches are bitwise equal (determinism) and rows without edges are exactly 0.
+"""
+import numpy as np
+import pytest
+import torch
+
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import metric, ops
+from oracle import isa_ref
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def shard(dev):
+    s = metric.Shard(metric.N_REDDIT, metric.E_REDDIT, 0, 1, 1, 1, dev)
+    yield s
+    del s
+    torch.cuda.empty_cache()
+
+
+def _check(shard, y, k=384):
+    s = shard.sample_rows(y, torch.arange(shard.n), k=k)
+    ref = isa_ref.aggregate(s["indptr"], s["indices"], s["x"], "src", s["alpha"])
+    bound = 1e-5 * isa_ref.aggregate_abs(s["indptr"], s["indices"], s["x"], "src", s["alpha"]) + 1e-6
+    err = np.abs(s["y"].astype(np.float64) - ref)
+    assert np.all(err <= bound), f"max err/bound {(err / bound).max():.3g} over {len(s['rows'])} rows"
+    return len(s["rows"])
+
+
+def test_metric_kernel_full_reddit_vs_oracle(shard):
+    g = shard.graph
+    assert g.n_rows == metric.N_REDDIT and g.nnz == metric.E_REDDIT
+    blocks = ops.BlockedPlan.auto_blocks(g, metric.F)
+    assert blocks == 20, "bench.py's auto block count for the Reddit table"
+    y = ops.aggregate_blocked(g, shard.x, shard.alpha, blocks=blocks)
+    y2 = ops.aggregate_blocked(g, shard.x, shard.alpha, blocks=blocks)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2), "two launches differ"
+    deg = g.indptr[1:] - g.indptr[:-1]
+    assert torch.all(y[deg == 0] == 0)
+    assert _check(shard, y) > 300
+
+
+def test_metric_single_pass_full_reddit_vs_oracle(shard):
+    """The unblocked row-chunk plan kernel (bench --impl plan) on the same inputs."""
+    y = ops.aggregate(shard.graph, shard.x, "src", shard.alpha, plan=512)
+    torch.cuda.synchronize()
+    _check(shard, y, k=128)
