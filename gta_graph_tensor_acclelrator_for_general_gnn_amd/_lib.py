@@ -10,7 +10,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgta.so")
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # enum mirrors of include/gta.h
 GTA_F32, GTA_BF16, GTA_F32_BF16 = 0, 1, 2
@@ -23,7 +23,6 @@ SF = {"NONE": 0, "RELU": 1, "EXP_LEAKY_RELU": 2, "ELU": 3, "EXP": 4, "LEAKY_RELU
 _i64, _i32, _vp, _cp = ctypes.c_int64, ctypes.c_int, ctypes.c_void_p, ctypes.c_char_p
 
 # name -> (restype, argtypes); every symbol here is declared in include/gta.h
-# except gta_debug_set (a tuning hook for bench.py)
 SIGNATURES = {
     "gta_abi_version": (_i32, []),
     "gta_last_error": (_cp, []),
@@ -53,6 +52,7 @@ SIGNATURES = {
                                      _i64, _vp]),
     "gta_tile_nnz": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "gta_debug_set": (_i32, [_cp, _i64]),
+    "gta_debug_get": (_i32, [_cp, ctypes.POINTER(_i64)]),
 }
 
 _lock = threading.Lock()

@@ -831,14 +831,63 @@ __device__ __forceinline__ float quad_bcast(float v) {  // lane (l & ~3) | SEL o
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), SEL * 0x55, 0xF, 0xF, false));
 }
 
+// In-launch ordered reduce (FUSE): instead of a k_seg_reduce pass, the LAST item of a row to
+// finish sums the row's partials in its fixed (block, part) order and writes y.  Hand-off
+// (cdna_hip_programming.md §5 split-K recipe, sc1 form; MI355X_MICROARCH.md § visibility): every
+// item stores its 512-B partial write-through (buffer store, sc1), the storing wave drains
+// (s_waitcnt vmcnt(0)), then one lane per half-wave adds 1 to the row's agent-scope counter;
+// the half-wave whose add returns (items - 1) is the last arriver and reads the row's partials
+// with sc1 loads (L1 bypassed; no other workgroup reads a slab line before its row's counter is
+// complete, and the launch boundary invalidates the L2s, so no XCD holds a stale copy).  The
+// sum order is the row's item list whatever the arrival order: bitwise equal to k_seg_reduce.
+// A row's only item (low-degree rows) writes y directly (0 + p, as the reduce would).
+// Counters are zeroed, and rows without items written, by k_fuse_prep ahead of every launch.
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+struct FuseArgs {
+  const int64_t* row_ptr;    // items of row r: row_items[row_ptr[r] .. row_ptr[r + 1])
+  const int32_t* row_items;  // (block, part) order
+  int32_t* cnt;              // arrival counter per row
+  const float* row_scale;
+  float* y;
+  int64_t ldy;
+  int accumulate;
+  uint32_t slab_bytes;       // slab range of the buffer descriptor (< 2^32)
+};
+
+__global__ void __launch_bounds__(kBlock)
+k_fuse_prep(int64_t n_rows, int F, FuseArgs fa) {
+  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (r >= n_rows) return;
+  fa.cnt[r] = 0;
+  if (fa.row_ptr[r + 1] != fa.row_ptr[r]) return;
+  const float v = (fa.row_scale ? fa.row_scale[r] : 1.f) * 0.f;  // k_seg_reduce's scale * (empty sum)
+  float* yp = fa.y + r * fa.ldy;
+  for (int c = 0; c < F; ++c) yp[c] = fa.accumulate ? yp[c] + v : v;
+}
+
+// y row epilogue of the ordered reduce: y = scale * s, or y += scale * s (k_seg_reduce's form)
+__device__ __forceinline__ void fuse_store_row(const FuseArgs& fa, int64_t row, int col, const float (&s)[4]) {
+  const float scale = fa.row_scale ? fa.row_scale[row] : 1.f;
+  float4* yp = reinterpret_cast<float4*>(fa.y + row * fa.ldy + col);
+  float4 o;
+  if (fa.accumulate) {
+    o = *yp;
+    o.x += scale * s[0]; o.y += scale * s[1]; o.z += scale * s[2]; o.w += scale * s[3];
+  } else {
+    o.x = scale * s[0]; o.y = scale * s[1]; o.z = scale * s[2]; o.w = scale * s[3];
+  }
+  *yp = o;
+}
+
 // W1 (WEIGHTED with one weight per edge, e.g. GCN / GraphSAGE-mean [E, 1]): the weights of a
 // 32-edge chunk arrive with its indices (lane l loads w[e + l]) and edge u's weight is broadcast
 // like its index (bcastG), instead of one load per edge per lane.
-template <bool WEIGHTED, int NT, bool W1 = false>
-__global__ void __launch_bounds__(kBlock)
+template <bool WEIGHTED, int NT, bool W1 = false, bool FUSE = false, int MINW = 1>
+__global__ void __launch_bounds__(kBlock, MINW)  // MINW: waves per SIMD the register allocation must allow
 k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
           uint32_t row_bytes, const float* __restrict__ w, int64_t ldw, float* __restrict__ slabs,
-          const SegItem* __restrict__ items) {
+          const SegItem* __restrict__ items, FuseArgs fa = FuseArgs{}) {
   constexpr int G = 32, F = 128, U = 8;
   const int lane = threadIdx.x & (kWave - 1);
   const int l32 = lane & (G - 1);
@@ -918,6 +967,55 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
     if (W1) wv = wvn;
     ic += G;
     if (WEIGHTED) wc += static_cast<int64_t>(G) * ldw;
+  }
+  if (FUSE) {
+    // Nothing of the epilogue stays live through the gather loop (the unfused kernel's 78 VGPRs,
+    // 6 waves per SIMD): the row is re-read from the item record (volatile: not kept from the
+    // first load) while the partial is stored, and its item count after.
+    if (len == 0) return;
+    const int col = l32 * 4;
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slabs, 0, fa.slab_bytes, 0x00020000);
+    u32x4 pv;
+    pv.x = __float_as_uint(acc[0]); pv.y = __float_as_uint(acc[1]);
+    pv.z = __float_as_uint(acc[2]); pv.w = __float_as_uint(acc[3]);
+    __builtin_amdgcn_raw_buffer_store_b128(pv, rs, static_cast<int>(static_cast<uint32_t>(k) * (F * 4u) + col * 4u), 0,
+                                           16 /* sc1: write-through */);
+    const int row = *reinterpret_cast<const volatile int32_t*>(&items[k].row);
+    const int64_t j0 = fa.row_ptr[row], j1 = fa.row_ptr[row + 1];
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before its ticket
+    if (j1 - j0 == 1) {  // the row's only item: y directly (0 + p, as the reduce would); its slab row is unread
+      const float s1[4] = {0.f + acc[0], 0.f + acc[1], 0.f + acc[2], 0.f + acc[3]};
+      fuse_store_row(fa, row, col, s1);
+      return;
+    }
+    int old = 0;
+    if (l32 == 0) old = __hip_atomic_fetch_add(fa.cnt + row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __shfl(old, lane & G);
+    if (old != static_cast<int>(j1 - j0) - 1) return;  // not the last arriver of this row
+    float s4[4] = {0.f, 0.f, 0.f, 0.f};
+    for (int64_t j = j0; j < j1; j += G) {
+      const int n = static_cast<int>(min<int64_t>(G, j1 - j));
+      const int ids = (l32 < n) ? fa.row_items[j + l32] : 0;
+      constexpr int R = 4;  // partials in flight (the gather loop's registers are dead here)
+      for (int t = 0; t < n; t += R) {
+        u32x4 p[R];
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+          const uint32_t id = static_cast<uint32_t>(__shfl(ids, (lane & G) | ((t + u) & (G - 1))));
+          if (t + u < n)
+            p[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(id * (F * 4u) + col * 4u), 0, 16 /* sc1 */);
+        }
+#pragma unroll
+        for (int u = 0; u < R; ++u) {
+          if (t + u < n) {
+            s4[0] += __uint_as_float(p[u].x); s4[1] += __uint_as_float(p[u].y);
+            s4[2] += __uint_as_float(p[u].z); s4[3] += __uint_as_float(p[u].w);
+          }
+        }
+      }
+    }
+    fuse_store_row(fa, row, col, s4);
+    return;
   }
   if (len > 0) {
     float* o = slabs + k * F + l32 * 4;
@@ -2317,30 +2415,84 @@ bool dispatch_lpe(int lpe, int nv, int xm, int wm, bool nt, const AggArgs& a, in
   }
 }
 
-int g_force_lpe = 0;  // tuning hooks (gta_debug_set); 0 = automatic
-int g_force_vw = 0;
-int g_agg_nt = 0;     // non-temporal index/weight loads in the SpMM form
-int g_agg_lean = 1;   // k_agg_lean for F = 64*VW SpMM shapes
-int64_t g_seg_waves = 0;  // persistent waves of the column-blocked kernel (0 = 8 per SIMD)
-int g_seg_quarter = 1;     // quarter-wave (4 items per wave) form of the blocked aggregate
-int g_seg_lanes = 32;      // lanes per item of that form at F = 128: 32 (2 items/wave, measured 3 % faster) or 16
-int g_seg_nt = 2;          // non-temporal bits of the multi-item forms at F = 128, U = 8: 2 = slab stores (-1 %)
-int g_seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
-int g_seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
-int g_apply_node_vec = 1;  // k_apply_node4 (float4, 32-bit index math) for the common apply_node shapes
-int g_seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
-int g_plan_len_sort = 1;   // blocked plan: each block's items sorted by length (matched half-wave pairs)
-int g_att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
-int g_att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
-int g_mm_blaslt = 1;        // plain fp32 UPDATE with M >= g_mm_blaslt_min_m on hipBLASLt (gta_update_mm_t)
-int64_t g_mm_blaslt_min_m = 1024;
-int g_mm_blaslt_tune = 1;  // time the heuristic's top candidates at a shape's first use
-int g_mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
-int g_mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
-int64_t g_mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
-int g_apply_edge_form = 1;  // 1: row-sweep K3 kernels (cols / pack); 0: the generic per-element kernel
-int g_esm_lane = 1;        // edge-per-lane edge-softmax when H in {4,8,16} and rows are 16-B aligned
-int g_esm_keep = 4;        // chunks of 64 edges held in VGPRs by the edge-per-lane form (2 or 4)
+// Tuning knobs (benchmark hooks, gta_debug_set): per calling THREAD, so a knob set by one thread
+// never changes another thread's concurrent calls; a call reads its own thread's values.  The
+// defaults are the measured choices.
+struct Tuning {
+  int force_lpe = 0;  // tuning hooks (gta_debug_set); 0 = automatic
+  int force_vw = 0;
+  int agg_nt = 0;     // non-temporal index/weight loads in the SpMM form
+  int agg_lean = 1;   // k_agg_lean for F = 64*VW SpMM shapes
+  int64_t seg_waves = 0;  // persistent waves of the column-blocked kernel (0 = 8 per SIMD)
+  int seg_quarter = 1;     // quarter-wave (4 items per wave) form of the blocked aggregate
+  int seg_lanes = 32;      // lanes per item of that form at F = 128: 32 (2 items/wave, measured 3 % faster) or 16
+  int seg_nt = 2;          // non-temporal bits of the multi-item forms at F = 128, U = 8: 2 = slab stores (-1 %)
+  int seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
+  int seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
+  int apply_node_vec = 1;  // k_apply_node4 (float4, 32-bit index math) for the common apply_node shapes
+  int seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
+  int plan_len_sort = 1;   // blocked plan: each block's items sorted by length (matched half-wave pairs)
+  int att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
+  int att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
+  int mm_blaslt = 1;        // plain fp32 UPDATE with M >= mm_blaslt_min_m on hipBLASLt (gta_update_mm_t)
+  int64_t mm_blaslt_min_m = 1024;
+  int mm_blaslt_tune = 1;  // time the heuristic's top candidates at a shape's first use
+  int mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
+  int mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
+  int64_t mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
+  int apply_edge_form = 1;  // 1: row-sweep K3 kernels (cols / pack); 0: the generic per-element kernel
+  int esm_lane = 1;        // edge-per-lane edge-softmax when H in {4,8,16} and rows are 16-B aligned
+  int esm_keep = 4;        // chunks of 64 edges held in VGPRs by the edge-per-lane form (2 or 4)
+  int seg_fuse = 0;          // k_agg_h32 with the in-launch ordered reduce (no k_seg_reduce pass): bitwise equal,
+                             // but 5.28 vs 4.93 ms on Reddit (the per-item drain + ticket costs more than the
+                             // pass it removes; profiles/r02_fused_reduce_ab.json); 2 = the same at 6 waves/SIMD
+};
+
+Tuning& tuning() {
+  thread_local Tuning t;
+  return t;
+}
+
+// Tuning hooks (gta.h): the calling thread's knobs, by name
+struct Knob {
+  const char* key;
+  int Tuning::*i32;
+  int64_t Tuning::*i64;
+};
+
+const Knob* find_knob(const char* key) {
+  static const Knob knobs[] = {
+      {"agg_lpe", &Tuning::force_lpe, nullptr},
+      {"agg_vw", &Tuning::force_vw, nullptr},
+      {"agg_nt", &Tuning::agg_nt, nullptr},
+      {"agg_lean", &Tuning::agg_lean, nullptr},
+      {"seg_waves", nullptr, &Tuning::seg_waves},
+      {"seg_nt", &Tuning::seg_nt, nullptr},
+      {"seg_u", &Tuning::seg_u, nullptr},
+      {"seg_lanes", &Tuning::seg_lanes, nullptr},
+      {"seg_lean", &Tuning::seg_lean, nullptr},
+      {"seg_fuse", &Tuning::seg_fuse, nullptr},
+      {"att_lean", &Tuning::att_lean, nullptr},
+      {"att_direct", &Tuning::att_direct, nullptr},
+      {"plan_len_sort", &Tuning::plan_len_sort, nullptr},
+      {"seg_lean_w1", &Tuning::seg_lean_w1, nullptr},
+      {"apply_node_vec", &Tuning::apply_node_vec, nullptr},
+      {"seg_quarter", &Tuning::seg_quarter, nullptr},
+      {"mm_prefetch", &Tuning::mm_prefetch, nullptr},
+      {"mm_blaslt", &Tuning::mm_blaslt, nullptr},
+      {"mm_blaslt_min_m", nullptr, &Tuning::mm_blaslt_min_m},
+      {"mm_blaslt_tune", &Tuning::mm_blaslt_tune, nullptr},
+      {"mm_vstore", &Tuning::mm_vstore, nullptr},
+      {"mm_blocks_per_cu", nullptr, &Tuning::mm_blocks_per_cu},
+      {"apply_edge_form", &Tuning::apply_edge_form, nullptr},
+      {"esm_lane", &Tuning::esm_lane, nullptr},
+      {"esm_keep", &Tuning::esm_keep, nullptr},
+  };
+  const std::string k(key ? key : "");
+  for (const Knob& kb : knobs)
+    if (k == kb.key) return &kb;
+  return nullptr;
+}
 
 }  // namespace
 
@@ -2352,34 +2504,19 @@ extern "C" {
 int gta_abi_version(void) { return GTA_ABI_VERSION; }
 const char* gta_last_error(void) { return g_err.c_str(); }
 
-// not in gta.h: benchmarking hook to pin the aggregate kernel variant
 int gta_debug_set(const char* key, int64_t value) {
-  std::string k(key ? key : "");
-  if (k == "agg_lpe") { g_force_lpe = static_cast<int>(value); return 0; }
-  if (k == "agg_vw") { g_force_vw = static_cast<int>(value); return 0; }
-  if (k == "agg_nt") { g_agg_nt = static_cast<int>(value); return 0; }
-  if (k == "agg_lean") { g_agg_lean = static_cast<int>(value); return 0; }
-  if (k == "seg_waves") { g_seg_waves = value; return 0; }
-  if (k == "seg_nt") { g_seg_nt = static_cast<int>(value); return 0; }
-  if (k == "seg_u") { g_seg_u = static_cast<int>(value); return 0; }
-  if (k == "seg_lanes") { g_seg_lanes = static_cast<int>(value); return 0; }
-  if (k == "seg_lean") { g_seg_lean = static_cast<int>(value); return 0; }
-  if (k == "att_lean") { g_att_lean = static_cast<int>(value); return 0; }
-  if (k == "att_direct") { g_att_direct = static_cast<int>(value); return 0; }
-  if (k == "plan_len_sort") { g_plan_len_sort = static_cast<int>(value); return 0; }
-  if (k == "seg_lean_w1") { g_seg_lean_w1 = static_cast<int>(value); return 0; }
-  if (k == "apply_node_vec") { g_apply_node_vec = static_cast<int>(value); return 0; }
-  if (k == "seg_quarter") { g_seg_quarter = static_cast<int>(value); return 0; }
-  if (k == "mm_prefetch") { g_mm_prefetch = static_cast<int>(value); return 0; }
-  if (k == "mm_blaslt") { g_mm_blaslt = static_cast<int>(value); return 0; }
-  if (k == "mm_blaslt_min_m") { g_mm_blaslt_min_m = value; return 0; }
-  if (k == "mm_blaslt_tune") { g_mm_blaslt_tune = static_cast<int>(value); return 0; }
-  if (k == "mm_vstore") { g_mm_vstore = static_cast<int>(value); return 0; }
-  if (k == "mm_blocks_per_cu") { g_mm_blocks_per_cu = value; return 0; }
-  if (k == "apply_edge_form") { g_apply_edge_form = static_cast<int>(value); return 0; }
-  if (k == "esm_lane") { g_esm_lane = static_cast<int>(value); return 0; }
-  if (k == "esm_keep") { g_esm_keep = static_cast<int>(value); return 0; }
-  return fail(GTA_ERR_ARG, "gta_debug_set: unknown key " + k);
+  const Knob* kb = find_knob(key);
+  if (!kb) return fail(GTA_ERR_ARG, std::string("gta_debug_set: unknown key ") + (key ? key : ""));
+  if (kb->i32) tuning().*(kb->i32) = static_cast<int>(value);
+  else tuning().*(kb->i64) = value;
+  return GTA_OK;
+}
+
+int gta_debug_get(const char* key, int64_t* value) {
+  const Knob* kb = find_knob(key);
+  if (!kb || !value) return fail(GTA_ERR_ARG, std::string("gta_debug_get: unknown key ") + (key ? key : ""));
+  *value = kb->i32 ? static_cast<int64_t>(tuning().*(kb->i32)) : tuning().*(kb->i64);
+  return GTA_OK;
 }
 
 int64_t gta_aggregate_plan_bytes(int64_t n_rows, int64_t nnz, int64_t chunk) {
@@ -2439,7 +2576,7 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
     return true;
   };
   int vw = ok_vw(4) ? 4 : (ok_vw(2) ? 2 : 1);
-  if (g_force_vw && g_force_vw <= vw && ok_vw(g_force_vw)) vw = g_force_vw;
+  if (tuning().force_vw && tuning().force_vw <= vw && ok_vw(tuning().force_vw)) vw = tuning().force_vw;
   // one edge per wave instruction (LPE = 64, wave-uniform row base) whenever the
   // row fills 64 lanes at >= 8 B/lane: measured 3 % faster than two edges per
   // instruction at float4 for F = 128 (profiles/r01_agg_sweep_1.json)
@@ -2453,8 +2590,8 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
     lpe = 4;
     while (lpe < lanes) lpe <<= 1;
   }
-  if (g_force_lpe == 32 && F == 128 && ok_vw(4)) { lpe = 32; vw = 4; nv = 1; }
-  if (g_force_lpe == 64 && F == 128 && ok_vw(2)) { lpe = 64; vw = 2; nv = 1; }
+  if (tuning().force_lpe == 32 && F == 128 && ok_vw(4)) { lpe = 32; vw = 4; nv = 1; }
+  if (tuning().force_lpe == 64 && F == 128 && ok_vw(2)) { lpe = 64; vw = 2; nv = 1; }
 
   AggArgs a{};
   a.indptr = indptr; a.indices = indices; a.n_rows = n_rows;
@@ -2472,7 +2609,7 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
   bool ok = false;
   // lean path: one edge per instruction exactly filling the wave, SpMM form
   int gl = (wm == WM_HEAD) ? gsz / vw : 0;
-  const bool lean_shape = g_agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
+  const bool lean_shape = tuning().agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
                           !a.x_is_row && wm != WM_FULL && (wm == WM_NONE || gl == 4 || gl == 8 || gl == 16);
   if (lean_shape) {
     const int64_t blocks = (bound + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -2492,9 +2629,9 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
     ok = true;
   }
   if (!ok) switch (vw) {
-    case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, g_agg_nt != 0, a, bound, s); break;
-    case 2: ok = dispatch_lpe<2>(lpe, nv, xm, wm, g_agg_nt != 0, a, bound, s); break;
-    default: ok = dispatch_lpe<1>(lpe, nv, xm, wm, g_agg_nt != 0, a, bound, s); break;
+    case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, tuning().agg_nt != 0, a, bound, s); break;
+    case 2: ok = dispatch_lpe<2>(lpe, nv, xm, wm, tuning().agg_nt != 0, a, bound, s); break;
+    default: ok = dispatch_lpe<1>(lpe, nv, xm, wm, tuning().agg_nt != 0, a, bound, s); break;
   }
   if (!ok) return fail(GTA_ERR_UNSUPPORTED, "aggregate: no kernel variant");
   GTA_LAUNCHED("k_aggregate");
@@ -2553,7 +2690,7 @@ int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indic
   GTA_HIP(hipMemsetAsync(v.lhist, 0, 64 * kLenBins * 4, s));
   k_blocked_items<<<gk, dim3(256), 0, s>>>(indptr, n_rows, B, item_edges, row_edges, v);
   GTA_LAUNCHED("k_blocked_items");
-  if (g_plan_len_sort && mi > 0) {
+  if (tuning().plan_len_sort && mi > 0) {
     k_items_len_scan<<<1, 64, 0, s>>>(v, n_rows, B);
     GTA_LAUNCHED("k_items_len_scan");
     k_items_permute<<<dim3(static_cast<unsigned>((mi + 255) / 256)), dim3(256), 0, s>>>(v, n_rows, B);
@@ -2563,11 +2700,15 @@ int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indic
   return GTA_OK;
 }
 
+// workspace of gta_aggregate_blocked: [arrival counters, one int32 per row, padded to 256 B][slab rows]
+inline int64_t blocked_cnt_bytes(int64_t n_rows) { return (n_rows * 4 + 255) / 256 * 256; }
+
 int64_t gta_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t F,
                                               int64_t item_edges) {
   if (n_rows < 0 || nnz < 0 || blocks < 1 || blocks > 63 || F <= 0 || item_edges < 1)
     return fail(GTA_ERR_ARG, "blocked_workspace_bytes: bad sizes");
-  return blocked_max_items(n_rows, nnz, static_cast<int>(blocks), item_edges) * F * static_cast<int64_t>(sizeof(float));
+  return blocked_cnt_bytes(n_rows) +
+         blocked_max_items(n_rows, nnz, static_cast<int>(blocks), item_edges) * F * static_cast<int64_t>(sizeof(float));
 }
 
 int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols, int64_t nnz,
@@ -2599,14 +2740,15 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
   hipStream_t s = S(stream);
   if (workspace) {  // single launch into per-item slab rows + ordered reduce
     const RowItems ri{v.row_ptr, v.row_items};
-    float* slabs = static_cast<float*>(workspace);
+    int32_t* cnt = static_cast<int32_t*>(workspace);
+    float* slabs = reinterpret_cast<float*>(static_cast<char*>(workspace) + blocked_cnt_bytes(n_rows));
     const int64_t items = mi;  // grid bound; the kernels stop at the plan's n_items
     const int64_t* nit = &v.hdr[4];
     const SegItem* its = v.items;
     const dim3 g2(static_cast<unsigned>((items + kWavesPerBlock - 1) / kWavesPerBlock)), blk2(kBlock);
     const int vq = static_cast<int>(F / 16);
     const int lph = w ? static_cast<int>((F / heads) / vq) : 0;
-    const bool quarter = g_seg_quarter && (vq == 4 || vq == 8 || vq == 16) && ldx % 4 == 0 && aligned(x, 16) &&
+    const bool quarter = tuning().seg_quarter && (vq == 4 || vq == 8 || vq == 16) && ldx % 4 == 0 && aligned(x, 16) &&
                          (!w || ((F / heads) % vq == 0 && lph >= 1 && 16 % lph == 0));
     if (items == 0) {
       // no edges: no items; the reduce below writes the (empty) rows
@@ -2618,31 +2760,45 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
 #define GTA_SEG4NT(VW_, U_, NT_)                                                                             \
   if (w) k_agg_seg4<VW_, U_, true, NT_><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its); \
   else k_agg_seg4<VW_, U_, false, NT_><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its)
-      if (vq == 8 && g_seg_lanes == 32) {  // half-wave items: 32 lanes x float4
+      if (vq == 8 && tuning().seg_lanes == 32) {  // half-wave items: 32 lanes x float4
         const int lph32 = w ? static_cast<int>((F / heads) / 4) : 0;
         const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
-        const bool lean = g_seg_lean && g_seg_u == 8 && n_cols < (1 << 24) &&
+        const bool lean = tuning().seg_lean && tuning().seg_u == 8 && n_cols < (1 << 24) &&
                           static_cast<uint64_t>(n_cols) * static_cast<uint64_t>(ldx) * 4u < (1ull << 32) &&
-                          (!w || lph32 == 4 || (heads == 1 && g_seg_lean_w1 && ldw < (int64_t(1) << 24)));
+                          (!w || lph32 == 4 || (heads == 1 && tuning().seg_lean_w1 && ldw < (int64_t(1) << 24)));
         const uint32_t rb = static_cast<uint32_t>(ldx * 4);
+        const bool fuse = lean && tuning().seg_fuse && static_cast<uint64_t>(mi) * F * 4u < (1ull << 32);
+        if (fuse) {  // in-launch ordered reduce: no k_seg_reduce pass
+          const FuseArgs fa{v.row_ptr, v.row_items, cnt, row_scale, y, ldy, accumulate,
+                            static_cast<uint32_t>(mi * F * 4)};
+          k_fuse_prep<<<dim3(static_cast<unsigned>((n_rows + kBlock - 1) / kBlock)), blk2, 0, s>>>(n_rows, 128, fa);
+          GTA_LAUNCHED("k_fuse_prep");
+          if (w && heads == 1) k_agg_h32<true, 2, true, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its, fa);
+          else if (!w) k_agg_h32<false, 2, false, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its, fa);
+          else if (tuning().seg_fuse == 2)
+            k_agg_h32<true, 2, false, true, 6><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its, fa);
+          else k_agg_h32<true, 2, false, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its, fa);
+          GTA_LAUNCHED("k_agg_h32 (fused reduce)");
+          return GTA_OK;
+        }
         if (lean) {
           if (w && heads == 1) k_agg_h32<true, 2, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (!w && g_seg_nt == 2) k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (!w && tuning().seg_nt == 2) k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
           else if (!w) k_agg_h32<false, 0><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (g_seg_nt == 2) k_agg_h32<true, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (g_seg_nt == 1) k_agg_h32<true, 1><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (tuning().seg_nt == 2) k_agg_h32<true, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (tuning().seg_nt == 1) k_agg_h32<true, 1><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
           else k_agg_h32<true, 0><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
         } else if (w && lph32 >= 1 && 32 % lph32 == 0 && (F / heads) % 4 == 0) {
-          if (g_seg_u == 4)
+          if (tuning().seg_u == 4)
             k_agg_seg4<4, 4, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                          lph32, slabs, its);
-          else if (g_seg_u == 16)
+          else if (tuning().seg_u == 16)
             k_agg_seg4<4, 16, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                           lph32, slabs, its);
-          else if (g_seg_nt == 1)
+          else if (tuning().seg_nt == 1)
             k_agg_seg4<4, 8, true, 1, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                          lph32, slabs, its);
-          else if (g_seg_nt == 2)
+          else if (tuning().seg_nt == 2)
             k_agg_seg4<4, 8, true, 2, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                          lph32, slabs, its);
           else
@@ -2656,9 +2812,9 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
           return fail(GTA_ERR_UNSUPPORTED, "aggregate_blocked: half-wave head layout");
       } else if (vq == 4) { GTA_SEG4(4, 4); }
       else if (vq == 8) {
-        if (g_seg_u == 2) { GTA_SEG4(8, 2); } else if (g_seg_u == 4) { GTA_SEG4(8, 4); }
-        else if (g_seg_nt == 1) { GTA_SEG4NT(8, 8, 1); } else if (g_seg_nt == 2) { GTA_SEG4NT(8, 8, 2); }
-        else if (g_seg_nt == 3) { GTA_SEG4NT(8, 8, 3); } else { GTA_SEG4(8, 8); }
+        if (tuning().seg_u == 2) { GTA_SEG4(8, 2); } else if (tuning().seg_u == 4) { GTA_SEG4(8, 4); }
+        else if (tuning().seg_nt == 1) { GTA_SEG4NT(8, 8, 1); } else if (tuning().seg_nt == 2) { GTA_SEG4NT(8, 8, 2); }
+        else if (tuning().seg_nt == 3) { GTA_SEG4NT(8, 8, 3); } else { GTA_SEG4(8, 8); }
       }
       else { GTA_SEG4(16, 2); }
 #undef GTA_SEG4
@@ -2687,7 +2843,7 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
   }
   if (!gl_ok) return fail(GTA_ERR_UNSUPPORTED, gl_msg);
   // persistent waves: enough for 8 per SIMD on every CU, never more than one per row
-  const int64_t waves = std::min<int64_t>(n_rows, g_seg_waves > 0 ? g_seg_waves : 256 * 32);
+  const int64_t waves = std::min<int64_t>(n_rows, tuning().seg_waves > 0 ? tuning().seg_waves : 256 * 32);
   const dim3 grid(static_cast<unsigned>((waves + kWavesPerBlock - 1) / kWavesPerBlock)), blk(kBlock);
   for (int b = 0; b < B; ++b) {
     SegView sv{v.perm, v.seg, B, b};
@@ -2752,7 +2908,7 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
   else k_agg_seg4<VW_, U_, false, 0, true><<<g4, blk, 0, s>>>(indices, nit, x, ldx, nullptr, 0, lph, slabs, \
                                                              it, att)
   const int lph32 = static_cast<int>((F / heads) / 4);
-  const bool lean = g_att_lean && elr && F == 128 && heads == 8 && g_seg_lanes == 32 && n_cols < (1 << 24) &&
+  const bool lean = tuning().att_lean && elr && F == 128 && heads == 8 && tuning().seg_lanes == 32 && n_cols < (1 << 24) &&
                     static_cast<uint64_t>(n_cols) * static_cast<uint64_t>(ldx) * 4u < (1ull << 32) &&
                     static_cast<uint64_t>(n_cols) * static_cast<uint64_t>(ldb) * 4u < (1ull << 32);
   if (lean) {
@@ -2760,16 +2916,16 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
     const uint32_t rb = static_cast<uint32_t>(ldx * 4), bbytes = static_cast<uint32_t>(ldb * 4);
     // single-item rows are common only when few blocks cut the rows (low degree, B <= 2); above
     // that the row_ptr reads at every item's end cost more than the rare direct writes save
-    const bool direct = (g_att_direct == 2 || (g_att_direct == 1 && B <= 2)) && ldy % 4 == 0 && aligned(y, 16);
+    const bool direct = (tuning().att_direct == 2 || (tuning().att_direct == 1 && B <= 2)) && ldy % 4 == 0 && aligned(y, 16);
     skip_single = direct;
     const int64_t* rp = direct ? v.row_ptr : nullptr;
-    if (g_att_lean == 2)
+    if (tuning().att_lean == 2)
       k_att_h32<2><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it, rp, normalize, y,
                                        ldy, sums);
     else
       k_att_h32<0><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it, rp, normalize, y,
                                        ldy, sums);
-  } else if (F == 128 && g_seg_lanes == 32 && (F / heads) % 4 == 0 && lph32 >= 1 && 32 % lph32 == 0) {
+  } else if (F == 128 && tuning().seg_lanes == 32 && (F / heads) % 4 == 0 && lph32 >= 1 && 32 % lph32 == 0) {
     const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
     if (elr) k_agg_seg4<4, 8, false, 0, true, GTA_SF_EXP_LEAKY_RELU, 32><<<g2h, blk, 0, s>>>(
         indices, nit, x, ldx, nullptr, 0, lph32, slabs, it, att);
@@ -2850,7 +3006,7 @@ int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indice
   if (n_rows == 0 || nnz == 0) return GTA_OK;
   const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
   const int fo = static_cast<int>(Fo), ga = static_cast<int>(Fo / Fa), gb = b ? static_cast<int>(Fo / Fb) : 1;
-  if (g_apply_edge_form == 0) {
+  if (tuning().apply_edge_form == 0) {
     k_apply_edge<<<grid, dim3(kBlock), 0, S(stream)>>>(bin, sf, indptr, indices, n_rows, a, a_mode, lda,
                                                        static_cast<int>(Fa), b, b_mode, ldb, static_cast<int>(Fb),
                                                        out, ldo, fo);
@@ -2888,7 +3044,7 @@ int gta_apply_node(int bin, int sf, int64_t n, const float* a, int64_t lda, int6
   if (n == 0) return GTA_OK;
   const int64_t total = n * Fo;
   const int bm = !b ? 0 : (Fb == Fo ? 1 : (Fb == 1 ? 2 : -1));
-  if (g_apply_node_vec && bm >= 0 && Fa == Fo && Fo % 4 == 0 && total / 4 < (int64_t(1) << 32) && lda % 4 == 0 &&
+  if (tuning().apply_node_vec && bm >= 0 && Fa == Fo && Fo % 4 == 0 && total / 4 < (int64_t(1) << 32) && lda % 4 == 0 &&
       ldo % 4 == 0 && aligned(a, 16) && aligned(out, 16) && (bm != 1 || (ldb % 4 == 0 && aligned(b, 16)))) {
     const uint32_t n4 = static_cast<uint32_t>(total / 4), F4 = static_cast<uint32_t>(Fo / 4);
     const dim3 g(static_cast<unsigned>(std::min<int64_t>((n4 + kBlock - 1) / kBlock, 256 * 16))), blk(kBlock);
@@ -2915,13 +3071,13 @@ int gta_edge_softmax(const int64_t* indptr, const int32_t* indices, int64_t n_ro
   if (lda < heads || ldb < heads) return fail(GTA_ERR_ARG, "edge_softmax: leading dimension < heads");
   if (n_rows == 0) return GTA_OK;
   const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
-  const bool vec = g_esm_lane && (heads == 4 || heads == 8 || heads == 16) && ldb % 4 == 0 && aligned(b_src, 16) &&
+  const bool vec = tuning().esm_lane && (heads == 4 || heads == 8 || heads == 16) && ldb % 4 == 0 && aligned(b_src, 16) &&
                    (nnz == 0 || aligned(out, 16));
   if (vec) {
 #define GTA_ESMV(H_, K_)                                                                                          \
   k_edge_softmax_v<H_, K_><<<grid, dim3(kBlock), 0, S(stream)>>>(indptr, indices, n_rows, a_dst, lda, b_src, ldb, \
                                                                  sf, normalize, out, sums)
-    const bool k4 = g_esm_keep >= 4 && heads <= 8;
+    const bool k4 = tuning().esm_keep >= 4 && heads <= 8;
     if (heads == 4) { if (k4) GTA_ESMV(4, 4); else GTA_ESMV(4, 2); }
     else if (heads == 8) { if (k4) GTA_ESMV(8, 4); else GTA_ESMV(8, 2); }
     else GTA_ESMV(16, 2);
@@ -2970,7 +3126,7 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
   return GTA_OK;
 }
 
-// Plain fp32 UPDATE (no row gather, no SF epilogue, M >= g_mm_blaslt_min_m; the row-streaming and
+// Plain fp32 UPDATE (no row gather, no SF epilogue, M >= tuning().mm_blaslt_min_m; the row-streaming and
 // split-K entry points) on hipBLASLt, the
 // vendor's tuned fp32 MFMA GEMM: measured faster than k_mm_rows on the layer shapes (Reddit
 // x.W 602 -> 128: 0.37 vs 0.58 ms; Flickr 500 -> 128: 0.12 vs 0.145 ms;
@@ -3030,7 +3186,7 @@ bool blaslt_f32(const float* x, int64_t ldx, int64_t M, int64_t K, const float* 
            hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
                                                  sizeof(wsb)) == HIPBLAS_STATUS_SUCCESS &&
            hipblasLtMatmulAlgoGetHeuristic(h->second.first, sh.md, sh.la, sh.lb, sh.lc, sh.lc, pref,
-                                           g_mm_blaslt_tune ? kBlasLtCandidates : 1, res, &nres) ==
+                                           tuning().mm_blaslt_tune ? kBlasLtCandidates : 1, res, &nres) ==
                HIPBLAS_STATUS_SUCCESS &&
            nres > 0 && res[0].state == HIPBLAS_STATUS_SUCCESS;
       if (pref) hipblasLtMatmulPreferenceDestroy(pref);
@@ -3096,30 +3252,30 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   if (K > INT32_MAX || N > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t: K/N too large");
   if (dtype != GTA_F32 && dtype != GTA_BF16 && dtype != GTA_F32_BF16) return fail(GTA_ERR_ARG, "update_mm_t: bad dtype");
   if (M == 0) return GTA_OK;
-  if (g_mm_blaslt && dtype == GTA_F32 && !row_idx && sf == GTA_SF_NONE && M >= g_mm_blaslt_min_m &&
+  if (tuning().mm_blaslt && dtype == GTA_F32 && !row_idx && sf == GTA_SF_NONE && M >= tuning().mm_blaslt_min_m &&
       blaslt_f32(static_cast<const float*>(x), ldx, M, K, static_cast<const float*>(wt), ldwt, N, out, ldo, S(stream))) {
     GTA_LAUNCHED("hipblaslt_matmul");
     return GTA_OK;
   }
   const int nt = N <= 16 ? 1 : N <= 32 ? 2 : N <= 64 ? 4 : 8;
   const int64_t groups = (M + 127) / 128;
-  const int64_t per_cu = g_mm_blocks_per_cu > 0 ? g_mm_blocks_per_cu : 8;
+  const int64_t per_cu = tuning().mm_blocks_per_cu > 0 ? tuning().mm_blocks_per_cu : 8;
   const int kc = (dtype == GTA_F32) ? (nt >= 8 ? 64 : 128) : (nt >= 8 ? 128 : 256);  // k_mm_rows KC
   const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
   const int64_t cap = (K <= kc) ? std::max<int64_t>(1, 256 * per_cu / ncb) : groups;  // W staged once: persistent
   const dim3 gr(static_cast<unsigned>(std::min<int64_t>(groups, cap) * ncb));
   // prefetch the next A fragment: measured 1.2x on fp32 (K = 602) and bf16 K = 128, and 1.1x on the
   // mixed path with a K tail since fp32 A loads are float4 pieces (GIN K = 100: 0.70 -> 0.64 ms,
-  // profiles/r01_mm_bench_2.json); bf16 x with a K tail stays without; g_mm_prefetch 2 = always, 0 = never
-  const bool pf = g_mm_prefetch == 2 || (g_mm_prefetch == 1 && (dtype != GTA_BF16 || K % 32 == 0));
+  // profiles/r01_mm_bench_2.json); bf16 x with a K tail stays without; tuning().mm_prefetch 2 = always, 0 = never
+  const bool pf = tuning().mm_prefetch == 2 || (tuning().mm_prefetch == 1 && (dtype != GTA_BF16 || K % 32 == 0));
 #define GTA_MMR(TA_, WT_, NT_)                                                                                \
   if (pf) k_mm_rows<TA_, WT_, NT_, true><<<gr, dim3(kBlock), 0, S(stream)>>>(                        \
       static_cast<const TA_*>(x), ldx, row_idx, M, static_cast<int>(K), static_cast<const WT_*>(wt), ldwt,        \
-      static_cast<int>(N), sf, out, ldo, 0, 0, g_mm_vstore);                                                      \
+      static_cast<int>(N), sf, out, ldo, 0, 0, tuning().mm_vstore);                                                      \
   else k_mm_rows<TA_, WT_, NT_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const TA_*>(x), ldx, row_idx, M, \
                                                                     static_cast<int>(K), static_cast<const WT_*>(wt), \
                                                                     ldwt, static_cast<int>(N), sf, out, ldo, 0, 0,  \
-                                                                    g_mm_vstore)
+                                                                    tuning().mm_vstore)
 #define GTA_MMR_NT(TA_, WT_) \
   if (nt == 1) GTA_MMR(TA_, WT_, 1); else if (nt == 2) GTA_MMR(TA_, WT_, 2); else if (nt == 4) GTA_MMR(TA_, WT_, 4); else GTA_MMR(TA_, WT_, 8)
   if (dtype == GTA_F32) { GTA_MMR_NT(float, float); }
@@ -3155,7 +3311,7 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
     return fail(GTA_ERR_ARG, "update_mm_t_split: workspace too small");
   if (nsl > 65535) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t_split: too many slices");
   float* ws = static_cast<float*>(workspace);
-  if (g_mm_blaslt && dtype == GTA_F32 && !row_idx && sf == GTA_SF_NONE && M >= g_mm_blaslt_min_m &&
+  if (tuning().mm_blaslt && dtype == GTA_F32 && !row_idx && sf == GTA_SF_NONE && M >= tuning().mm_blaslt_min_m &&
       blaslt_f32(static_cast<const float*>(x), ldx, M, K, static_cast<const float*>(wt), ldwt, N, out, ldo, S(stream))) {
     GTA_LAUNCHED("hipblaslt_matmul");
     return GTA_OK;
@@ -3164,14 +3320,14 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
   const int64_t groups = (M + 127) / 128;
   const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
   const dim3 gr(static_cast<unsigned>(groups * ncb), static_cast<unsigned>(nsl));
-  const bool pf = g_mm_prefetch == 2 || (g_mm_prefetch == 1 && (dtype != GTA_BF16 || ks % 32 == 0));
+  const bool pf = tuning().mm_prefetch == 2 || (tuning().mm_prefetch == 1 && (dtype != GTA_BF16 || ks % 32 == 0));
   const int ki = static_cast<int>(K);
   hipStream_t s = S(stream);
 #define GTA_MMS(TA_, WT_, NT_)                                                                                    \
   if (pf) k_mm_rows<TA_, WT_, NT_, true><<<gr, dim3(kBlock), 0, s>>>(static_cast<const TA_*>(x), ldx, row_idx, M, ki, \
-      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N, g_mm_vstore);                                 \
+      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N, tuning().mm_vstore);                                 \
   else k_mm_rows<TA_, WT_, NT_><<<gr, dim3(kBlock), 0, s>>>(static_cast<const TA_*>(x), ldx, row_idx, M, ki,          \
-      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N, g_mm_vstore)
+      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N, tuning().mm_vstore)
 #define GTA_MMS_NT(TA_, WT_) \
   if (nt == 1) GTA_MMS(TA_, WT_, 1); else if (nt == 2) GTA_MMS(TA_, WT_, 2); else if (nt == 4) GTA_MMS(TA_, WT_, 4); else GTA_MMS(TA_, WT_, 8)
   if (dtype == GTA_F32) { GTA_MMS_NT(float, float); }

@@ -491,4 +491,13 @@ def tile_nnz(graph, T):
 
 
 def set_debug(key, value):
+    """Set a tuning knob of libgta for the CALLING thread (include/gta.h: gta_debug_set)."""
     check(_L().gta_debug_set(key.encode(), int(value)), "debug_set")
+
+
+def get_debug(key):
+    """The calling thread's value of a libgta tuning knob."""
+    import ctypes
+    v = ctypes.c_int64(0)
+    check(_L().gta_debug_get(key.encode(), ctypes.byref(v)), "debug_get")
+    return int(v.value)

@@ -37,7 +37,8 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 2  /* 2: blocked plans of bounded items (nnz, item_edges) */
+#define GTA_ABI_VERSION 3  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+                              hooks, blocked workspace holds per-row arrival counters */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -70,6 +71,13 @@ enum { GTA_SF_NONE = 0, GTA_SF_RELU = 1, GTA_SF_EXP_LEAKY_RELU = 2 /* exp(leaky_
 
 int gta_abi_version(void);
 const char* gta_last_error(void);
+
+/* Tuning hooks (benchmarks and kernel-form tests): named knobs that pick a kernel variant
+ * (DESIGN.md §3.1 lists them).  They are per calling THREAD -- a knob set on one thread never
+ * changes another thread's concurrent calls -- and every entry point reads its own thread's
+ * values, so the library keeps no process-wide mutable state.  Unknown key: GTA_ERR_ARG. */
+int gta_debug_set(const char* key, int64_t value);
+int gta_debug_get(const char* key, int64_t* value);
 
 /* ---- K1 SCATTER (node -> edge copy) -------------------------------------
  * out[e, :] = x[dir==R ? dst(e) : src(e), :]          (bit-exact copy)

@@ -53,3 +53,27 @@ def test_product_path_refuses_cpu_tensors():
     g = G.synthetic(20, 60, seed=0)
     with pytest.raises(_lib.GTAError):
         ops.aggregate(g, torch.zeros(20, 4), "src")
+
+
+def test_tuning_knobs_are_per_thread(lib):
+    """ADVICE/VERDICT r1: the tuning knobs are the calling thread's (no process-wide mutable state):
+    a knob set on one thread is not seen by another thread's calls."""
+    import threading
+
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
+    base = ops.get_debug("seg_lean")
+    seen = {}
+
+    def other():
+        ops.set_debug("seg_lean", 1 - base)
+        seen["other"] = ops.get_debug("seg_lean")
+
+    t = threading.Thread(target=other)
+    t.start()
+    t.join()
+    assert seen["other"] == 1 - base
+    assert ops.get_debug("seg_lean") == base
+    with pytest.raises(_lib.GTAError):
+        ops.set_debug("no_such_knob", 1)
+    with pytest.raises(_lib.GTAError):
+        ops.get_debug("no_such_knob")

@@ -393,7 +393,7 @@ def test_edge_softmax_other_sf_and_errors(dev):
 
 @pytest.mark.parametrize("knobs", [{"seg_quarter": 0}, {"seg_u": 2}, {"seg_u": 4}, {"seg_nt": 3}, {"seg_lanes": 16},
                                    {"seg_lanes": 16, "seg_u": 4}, {"seg_lean": 0}, {"seg_nt": 0}, {"seg_nt": 1},
-                                   {"seg_lean_w1": 0}])
+                                   {"seg_lean_w1": 0}, {"seg_fuse": 0}, {"seg_fuse": 2}])
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 0), (64, 4), (256, 16), (128, 1)])
 def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     """Every form of the blocked kernel (one item per wave, quarter-wave with 2/4/8 edges per
@@ -405,7 +405,8 @@ def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
     w = torch.from_numpy(rng.random((g.nnz, heads)).astype(np.float32)).to(dev) if heads else None
     y0 = ops.aggregate_blocked(g, x, w, blocks=8)
-    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 2, "seg_lanes": 32, "seg_lean": 1, "seg_lean_w1": 1}
+    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 2, "seg_lanes": 32, "seg_lean": 1, "seg_lean_w1": 1,
+                "seg_fuse": 0}
     try:
         for k, v in knobs.items():
             ops.set_debug(k, v)
@@ -743,3 +744,46 @@ def test_blocked_plan_length_sort_bitwise(dev, blocks, item_edges, heads):
         ops.set_debug("plan_len_sort", 1)
     assert torch.equal(outs[0][0], outs[1][0])
     assert torch.equal(outs[0][1][0], outs[1][1][0]) and torch.equal(outs[0][1][1], outs[1][1][1])
+
+
+@pytest.mark.parametrize("heads", [8, 1, 0])
+@pytest.mark.parametrize("accumulate", [False, True])
+def test_aggregate_blocked_fused_reduce_bitwise(dev, heads, accumulate):
+    """The in-launch ordered reduce (last-arriving item of a row sums its partials, seg_fuse=1 / 2)
+    == the two-launch form (k_seg_reduce, seg_fuse=0, the default) bitwise, on rows of every kind:
+    empty (scale inf: 0 * inf = NaN in both), one item (written directly), many blocks, and rows
+    split into several parts per block (item_edges 16); with row_scale and accumulate."""
+    n = 700
+    rng = np.random.default_rng(11 + heads)
+    deg = rng.integers(0, 6, n)
+    deg[::7] = 0
+    deg[3::50] = rng.integers(300, 1500, len(deg[3::50]))
+    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    ix = np.concatenate([np.sort(rng.choice(n, d, replace=d > n)) for d in deg]).astype(np.int32)
+    g = G.from_numpy(ip, ix).to(dev)
+    x = torch.from_numpy(rng.standard_normal((n, 128)).astype(np.float32)).to(dev)
+    w = torch.from_numpy(rng.random((g.nnz, heads)).astype(np.float32)).to(dev) if heads else None
+    scale = torch.from_numpy(np.where(deg > 0, 1.0 / np.maximum(deg, 1), np.inf).astype(np.float32)).to(dev)
+    y_init = torch.from_numpy(rng.standard_normal((n, 128)).astype(np.float32)).to(dev)
+    plan = ops.BlockedPlan(g, blocks=6, item_edges=16)
+    outs = []
+    for fuse in (0, 1, 2):
+        ops.set_debug("seg_fuse", fuse)
+        try:
+            y = y_init.clone()
+            outs.append(ops.aggregate_blocked(g, x, w, row_scale=scale, out=y, accumulate=accumulate, plan=plan))
+        finally:
+            ops.set_debug("seg_fuse", 0)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(torch.nan_to_num(o, nan=7.0), torch.nan_to_num(outs[0], nan=7.0))
+        assert torch.equal(torch.isnan(o), torch.isnan(outs[0]))
+    xn, wn = x.cpu().numpy(), None if w is None else w.cpu().numpy()
+    ref = isa_ref.aggregate(ip, ix, xn, "src", wn) * np.where(deg > 0, 1.0 / np.maximum(deg, 1), 0)[:, None]
+    if accumulate:
+        ref = ref + y_init.cpu().numpy()
+    has = deg > 0
+    bound = 1e-5 * isa_ref.aggregate_abs(ip, ix, xn, "src", wn) + 1e-6 + (1e-6 * np.abs(ref) if accumulate else 0)
+    err = np.abs(outs[1].cpu().numpy().astype(np.float64) - ref)
+    assert np.all(err[has] <= bound[has])
+    assert torch.isnan(outs[1][torch.from_numpy(~has).to(dev)]).all()  # 0 * inf, as the reduce pass gives
