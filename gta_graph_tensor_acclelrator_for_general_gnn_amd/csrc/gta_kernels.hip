@@ -2331,6 +2331,236 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
   }
 }
 
+// fp32 UPDATE on MFMA with an LDS-DMA ring (the plain fp32 GEMM of GCN/GAT/SAGE layers,
+// `template/ISA_defination.yaml:1-31` j,ij->i; LOAD_W `code/interpreter.py:335-343`).
+// Why not k_mm_rows: there each K chunk of W is staged synchronously (stage, barrier, compute)
+// and A fragments are loaded one 16-k step ahead, so at 4 waves per SIMD the MFMA pipe waits on
+// HBM latency (61 TF/s of 157 at K = 602).  Here both operands go global -> LDS by
+// global_load_lds (no VGPR staging), three 16-k stages deep, so every stage has two MFMA steps
+// of other stages (>= 4k cycles per SIMD) to land:
+//   block = 4 waves = 128 rows x BN = 16*NT columns; per 16-k stage wave w DMAs its own two
+//   16-row A fragments (lane L = 16g + r holds x[row r][k0 + 4g .. +3], exactly the lane's MFMA
+//   fragment, so the ds_read is lane-linear: conflict-free) and NT/4 of the block's NT
+//   B fragments (W^T rows, same layout);
+//   per stage: counted s_waitcnt vmcnt (this wave's stage landed; the next stays in flight),
+//   lgkmcnt(0) (this wave's reads of the slot about to be refilled are done), raw s_barrier (every
+//   wave's DMA of the stage landed, every wave done with the old slot), then the DMA of stage
+//   s + 2 and the 16-k MFMA step of stage s (2 x NT x 4 v_mfma_f32_16x16x4_f32).
+// A K tail (K % 16) is one last step from registers with masked loads.  Rows past M and columns
+// past N read clamped rows and are not stored.  Same per-lane k order and fma chain as
+// k_mm_rows: results bitwise equal to it.  LDS: 3 x (8 + NT) KiB (48 KiB at N = 128: 3 blocks/CU).
+// generic -> LDS address space, and the 32-bit LDS byte address (macros: a __device__ helper
+// taking or returning address-space-3 pointers keeps hipcc from emitting a template kernel's host stub)
+#define GTA_TO_LDS(p) ((__attribute__((address_space(3))) void*)(p))
+#define GTA_LDS_ADDR(p) static_cast<uint32_t>(reinterpret_cast<uintptr_t>(GTA_TO_LDS(p)))
+template <int OFF>
+__device__ __forceinline__ void ds_read16(f32x4& v, uint32_t a) {  // result valid after an lgkmcnt wait
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
+}
+__device__ __forceinline__ void ds_read16_dyn(f32x4& v, uint32_t a, int c) {  // c: 1 KiB fragment index (unrolled)
+  switch (c) {
+    case 0: ds_read16<0>(v, a); break;
+    case 1: ds_read16<1024>(v, a); break;
+    case 2: ds_read16<2048>(v, a); break;
+    case 3: ds_read16<3072>(v, a); break;
+    case 4: ds_read16<4096>(v, a); break;
+    case 5: ds_read16<5120>(v, a); break;
+    case 6: ds_read16<6144>(v, a); break;
+    default: ds_read16<7168>(v, a); break;
+  }
+}
+
+template <int NT, bool A4 = false>  // A4: x rows not 16-B aligned (e.g. K = 602): A DMA'd in 4-B pieces
+__global__ void __launch_bounds__(kBlock, 3)  // 3 waves per SIMD = 3 blocks per CU (the LDS bound)
+k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
+          const float* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
+          int vec_store) {
+  static_assert(NT == 4 || NT == 8, "B fragments split evenly over the 4 waves");
+  constexpr int KS = 16, D = 3, BN = 16 * NT;
+  constexpr int A_BYTES = 4 * 2 * 1024, STAGE = A_BYTES + NT * 1024;
+  constexpr int PER_STAGE = (A4 ? 8 : 2) + NT / 4;  // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char lds[D * STAGE];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = wave_id_uniform();
+  const int g = lane >> 4, r16 = lane & 15;
+  const int ncb = (N + BN - 1) / BN;
+  const int n0 = static_cast<int>(blockIdx.x % ncb) * BN;
+  // persistent: this block's 128-row groups are grp0, grp0 + gstep, ...; the ring runs on across
+  // them (stage t = (group j, 16-k step s)), so the next group's first stages land while this
+  // group finishes and no block pays a prologue after the first
+  const int64_t grp0 = blockIdx.x / ncb, gstep = gridDim.x / ncb;
+  const int64_t n_groups = (M + 127) / 128;
+  const int64_t my_groups = grp0 < n_groups ? (n_groups - grp0 + gstep - 1) / gstep : 0;
+  const int S = K / KS;  // whole 16-k stages per group (a K tail is one register step)
+  const int64_t T = my_groups * S;
+  const float* bsrc[NT / 4];
+#pragma unroll
+  for (int t = 0; t < NT / 4; ++t) {
+    const int n = min(n0 + 16 * (wv * (NT / 4) + t) + r16, N - 1);
+    bsrc[t] = wt + static_cast<int64_t>(n) * ldwt + 4 * g;
+  }
+  // A source rows of group j: A4: a 4-B DMA instruction p fills reader lanes 16p .. 16p + 15 of
+  // the fragment image, so DMA lane L loads x[row L/4][k0 + 4p + L%4]; 16-B form: lane (g, r16)
+  // loads x[row r16][k0 + 4g .. +3], its own MFMA fragment
+  auto a_row = [&](int64_t j, int i, int sub) __attribute__((always_inline)) -> const float* {
+    const int64_t m = min<int64_t>((grp0 + j * gstep) * 128 + wv * 32 + 16 * i + sub, M - 1);
+    return x + (row_idx ? static_cast<int64_t>(row_idx[m]) : m) * ldx;
+  };
+  const float* asrc[2];
+  int64_t asrc_j = -1;
+  auto issue = [&](int64_t t) __attribute__((always_inline)) {
+    const int64_t j = t / S;
+    const int k = static_cast<int>(t - j * S) * KS;
+    if (j != asrc_j) {
+#pragma unroll
+      for (int i = 0; i < 2; ++i) asrc[i] = a_row(j, i, A4 ? lane >> 2 : r16) + (A4 ? (lane & 3) : 4 * g);
+      asrc_j = j;
+    }
+    char* base = lds + (t % D) * STAGE;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      if constexpr (A4) {
+#pragma unroll
+        for (int p = 0; p < 4; ++p)
+          __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[i] + k + 4 * p),
+                                           GTA_TO_LDS(base + (wv * 2 + i) * 1024 + p * 256), 4, 0, 0);
+      } else {
+        __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[i] + k), GTA_TO_LDS(base + (wv * 2 + i) * 1024), 16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NT / 4; ++q)
+      __builtin_amdgcn_global_load_lds(const_cast<float*>(bsrc[q] + k),  // (a const source fails the host pass)
+                                       GTA_TO_LDS(base + A_BYTES + (wv * (NT / 4) + q) * 1024), 16, 0, 0);
+  };
+  f32x4 acc[2][NT];
+  auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int c = 0; c < NT; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  auto mma = [&](const float (&av)[2][4], const float4& b4, int c) {
+    const float bj[4] = {b4.x, b4.y, b4.z, b4.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][j], bj[j], acc[i][c], 0, 0, 0);
+  };
+  const bool vstore = vec_store && ldo % 4 == 0 && aligned(out, 16);
+  auto epilogue = [&](int64_t j) __attribute__((always_inline)) {
+    const int64_t mw = (grp0 + j * gstep) * 128 + wv * 32;
+    if (vstore) {  // quad-transposed 16-B row stores (k_mm_rows' epilogue)
+      const int p = r16 & 3, q = r16 >> 2;
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int c = 0; c < NT; ++c) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = sf_apply(sf, acc[i][c][r]);
+#pragma unroll
+          for (int m2 = 0; m2 < 2; ++m2) {
+            const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
+            const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2 + 1]), 0xB1, 0xF, 0xF, false));
+            if (p & 1) v[2 * m2] = sb; else v[2 * m2 + 1] = sa;
+          }
+#pragma unroll
+          for (int m2 = 0; m2 < 2; ++m2) {
+            const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2]), 0x4E, 0xF, 0xF, false));
+            const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2 + 2]), 0x4E, 0xF, 0xF, false));
+            if (p & 2) v[m2] = sb; else v[m2 + 2] = sa;
+          }
+          const int64_t m = mw + 16 * i + 4 * g + p;
+          const int n = n0 + 16 * c + 4 * q;
+          if (m < M) {
+            if (n + 3 < N) {
+              *reinterpret_cast<float4*>(out + m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (n + r < N) out[m * ldo + n + r] = v[r];
+            }
+          }
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int c = 0; c < NT; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t m = mw + 16 * i + 4 * g + r;
+            const int n = n0 + 16 * c + r16;
+            if (m < M && n < N) out[m * ldo + n] = sf_apply(sf, acc[i][c][r]);
+          }
+    }
+  };
+  auto tail = [&](int64_t j) __attribute__((always_inline)) {  // the K tail from registers: k = S*16 + 4g + j < K, zeros past it
+    const int k0 = S * KS + 4 * g;
+    auto ld4 = [&](const float* p) __attribute__((always_inline)) {  // p = row + k0
+      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (k0 < K) v.x = p[0];
+      if (k0 + 1 < K) v.y = p[1];
+      if (k0 + 2 < K) v.z = p[2];
+      if (k0 + 3 < K) v.w = p[3];
+      return v;
+    };
+    float av[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const float4 a4 = ld4(a_row(j, i, r16) + k0);
+      av[i][0] = a4.x; av[i][1] = a4.y; av[i][2] = a4.z; av[i][3] = a4.w;
+    }
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      const int n = min(n0 + 16 * c + r16, N - 1);
+      mma(av, ld4(wt + static_cast<int64_t>(n) * ldwt + k0), c);
+    }
+  };
+  zero_acc();  // (the host sends K >= 32: every group has stages)
+  if (T > 0) issue(0);
+  if (T > 1) issue(1);
+  int64_t t = 0;
+  for (int64_t j = 0; j < my_groups; ++j) {
+  for (int s = 0; s < S; ++s, ++t) {
+    if (t + 1 < T) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STAGE) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (t + 2 < T) issue(t + 2);
+    // fragment reads in inline asm: hipcc cannot tell them apart from the DMA in flight into
+    // another slot and would wait vmcnt(0) before a plain LDS read (draining the ring every step).
+    // The asm wait names every loaded register, so no MFMA is scheduled above it.
+    const uint32_t sa = GTA_LDS_ADDR(lds + (t % D) * STAGE + (wv * 2) * 1024) + static_cast<uint32_t>(lane) * 16u;
+    const uint32_t sb = GTA_LDS_ADDR(lds + (t % D) * STAGE + A_BYTES) + static_cast<uint32_t>(lane) * 16u;
+    f32x4 a4[2], b4[NT];
+    ds_read16<0>(a4[0], sa);
+    ds_read16<1024>(a4[1], sa);
+#pragma unroll
+    for (int c = 0; c < NT; ++c) ds_read16_dyn(b4[c], sb, c);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a4[0]), "+v"(a4[1]) :: "memory");
+#pragma unroll
+    for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(b4[c]));
+    float av[2][4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      av[i][0] = a4[i][0]; av[i][1] = a4[i][1]; av[i][2] = a4[i][2]; av[i][3] = a4[i][3];
+    }
+#pragma unroll
+    for (int c = 0; c < NT; ++c) mma(av, make_float4(b4[c][0], b4[c][1], b4[c][2], b4[c][3]), c);
+  }
+  // the group's last stage is done: its K tail, its rows out, the next group's sums
+  if (K % KS) tail(j);
+  epilogue(j);
+  zero_acc();
+  // the counted waits above assume only ring DMA is outstanding; stores may retire out of order
+  // with the loads, so drain them here (the next group's first stages have had a step to land)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
 // out[m, n] = sf(sum_s ws[s][m][n]) in slice order (split-K UPDATE; ws slices are [M, N] dense)
 __global__ void __launch_bounds__(kBlock)
 k_mm_slices_sum(const float* __restrict__ ws, int S, int64_t M, int N, int sf, float* __restrict__ out, int64_t ldo) {
@@ -2436,7 +2666,10 @@ struct Tuning {
   int att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
   int mm_blaslt = 1;        // plain fp32 UPDATE with M >= mm_blaslt_min_m on hipBLASLt (gta_update_mm_t)
   int64_t mm_blaslt_min_m = 1024;
-  int mm_blaslt_tune = 1;  // time the heuristic's top candidates at a shape's first use
+  int mm_blaslt_tune = 0;  // 1: time the heuristic's top candidates at a shape's first use (faster, but the pick
+                            // can differ between processes: ranks could disagree bitwise); 0: its first choice
+  int mm_ring = 1;          // fp32 UPDATE on k_mm_ring (LDS-DMA ring) instead of k_mm_rows
+  int64_t mm_ring_blocks_per_cu = 0;  // k_mm_ring persistent grid: blocks per CU (0 = 3)
   int mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
   int mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
   int64_t mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
@@ -2483,6 +2716,8 @@ const Knob* find_knob(const char* key) {
       {"mm_blaslt_min_m", nullptr, &Tuning::mm_blaslt_min_m},
       {"mm_blaslt_tune", &Tuning::mm_blaslt_tune, nullptr},
       {"mm_vstore", &Tuning::mm_vstore, nullptr},
+      {"mm_ring", &Tuning::mm_ring, nullptr},
+      {"mm_ring_blocks_per_cu", nullptr, &Tuning::mm_ring_blocks_per_cu},
       {"mm_blocks_per_cu", nullptr, &Tuning::mm_blocks_per_cu},
       {"apply_edge_form", &Tuning::apply_edge_form, nullptr},
       {"esm_lane", &Tuning::esm_lane, nullptr},
@@ -3149,22 +3384,35 @@ bool blaslt_f32(const float* x, int64_t ldx, int64_t M, int64_t K, const float* 
                 float* out, int64_t ldo, hipStream_t s) {
   static std::mutex mu;
   static std::map<int, std::pair<hipblasLtHandle_t, void*>> handles;  // per device: handle, workspace
-  static std::map<std::tuple<int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t>, BlasLtShape> shapes;
+  static std::map<std::tuple<int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int>, BlasLtShape> shapes;
   std::lock_guard<std::mutex> lock(mu);
+  // the device the stream belongs to (not the calling thread's current device)
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return false;
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing(s, &cap) != hipSuccess) return false;
+  const bool capturing = cap != hipStreamCaptureStatusNone;
   auto h = handles.find(dev);
   if (h == handles.end()) {
+    // a device's first use allocates (handle, workspace): never inside a graph capture -- the
+    // caller then runs the hand-written kernel instead (gta.h)
+    if (capturing) return false;
+    int cur = 0;
+    if (hipGetDevice(&cur) != hipSuccess || (cur != dev && hipSetDevice(dev) != hipSuccess)) return false;
     hipblasLtHandle_t hd = nullptr;
     void* ws = nullptr;
-    if (hipblasLtCreate(&hd) != HIPBLAS_STATUS_SUCCESS) return false;
-    if (hipMalloc(&ws, kBlasLtWorkspace) != hipSuccess) {
+    bool made = hipblasLtCreate(&hd) == HIPBLAS_STATUS_SUCCESS;
+    if (made && hipMalloc(&ws, kBlasLtWorkspace) != hipSuccess) {
       hipblasLtDestroy(hd);
-      return false;
+      made = false;
     }
+    if (cur != dev) (void)hipSetDevice(cur);
+    if (!made) return false;
     h = handles.emplace(dev, std::make_pair(hd, ws)).first;
   }
-  const auto key = std::make_tuple(dev, M, K, N, ldx, ldwt, ldo);
+  const int tune = tuning().mm_blaslt_tune;
+  const auto key = std::make_tuple(dev, M, K, N, ldx, ldwt, ldo, tune);
+  if (tune && capturing && shapes.find(key) == shapes.end()) return false;  // timing needs a live stream
   auto it = shapes.find(key);
   if (it == shapes.end()) {
     BlasLtShape sh;
@@ -3186,7 +3434,7 @@ bool blaslt_f32(const float* x, int64_t ldx, int64_t M, int64_t K, const float* 
            hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
                                                  sizeof(wsb)) == HIPBLAS_STATUS_SUCCESS &&
            hipblasLtMatmulAlgoGetHeuristic(h->second.first, sh.md, sh.la, sh.lb, sh.lc, sh.lc, pref,
-                                           tuning().mm_blaslt_tune ? kBlasLtCandidates : 1, res, &nres) ==
+                                           tune ? kBlasLtCandidates : 1, res, &nres) ==
                HIPBLAS_STATUS_SUCCESS &&
            nres > 0 && res[0].state == HIPBLAS_STATUS_SUCCESS;
       if (pref) hipblasLtMatmulPreferenceDestroy(pref);
@@ -3203,8 +3451,7 @@ bool blaslt_f32(const float* x, int64_t ldx, int64_t M, int64_t K, const float* 
         };
         const auto so = span(out, M, ldo, N);
         const bool disjoint = !overlap(so, span(x, M, ldx, K)) && !overlap(so, span(wt, N, ldwt, K));
-        hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-        if (nres > 1 && disjoint && hipStreamIsCapturing(s, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone) {
+        if (nres > 1 && disjoint && !capturing) {
           hipEvent_t e0, e1;
           if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
             const float alpha = 1.f, beta = 0.f;
@@ -3259,6 +3506,26 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   }
   const int nt = N <= 16 ? 1 : N <= 32 ? 2 : N <= 64 ? 4 : 8;
   const int64_t groups = (M + 127) / 128;
+  if (tuning().mm_ring && dtype == GTA_F32 && nt >= 4 && K >= 32 && aligned(x, 4) && aligned(wt, 16) &&
+      ldwt % 4 == 0) {
+    // persistent: at most 3 blocks per CU (48 KiB of LDS each at N = 128), every block the same
+    // number of row groups (+-1)
+    const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
+    const int64_t per_cu = tuning().mm_ring_blocks_per_cu > 0 ? tuning().mm_ring_blocks_per_cu : 3;
+    const int64_t slots = std::max<int64_t>(1, 256 * per_cu / ncb);
+    const int64_t rounds = (groups + slots - 1) / slots;
+    const dim3 gr(static_cast<unsigned>(((groups + rounds - 1) / rounds) * ncb));
+    const bool a16 = aligned(x, 16) && ldx % 4 == 0;  // 16-B A pieces
+#define GTA_RING(NT_, A4_)                                                                                      \
+  k_mm_ring<NT_, A4_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const float*>(x), ldx, row_idx, M,         \
+                                                          static_cast<int>(K), static_cast<const float*>(wt), ldwt, \
+                                                          static_cast<int>(N), sf, out, ldo, tuning().mm_vstore)
+    if (nt == 8) { if (a16) GTA_RING(8, false); else GTA_RING(8, true); }
+    else { if (a16) GTA_RING(4, false); else GTA_RING(4, true); }
+#undef GTA_RING
+    GTA_LAUNCHED("k_mm_ring");
+    return GTA_OK;
+  }
   const int64_t per_cu = tuning().mm_blocks_per_cu > 0 ? tuning().mm_blocks_per_cu : 8;
   const int kc = (dtype == GTA_F32) ? (nt >= 8 ? 64 : 128) : (nt >= 8 ? 128 : 256);  // k_mm_rows KC
   const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);

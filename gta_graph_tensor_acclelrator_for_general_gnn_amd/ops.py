@@ -475,7 +475,11 @@ def _transposed(w):
         return ent[2]
     if len(_WT_CACHE) >= 64:
         _WT_CACHE.clear()
-    wt = w.t().contiguous()
+    K, N = w.shape
+    per16 = 16 // w.element_size()
+    ld = -(-K // per16) * per16  # rows padded to 16 B: the ring GEMM DMAs W^T in 16-B pieces
+    wt = w.new_zeros(N, ld)[:, :K]
+    wt.copy_(w.t())
     _WT_CACHE[id(w)] = (weakref.ref(w), w._version, wt)
     return wt
 

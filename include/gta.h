@@ -222,14 +222,19 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
                   float* out, int64_t ldo, void* stream);
 
 /* Same UPDATE with W given TRANSPOSED: wt [N, K] row-major (leading dimension
- * ldwt >= K), dtype as above.  Runs the row-streaming kernel: a block owns all N
- * columns (up to 128 per block) and walks 128-row groups, so x is read once; wt
- * is staged into LDS with 16-B copies.  The contraction order differs from
- * gta_update_mm (fp32 rounding only).  A plain fp32 product (GTA_F32, row_idx NULL,
- * GTA_SF_NONE, M >= 1024) runs on hipBLASLt instead (the algorithm timed fastest at the
- * shape's first use in the process: repeat calls are bitwise equal, separate processes may
- * pick another algorithm and differ by fp32 rounding); this also applies to
- * gta_update_mm_t_split. */
+ * ldwt >= K), dtype as above.  Runs a row-streaming kernel: a block owns up to 128 of
+ * the N columns and walks 128-row groups, so x is read once.  fp32 with N > 32 and
+ * 16-B aligned wt rows (ldwt % 4 == 0) runs k_mm_ring: x and wt go global -> LDS by DMA
+ * through a 3-stage ring (persistent blocks, the ring running on across row groups);
+ * otherwise k_mm_rows (x fragments straight to registers, wt staged per K chunk).  Both
+ * contract k in the same order: bitwise equal to each other, fp32 rounding away from
+ * gta_update_mm.  A plain fp32 product (GTA_F32, row_idx NULL, GTA_SF_NONE, M >= 1024) runs
+ * on hipBLASLt instead, with the library heuristic's FIRST choice for the shape: the same
+ * algorithm in every process, so ranks agree bitwise (tuning knob mm_blaslt_tune = 1 times the
+ * top candidates instead: faster, but the pick may then differ between processes).  The
+ * library's per-device handle and workspace are created at the device's first plain fp32 call;
+ * a call made while the stream is being captured into a graph never creates them (nor times
+ * anything) and runs the hand-written kernel instead.  Also applies to gta_update_mm_t_split. */
 int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                     int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream);
 

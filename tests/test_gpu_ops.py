@@ -787,3 +787,39 @@ def test_aggregate_blocked_fused_reduce_bitwise(dev, heads, accumulate):
     err = np.abs(outs[1].cpu().numpy().astype(np.float64) - ref)
     assert np.all(err[has] <= bound[has])
     assert torch.isnan(outs[1][torch.from_numpy(~has).to(dev)]).all()  # 0 * inf, as the reduce pass gives
+
+
+@pytest.mark.parametrize("M,K,N,gathered,sf", [(40000, 602, 128, False, None), (20000, 602, 128, True, "RELU"),
+                                               (33000, 37, 200, False, None), (3001, 64, 64, False, "RELU"),
+                                               (17000, 1433, 128, False, None), (777, 100, 100, True, None),
+                                               (130, 48, 72, False, "ELU"), (89250, 500, 128, False, None)])
+def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
+    """k_mm_ring (fp32 UPDATE through the 3-stage LDS-DMA ring, the default for plain fp32 GEMMs)
+    == k_mm_rows bitwise (same per-lane k order and MFMA chain), and both within the fp64 bound:
+    K tails, rows past M, columns past N (two column blocks at N = 200), gathered rows, SF epilogues,
+    x rows not 16-B aligned (K = 602, 1433: the 4-B A-DMA form).  Shapes with enough row groups not
+    to take the split-K form."""
+    assert ops._mm_splits(M, K, N) == 1
+    rng = np.random.default_rng(M + K + N)
+    x = torch.from_numpy(rng.standard_normal((M + 5, K)).astype(np.float32))
+    w = torch.from_numpy((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32))
+    idx = torch.from_numpy(rng.integers(0, M + 5, M).astype(np.int32)) if gathered else None
+    xd, wd = x.to(dev), w.to(dev)
+    idd = None if idx is None else idx.to(dev)
+    outs = []
+    old_min = ops.MM_ROWS_MIN_M
+    try:
+        ops.MM_ROWS_MIN_M = 0
+        ops.set_debug("mm_blaslt", 0)
+        for ring in (0, 1):
+            ops.set_debug("mm_ring", ring)
+            outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
+    finally:
+        ops.set_debug("mm_ring", 1)
+        ops.set_debug("mm_blaslt", 1)
+        ops.MM_ROWS_MIN_M = old_min
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    xs = x.numpy()[idx.numpy()] if gathered else x.numpy()[:M]
+    ref = isa_ref.mm(xs, w.numpy(), sf_kind=sf)
+    _check(outs[1], ref, np.abs(xs).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "k_mm_ring")
