@@ -256,3 +256,36 @@ def test_gather_acc_fusion_bitwise_on_gpu(golden_dir, manifest, cora, dev, plan_
             vals[on] = [ex.tensor_of(i) for i in range(len(og))]
         for i, (a, b) in enumerate(zip(vals[True], vals[False])):
             assert torch.equal(a, b), f"{rec['file']} op {i}"
+
+
+def test_repeated_execute_replays_a_hip_graph(golden_dir, manifest, cora, dev, tmp_path, monkeypatch):
+    """execute() called again with the same graph and input tensors replays one captured HIP graph
+    (executor.AUTO_GRAPH): results equal the eager first call bitwise, follow in-place input
+    updates, and a new input tensor object means a new eager run."""
+    import shutil
+    rec = [s for s in manifest["streams"] if s.get("file") == "GCN-cora-layer1-original-c0.yaml"][0]
+    monkeypatch.chdir(tmp_path)
+    os.makedirs("Results/Insts")
+    os.makedirs("Network/GCN/GCN-cora/GCN-original")
+    shutil.copy(os.path.join(golden_dir, "streams", rec["file"]), "Results/Insts/GCN-cora-layer1-original.yaml")
+    shutil.copy(os.path.join(golden_dir, "ops", rec["op_yaml"]), "Network/GCN/GCN-cora/GCN-original/GCN-layer1-original.yaml")
+    ip, ix = cora
+    gd = G.from_numpy(ip, ix, device=dev)
+    og = ir.OpGraph.load("Network/GCN/GCN-cora/GCN-original/GCN-layer1-original.yaml")
+    tensors = workloads.make_tensors(og, gd, "GCN", seed=0)
+    run = lambda: executor.execute(rec["tile_size_list"], "cora", "GCN", "layer1", False, False,  # noqa: E731
+                                   graph=gd, tensors=tensors)
+    first = {k: v.clone() for k, v in run().outputs.items()}
+    n_before = sum(e.run is not None for e in executor._AUTO.values())
+    second = run()
+    third = run()
+    assert sum(e.run is not None for e in executor._AUTO.values()) == n_before + 1
+    assert second.outputs.keys() == first.keys() and second.model_rw == third.model_rw is not None
+    for k in first:
+        assert torch.equal(second.outputs[k], first[k]) and torch.equal(third.outputs[k], first[k])
+    tensors["x"].mul_(0.5)  # same storage, new values: the replay reads them
+    fresh = executor.Executor(og, ir.Stream(ir.read_yaml("Results/Insts/GCN-cora-layer1-original.yaml")), gd,
+                              tensors, Semantics.for_network("GCN", False)).run()
+    again = run()
+    for k in fresh:
+        assert torch.equal(again.outputs[k], fresh[k])
