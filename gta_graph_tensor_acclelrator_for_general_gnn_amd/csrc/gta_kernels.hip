@@ -908,8 +908,10 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
   const int32_t* ic = indices + it.beg;
   const float* wc = WEIGHTED ? w + it.beg * ldw + (W1 ? 0 : h) : nullptr;
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  // NT bit 0: non-temporal index loads, bit 2: non-temporal weight loads (both streams are read
+  // once), bit 1: non-temporal slab stores
   auto ldi = [&](const int32_t* p) { return (NT & 1) ? __builtin_nontemporal_load(p) : *p; };
-  auto ldw_ = [&](const float* p) { return (NT & 1) ? __builtin_nontemporal_load(p) : *p; };
+  auto ldw_ = [&](const float* p) { return (NT & 4) ? __builtin_nontemporal_load(p) : *p; };
   auto row = [&](int src) -> float4 {
     return *reinterpret_cast<const float4*>(xb + (__umul24(static_cast<uint32_t>(src), row_bytes) + colb));
   };
@@ -2656,7 +2658,9 @@ struct Tuning {
   int64_t seg_waves = 0;  // persistent waves of the column-blocked kernel (0 = 8 per SIMD)
   int seg_quarter = 1;     // quarter-wave (4 items per wave) form of the blocked aggregate
   int seg_lanes = 32;      // lanes per item of that form at F = 128: 32 (2 items/wave, measured 3 % faster) or 16
-  int seg_nt = 2;          // non-temporal bits of the multi-item forms at F = 128, U = 8: 2 = slab stores (-1 %)
+  int seg_nt = 3;          // non-temporal bits of the multi-item forms at F = 128, U = 8: 2 = slab stores (-1 %);
+                           // k_agg_h32 (8 heads): 3 = + index loads (-0.5 %: 4.829 vs 4.852 ms), 6/7 = weight
+                           // loads too (+3 %), profiles/r02_nt_bits_ab.json
   int seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
   int seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
   int apply_node_vec = 1;  // k_apply_node4 (float4, 32-bit index math) for the common apply_node shapes
@@ -3018,10 +3022,13 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
         }
         if (lean) {
           if (w && heads == 1) k_agg_h32<true, 2, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (!w && tuning().seg_nt == 2) k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (!w && (tuning().seg_nt & 2)) k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
           else if (!w) k_agg_h32<false, 0><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
           else if (tuning().seg_nt == 2) k_agg_h32<true, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (tuning().seg_nt == 1) k_agg_h32<true, 1><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (tuning().seg_nt == 1) k_agg_h32<true, 5><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (tuning().seg_nt == 3) k_agg_h32<true, 3><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (tuning().seg_nt == 6) k_agg_h32<true, 6><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+          else if (tuning().seg_nt == 7) k_agg_h32<true, 7><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
           else k_agg_h32<true, 0><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
         } else if (w && lph32 >= 1 && 32 % lph32 == 0 && (F / heads) % 4 == 0) {
           if (tuning().seg_u == 4)
@@ -3033,7 +3040,7 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
           else if (tuning().seg_nt == 1)
             k_agg_seg4<4, 8, true, 1, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                          lph32, slabs, its);
-          else if (tuning().seg_nt == 2)
+          else if (tuning().seg_nt == 2 || tuning().seg_nt == 3)  // (3: the lean kernel's default)
             k_agg_seg4<4, 8, true, 2, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
                                                                          lph32, slabs, its);
           else

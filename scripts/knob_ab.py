@@ -82,7 +82,7 @@ def main():
         json.dump({"n": args.n, "e": args.e, "blocks": B, "variants": out}, f, indent=1)
 
 
-DEFAULTS = {"seg_fuse": 0, "seg_lean": 1, "seg_nt": 2, "plan_len_sort": 1, "seg_lanes": 32, "seg_u": 8,
+DEFAULTS = {"seg_fuse": 0, "seg_lean": 1, "seg_nt": 3, "plan_len_sort": 1, "seg_lanes": 32, "seg_u": 8,
             "seg_quarter": 1, "seg_lean_w1": 1}
 
 if __name__ == "__main__":

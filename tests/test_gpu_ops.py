@@ -391,7 +391,8 @@ def test_edge_softmax_other_sf_and_errors(dev):
         ops.edge_softmax(g, a, b[:, :4].contiguous())
 
 
-@pytest.mark.parametrize("knobs", [{"seg_quarter": 0}, {"seg_u": 2}, {"seg_u": 4}, {"seg_nt": 3}, {"seg_lanes": 16},
+@pytest.mark.parametrize("knobs", [{"seg_quarter": 0}, {"seg_u": 2}, {"seg_u": 4}, {"seg_nt": 2}, {"seg_nt": 6},
+                                   {"seg_nt": 7}, {"seg_lanes": 16},
                                    {"seg_lanes": 16, "seg_u": 4}, {"seg_lean": 0}, {"seg_nt": 0}, {"seg_nt": 1},
                                    {"seg_lean_w1": 0}, {"seg_fuse": 0}, {"seg_fuse": 2}])
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 0), (64, 4), (256, 16), (128, 1)])
@@ -405,7 +406,7 @@ def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
     w = torch.from_numpy(rng.random((g.nnz, heads)).astype(np.float32)).to(dev) if heads else None
     y0 = ops.aggregate_blocked(g, x, w, blocks=8)
-    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 2, "seg_lanes": 32, "seg_lean": 1, "seg_lean_w1": 1,
+    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 3, "seg_lanes": 32, "seg_lean": 1, "seg_lean_w1": 1,
                 "seg_fuse": 0}
     try:
         for k, v in knobs.items():
