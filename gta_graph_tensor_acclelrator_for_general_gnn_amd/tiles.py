@@ -10,9 +10,13 @@ one integer-atomic histogram kernel (gta_tile_nnz); equal to the dense count for
 a CSR with column-sorted rows, duplicates included (tests/test_gpu_ops.py pins it
 to the reference's output).
 """
+import math
+
+import numpy as np
 import torch
 
 from . import ops
+from .graph import Graph
 
 
 def gen_size(start, end):
@@ -62,3 +66,41 @@ def metadata(graph, start=64, end=None):
 def nnz_in_tiles(graph):
     """Sum of all tile counts (edges minus self loops): the edge-tile total simulate() sweeps."""
     return int(ops.tile_nnz(graph, graph.n_rows).sum().item())
+
+
+# ---- the Reddit/Flickr variant ("FinalVersion For Paper/preprocessing_forReditFlickr.py") ----
+REDDIT_FLICKR_FRACTION = 0.25      # slice_matrix (:10-13): the first quarter of the 16x1 tile rows
+REDDIT_FLICKR_BLOCKS = [64, 128, 256, 512, 1024, 1600, 2048, 2560, 3200, 3840, 4480, 5120, 5760, 6400, 7040,
+                        7680, 8192]  # process_and_save's list (:40)
+
+
+def reblock(counts16, block, fraction=REDDIT_FLICKR_FRACTION):
+    """preprocessing_forReditFlickr.py:10-24 on a 16x1 tile-count matrix [ceil(N/16), N]: keep the
+    first int(rows * fraction) tile rows, then sum every `block` consecutive rows into one
+    (ceil(kept / block) rows, float64 like the reference's np.zeros accumulator; counts are
+    integers, so the sum order cannot change a value)."""
+    m = np.asarray(counts16)
+    keep = int(m.shape[0] * fraction)
+    nr = math.ceil(keep / block)
+    out = np.zeros((nr, m.shape[1]), dtype=np.float64)
+    if keep:
+        pad = np.zeros((nr * block, m.shape[1]), dtype=np.float64)
+        pad[:keep] = m[:keep]
+        out[:] = pad.reshape(nr, block, m.shape[1]).sum(axis=1)
+    return out
+
+
+def reddit_flickr_tiles(graph, block, fraction=REDDIT_FLICKR_FRACTION):
+    """The same matrix straight from the CSR on the GPU, without the [ceil(N/16), N] 16x1 matrix:
+    a 16x1 tile's count is the number of distinct (dst, src) pairs in its 16 rows, so summing
+    `block` tiles is the tile count at T = 16 * block over the kept rows (the first
+    16 * int(ceil(N/16) * fraction) rows): one gta_tile_nnz launch on that row range.
+    float64 [ceil(kept / block), N]."""
+    tiles16 = -(-graph.n_rows // 16)
+    keep = int(tiles16 * fraction)
+    rows = min(graph.n_rows, 16 * keep)
+    if rows == 0:
+        return torch.zeros(0, graph.n_cols, dtype=torch.float64, device=graph.device)
+    sub = Graph(graph.indptr[:rows + 1], graph.indices[:int(graph.indptr[rows])], n_cols=graph.n_cols)
+    c = ops.tile_nnz(sub, 16 * block)
+    return c.to(torch.float64)
