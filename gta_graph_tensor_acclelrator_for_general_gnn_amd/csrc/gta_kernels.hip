@@ -2359,6 +2359,15 @@ template <int OFF>
 __device__ __forceinline__ void ds_read16(f32x4& v, uint32_t a) {  // result valid after an lgkmcnt wait
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(a), "i"(OFF));
 }
+__device__ __forceinline__ void ds_read16_idx(f32x4& v, uint32_t a, int c) {  // c: 1 KiB fragment index < 16 (unrolled)
+  switch (c) {
+#define GTA_DSR(C_) case C_: ds_read16<(C_) * 1024>(v, a); break;
+    GTA_DSR(0) GTA_DSR(1) GTA_DSR(2) GTA_DSR(3) GTA_DSR(4) GTA_DSR(5) GTA_DSR(6) GTA_DSR(7)
+    GTA_DSR(8) GTA_DSR(9) GTA_DSR(10) GTA_DSR(11) GTA_DSR(12) GTA_DSR(13) GTA_DSR(14)
+#undef GTA_DSR
+    default: ds_read16<15 * 1024>(v, a); break;
+  }
+}
 __device__ __forceinline__ void ds_read16_dyn(f32x4& v, uint32_t a, int c) {  // c: 1 KiB fragment index (unrolled)
   switch (c) {
     case 0: ds_read16<0>(v, a); break;
@@ -2372,15 +2381,18 @@ __device__ __forceinline__ void ds_read16_dyn(f32x4& v, uint32_t a, int c) {  //
   }
 }
 
-template <int NT, bool A4 = false>  // A4: x rows not 16-B aligned (e.g. K = 602): A DMA'd in 4-B pieces
-__global__ void __launch_bounds__(kBlock, 3)  // 3 waves per SIMD = 3 blocks per CU (the LDS bound)
+// KH: 16-k halves per ring stage (1: 16-k stages, 2: 32-k stages, half the barriers); D: stages
+template <int NT, bool A4 = false, int KH = 1, int D = 3>  // A4: x rows not 16-B aligned (K = 602): 4-B A DMA
+__global__ void __launch_bounds__(kBlock, (KH == 1 ? 3 : (D == 2 ? 2 : 1)))  // waves per SIMD = blocks per CU (LDS)
 k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const float* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
-          int vec_store) {
+          int vec_store, int tuning_prio = 0) {
   static_assert(NT == 4 || NT == 8, "B fragments split evenly over the 4 waves");
-  constexpr int KS = 16, D = 3, BN = 16 * NT;
-  constexpr int A_BYTES = 4 * 2 * 1024, STAGE = A_BYTES + NT * 1024;
-  constexpr int PER_STAGE = (A4 ? 8 : 2) + NT / 4;  // DMA instructions per wave per stage
+  static_assert(KH == 1 || KH == 2, "16- or 32-k stages");
+  constexpr int KS = 16 * KH, BN = 16 * NT;
+  // stage image: A [wave][i][h] then B [c][h], 1 KiB fragments (16 rows x 16 k)
+  constexpr int A_BYTES = 4 * 2 * KH * 1024, STAGE = A_BYTES + NT * KH * 1024;
+  constexpr int PER_STAGE = KH * ((A4 ? 8 : 2) + NT / 4);  // DMA instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char lds[D * STAGE];
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = wave_id_uniform();
@@ -2393,7 +2405,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   const int64_t grp0 = blockIdx.x / ncb, gstep = gridDim.x / ncb;
   const int64_t n_groups = (M + 127) / 128;
   const int64_t my_groups = grp0 < n_groups ? (n_groups - grp0 + gstep - 1) / gstep : 0;
-  const int S = K / KS;  // whole 16-k stages per group (a K tail is one register step)
+  const int S = K / KS;  // whole stages per group (a K tail: register steps of 16 k)
   const int64_t T = my_groups * S;
   const float* bsrc[NT / 4];
 #pragma unroll
@@ -2420,20 +2432,24 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     }
     char* base = lds + (t % D) * STAGE;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      if constexpr (A4) {
+    for (int h = 0; h < KH; ++h) {
 #pragma unroll
-        for (int p = 0; p < 4; ++p)
-          __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[i] + k + 4 * p),
-                                           GTA_TO_LDS(base + (wv * 2 + i) * 1024 + p * 256), 4, 0, 0);
-      } else {
-        __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[i] + k), GTA_TO_LDS(base + (wv * 2 + i) * 1024), 16, 0, 0);
+      for (int i = 0; i < 2; ++i) {
+        char* dst = base + ((wv * 2 + i) * KH + h) * 1024;
+        if constexpr (A4) {
+#pragma unroll
+          for (int p = 0; p < 4; ++p)
+            __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[i] + k + 16 * h + 4 * p), GTA_TO_LDS(dst + p * 256),
+                                             4, 0, 0);
+        } else {
+          __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[i] + k + 16 * h), GTA_TO_LDS(dst), 16, 0, 0);
+        }
       }
-    }
 #pragma unroll
-    for (int q = 0; q < NT / 4; ++q)
-      __builtin_amdgcn_global_load_lds(const_cast<float*>(bsrc[q] + k),  // (a const source fails the host pass)
-                                       GTA_TO_LDS(base + A_BYTES + (wv * (NT / 4) + q) * 1024), 16, 0, 0);
+      for (int q = 0; q < NT / 4; ++q)
+        __builtin_amdgcn_global_load_lds(const_cast<float*>(bsrc[q] + k + 16 * h),  // (a const source fails the host pass)
+                                         GTA_TO_LDS(base + A_BYTES + ((wv * (NT / 4) + q) * KH + h) * 1024), 16, 0, 0);
+    }
   };
   f32x4 acc[2][NT];
   auto zero_acc = [&]() __attribute__((always_inline)) {
@@ -2498,60 +2514,78 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
           }
     }
   };
-  auto tail = [&](int64_t j) __attribute__((always_inline)) {  // the K tail from registers: k = S*16 + 4g + j < K, zeros past it
-    const int k0 = S * KS + 4 * g;
-    auto ld4 = [&](const float* p) __attribute__((always_inline)) {  // p = row + k0
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (k0 < K) v.x = p[0];
-      if (k0 + 1 < K) v.y = p[1];
-      if (k0 + 2 < K) v.z = p[2];
-      if (k0 + 3 < K) v.w = p[3];
-      return v;
-    };
-    float av[2][4];
+  auto tail = [&](int64_t j) __attribute__((always_inline)) {  // the K tail from registers, 16 k per step:
+    for (int kt = S * KS; kt < K; kt += 16) {                     // k = kt + 4g + jj < K, zeros past it
+      const int k0 = kt + 4 * g;
+      auto ld4 = [&](const float* p) __attribute__((always_inline)) {  // p = row + k0
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (k0 < K) v.x = p[0];
+        if (k0 + 1 < K) v.y = p[1];
+        if (k0 + 2 < K) v.z = p[2];
+        if (k0 + 3 < K) v.w = p[3];
+        return v;
+      };
+      float av[2][4];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const float4 a4 = ld4(a_row(j, i, r16) + k0);
-      av[i][0] = a4.x; av[i][1] = a4.y; av[i][2] = a4.z; av[i][3] = a4.w;
-    }
+      for (int i = 0; i < 2; ++i) {
+        const float4 a4 = ld4(a_row(j, i, r16) + k0);
+        av[i][0] = a4.x; av[i][1] = a4.y; av[i][2] = a4.z; av[i][3] = a4.w;
+      }
 #pragma unroll
-    for (int c = 0; c < NT; ++c) {
-      const int n = min(n0 + 16 * c + r16, N - 1);
-      mma(av, ld4(wt + static_cast<int64_t>(n) * ldwt + k0), c);
+      for (int c = 0; c < NT; ++c) {
+        const int n = min(n0 + 16 * c + r16, N - 1);
+        mma(av, ld4(wt + static_cast<int64_t>(n) * ldwt + k0), c);
+      }
     }
   };
   zero_acc();  // (the host sends K >= 32: every group has stages)
-  if (T > 0) issue(0);
-  if (T > 1) issue(1);
+#pragma unroll
+  for (int p = 0; p + 1 < D; ++p)
+    if (p < T) issue(p);
   int64_t t = 0;
   for (int64_t j = 0; j < my_groups; ++j) {
   for (int s = 0; s < S; ++s, ++t) {
-    if (t + 1 < T) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STAGE) : "memory");
+    // stage t landed (stages t+1 .. t+D-2 may stay in flight), every wave done with the slot
+    // about to be refilled (read at t-1)
+    if (D == 3 && t + 1 < T) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STAGE) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + 2 < T) issue(t + 2);
+    if (t + D - 1 < T) issue(t + D - 1);
     // fragment reads in inline asm: hipcc cannot tell them apart from the DMA in flight into
     // another slot and would wait vmcnt(0) before a plain LDS read (draining the ring every step).
     // The asm wait names every loaded register, so no MFMA is scheduled above it.
-    const uint32_t sa = GTA_LDS_ADDR(lds + (t % D) * STAGE + (wv * 2) * 1024) + static_cast<uint32_t>(lane) * 16u;
+    // all the stage's fragment reads issued at once; half h's MFMAs start when its reads are in
+    // (LDS returns in order: lgkmcnt(reads of the later halves))
+    const uint32_t sa = GTA_LDS_ADDR(lds + (t % D) * STAGE + (wv * 2) * KH * 1024) + static_cast<uint32_t>(lane) * 16u;
     const uint32_t sb = GTA_LDS_ADDR(lds + (t % D) * STAGE + A_BYTES) + static_cast<uint32_t>(lane) * 16u;
-    f32x4 a4[2], b4[NT];
-    ds_read16<0>(a4[0], sa);
-    ds_read16<1024>(a4[1], sa);
+    f32x4 a4[KH][2], b4[KH][NT];
 #pragma unroll
-    for (int c = 0; c < NT; ++c) ds_read16_dyn(b4[c], sb, c);
-    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a4[0]), "+v"(a4[1]) :: "memory");
+    for (int h = 0; h < KH; ++h) {
+      ds_read16_idx(a4[h][0], sa, h);
+      ds_read16_idx(a4[h][1], sa, KH + h);
 #pragma unroll
-    for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(b4[c]));
-    float av[2][4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      av[i][0] = a4[i][0]; av[i][1] = a4[i][1]; av[i][2] = a4[i][2]; av[i][3] = a4[i][3];
+      for (int c = 0; c < NT; ++c) ds_read16_idx(b4[h][c], sb, c * KH + h);
     }
 #pragma unroll
-    for (int c = 0; c < NT; ++c) mma(av, make_float4(b4[c][0], b4[c][1], b4[c][2], b4[c][3]), c);
+    for (int h = 0; h < KH; ++h) {
+      if (h + 1 < KH) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a4[h][0]), "+v"(a4[h][1]) : "n"(2 + NT) : "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a4[h][0]), "+v"(a4[h][1]) :: "memory");
+#pragma unroll
+      for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(b4[h][c]));
+      // j outermost: the 2 x NT accumulators are each touched once per 2*NT MFMAs; per
+      // accumulator the k order is k_mm_rows' (bitwise equal)
+      if (tuning_prio) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int c = 0; c < NT; ++c)
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+            acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[h][i][j], b4[h][c][j], acc[i][c], 0, 0, 0);
+      if (tuning_prio) __builtin_amdgcn_s_setprio(0);
+    }
   }
   // the group's last stage is done: its K tail, its rows out, the next group's sums
   if (K % KS) tail(j);
@@ -2673,7 +2707,9 @@ struct Tuning {
   int mm_blaslt_tune = 0;  // 1: time the heuristic's top candidates at a shape's first use (faster, but the pick
                             // can differ between processes: ranks could disagree bitwise); 0: its first choice
   int mm_ring = 1;          // fp32 UPDATE on k_mm_ring (LDS-DMA ring) instead of k_mm_rows
-  int64_t mm_ring_blocks_per_cu = 0;  // k_mm_ring persistent grid: blocks per CU (0 = 3)
+  int64_t mm_ring_blocks_per_cu = 0;  // k_mm_ring persistent grid: blocks per CU (0 = what LDS allows)
+  int mm_ring_form = 0;      // k_mm_ring stages: 0 = 16 k x 3 stages, 1 = 32 k x 2, 2 = 32 k x 3
+  int mm_ring_prio = 1;      // k_mm_ring: raise the wave priority around its MFMA block (+2-3 %, r02_mm_ab)
   int mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
   int mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
   int64_t mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
@@ -2722,6 +2758,8 @@ const Knob* find_knob(const char* key) {
       {"mm_vstore", &Tuning::mm_vstore, nullptr},
       {"mm_ring", &Tuning::mm_ring, nullptr},
       {"mm_ring_blocks_per_cu", nullptr, &Tuning::mm_ring_blocks_per_cu},
+      {"mm_ring_form", &Tuning::mm_ring_form, nullptr},
+      {"mm_ring_prio", &Tuning::mm_ring_prio, nullptr},
       {"mm_blocks_per_cu", nullptr, &Tuning::mm_blocks_per_cu},
       {"apply_edge_form", &Tuning::apply_edge_form, nullptr},
       {"esm_lane", &Tuning::esm_lane, nullptr},
@@ -3518,17 +3556,23 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
     // persistent: at most 3 blocks per CU (48 KiB of LDS each at N = 128), every block the same
     // number of row groups (+-1)
     const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
-    const int64_t per_cu = tuning().mm_ring_blocks_per_cu > 0 ? tuning().mm_ring_blocks_per_cu : 3;
+    const int64_t lds_blocks = tuning().mm_ring_form == 1 ? 2 : tuning().mm_ring_form == 2 ? 1 : 3;  // LDS per CU
+    const int64_t per_cu = tuning().mm_ring_blocks_per_cu > 0 ? tuning().mm_ring_blocks_per_cu : lds_blocks;
     const int64_t slots = std::max<int64_t>(1, 256 * per_cu / ncb);
     const int64_t rounds = (groups + slots - 1) / slots;
     const dim3 gr(static_cast<unsigned>(((groups + rounds - 1) / rounds) * ncb));
     const bool a16 = aligned(x, 16) && ldx % 4 == 0;  // 16-B A pieces
-#define GTA_RING(NT_, A4_)                                                                                      \
-  k_mm_ring<NT_, A4_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const float*>(x), ldx, row_idx, M,         \
-                                                          static_cast<int>(K), static_cast<const float*>(wt), ldwt, \
-                                                          static_cast<int>(N), sf, out, ldo, tuning().mm_vstore)
-    if (nt == 8) { if (a16) GTA_RING(8, false); else GTA_RING(8, true); }
-    else { if (a16) GTA_RING(4, false); else GTA_RING(4, true); }
+    const int form = tuning().mm_ring_form;  // 0: 16-k stages x 3; 1: 32-k stages x 2; 2: 32-k stages x 3
+#define GTA_RING(NT_, A4_, KH_, D_)                                                                              \
+  k_mm_ring<NT_, A4_, KH_, D_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const float*>(x), ldx, row_idx, M, \
+                                                                   static_cast<int>(K), static_cast<const float*>(wt), \
+                                                                   ldwt, static_cast<int>(N), sf, out, ldo,          \
+                                                                   tuning().mm_vstore, tuning().mm_ring_prio)
+#define GTA_RING_F(NT_, A4_) \
+  if (form == 1) GTA_RING(NT_, A4_, 2, 2); else if (form == 2) GTA_RING(NT_, A4_, 2, 3); else GTA_RING(NT_, A4_, 1, 3)
+    if (nt == 8) { if (a16) { GTA_RING_F(8, false); } else { GTA_RING_F(8, true); } }
+    else { if (a16) { GTA_RING_F(4, false); } else { GTA_RING_F(4, true); } }
+#undef GTA_RING_F
 #undef GTA_RING
     GTA_LAUNCHED("k_mm_ring");
     return GTA_OK;

@@ -12,10 +12,12 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops  # noqa: E402
 
-FORMS = {"ring": {"mm_blaslt": 0, "mm_ring": 1}, "rows": {"mm_blaslt": 0, "mm_ring": 0},
+FORMS = {"ring": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 0},
+         "ring_noprio": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 0, "mm_ring_prio": 0},
+         "rows": {"mm_blaslt": 0, "mm_ring": 0},
          "hipblaslt": {"mm_blaslt": 1, "mm_ring": 0, "mm_blaslt_tune": 1},
          "hipblaslt_top1": {"mm_blaslt": 1, "mm_ring": 0, "mm_blaslt_tune": 0}}
-DEFAULTS = {"mm_blaslt": 1, "mm_ring": 1, "mm_blaslt_tune": 0}
+DEFAULTS = {"mm_blaslt": 1, "mm_ring": 1, "mm_blaslt_tune": 0, "mm_ring_form": 0, "mm_ring_prio": 1}
 
 
 def main():
@@ -53,7 +55,7 @@ def main():
             for f in FORMS:
                 ms = float(np.median(t[f]))
                 rec[f] = {"ms": ms, "TF": 2 * M * K * N / ms / 1e9}
-            rec["ring_eq_rows_bitwise"] = bool(torch.equal(y["ring"], y["rows"]))
+            rec["ring_eq_rows_bitwise"] = bool(all(torch.equal(y[f], y["rows"]) for f in FORMS if f.startswith("ring")))
             rec["ring_vs_blaslt_max_abs"] = float((y["ring"] - y["hipblaslt"]).abs().max())
             out[f"M={M} K={K} N={N}"] = rec
             print(f"M={M} K={K} N={N} " + "  ".join(f"{f} {rec[f]['ms']:.3f} ms {rec[f]['TF']:.1f} TF"

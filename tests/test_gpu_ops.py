@@ -812,15 +812,18 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     try:
         ops.MM_ROWS_MIN_M = 0
         ops.set_debug("mm_blaslt", 0)
-        for ring in (0, 1):
+        for ring, form in ((0, 0), (1, 0), (1, 1), (1, 2)):  # k_mm_rows, then the ring's three stage forms
             ops.set_debug("mm_ring", ring)
+            ops.set_debug("mm_ring_form", form)
             outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
     finally:
         ops.set_debug("mm_ring", 1)
+        ops.set_debug("mm_ring_form", 0)
         ops.set_debug("mm_blaslt", 1)
         ops.MM_ROWS_MIN_M = old_min
     torch.cuda.synchronize()
-    assert torch.equal(outs[0], outs[1])
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
     xs = x.numpy()[idx.numpy()] if gathered else x.numpy()[:M]
     ref = isa_ref.mm(xs, w.numpy(), sf_kind=sf)
     _check(outs[1], ref, np.abs(xs).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "k_mm_ring")
