@@ -827,3 +827,37 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     xs = x.numpy()[idx.numpy()] if gathered else x.numpy()[:M]
     ref = isa_ref.mm(xs, w.numpy(), sf_kind=sf)
     _check(outs[1], ref, np.abs(xs).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "k_mm_ring")
+
+
+@pytest.mark.parametrize("n", [1, 37])
+def test_degenerate_graphs_every_op(dev, n):
+    """Graphs with no edges at all (and a single node): every op returns its defined value -- zero
+    aggregates (or the untouched accumulator), empty edge tensors, zero tile counts -- and no launch
+    fails (no zero-sized grids)."""
+    g = G.from_numpy(np.zeros(n + 1, np.int64), np.zeros(0, np.int32), device=dev)
+    F = 128
+    x = torch.randn(n, F, device=dev)
+    w8 = torch.zeros(0, 8, device=dev)
+    assert torch.equal(ops.aggregate(g, x, "src", w8), torch.zeros(n, F, device=dev))
+    assert torch.equal(ops.aggregate(g, x, "src", None, plan=64), torch.zeros(n, F, device=dev))
+    acc = x.clone()
+    assert torch.equal(ops.aggregate(g, x, "src", None, out=acc, accumulate=True), x)
+    for fuse in (0, 1):
+        ops.set_debug("seg_fuse", fuse)
+        try:
+            assert torch.equal(ops.aggregate_blocked(g, x, w8, blocks=4), torch.zeros(n, F, device=dev))
+        finally:
+            ops.set_debug("seg_fuse", 0)
+    assert ops.scatter(g, x, "C").shape == (0, F)
+    assert torch.equal(ops.gather_add(g, torch.zeros(0, F, device=dev)), torch.zeros(n, F, device=dev))
+    assert ops.apply_edge(g, "MUL", None, torch.zeros(0, F, device=dev), "edge", x, "src").shape == (0, F)
+    a = torch.randn(n, 8, device=dev)
+    out, sums = ops.edge_softmax(g, a, a.clone(), want_sums=True)
+    assert out.shape == (0, 8) and torch.equal(sums, torch.zeros(n, 8, device=dev))
+    y, _ = ops.gat_aggregate_blocked(g, x, a, a.clone(), blocks=4)
+    assert y.shape == (n, F) and torch.equal(y, torch.zeros(n, F, device=dev))  # 0 / 0 rows give 0
+    assert int(ops.tile_nnz(g, 16).sum()) == 0
+    wm = torch.randn(F, 64, device=dev)
+    assert ops.update_mm(x, wm).shape == (n, 64)
+    assert ops.update_mm(x[:0], wm).shape == (0, 64)
+    torch.cuda.synchronize()
