@@ -64,6 +64,16 @@ def log(rank, msg):
     print(f"[bench rank {rank}] {time.strftime('%H:%M:%S')} {msg}", file=sys.stderr, flush=True)
 
 
+def make_inputs(n=N_REDDIT, e=E_REDDIT, dev=None):
+    """(graph, X1, alpha) of the whole metric workload on one device (the probe scripts' entry)."""
+    sh = metric.Shard(n, e, 0, 1, 1, 1, dev or torch.device("cuda", 0), keep_rows=False)
+    return sh.graph, sh.x, sh.alpha
+
+
+alg_bytes = metric.alg_bytes
+auto_blocks = ops.BlockedPlan.auto_blocks
+
+
 # ----------------------------------------------------------------------------------------------
 # the timed workload
 # ----------------------------------------------------------------------------------------------

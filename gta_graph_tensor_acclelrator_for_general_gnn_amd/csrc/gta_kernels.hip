@@ -2422,15 +2422,24 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   };
   const float* asrc[2];
   int64_t asrc_j = -1;
-  auto issue = [&](int64_t t) __attribute__((always_inline)) {
-    const int64_t j = t / S;
-    const int k = static_cast<int>(t - j * S) * KS;
+  // the next stage to DMA as (group, stage in group, ring slot), advanced by one per call: no
+  // 64-bit division per stage (its ~150 scalar instructions per stage were measurable)
+  int64_t iss_j = 0;
+  int iss_s = 0, iss_slot = 0;
+  auto issue = [&]() __attribute__((always_inline)) {
+    const int64_t j = iss_j;
+    const int k = iss_s * KS;
     if (j != asrc_j) {
 #pragma unroll
       for (int i = 0; i < 2; ++i) asrc[i] = a_row(j, i, A4 ? lane >> 2 : r16) + (A4 ? (lane & 3) : 4 * g);
       asrc_j = j;
     }
-    char* base = lds + (t % D) * STAGE;
+    char* base = lds + iss_slot * STAGE;
+    iss_slot = iss_slot + 1 == D ? 0 : iss_slot + 1;
+    if (++iss_s == S) {
+      iss_s = 0;
+      ++iss_j;
+    }
 #pragma unroll
     for (int h = 0; h < KH; ++h) {
 #pragma unroll
@@ -2541,10 +2550,11 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   zero_acc();  // (the host sends K >= 32: every group has stages)
 #pragma unroll
   for (int p = 0; p + 1 < D; ++p)
-    if (p < T) issue(p);
+    if (p < T) issue();
   int64_t t = 0;
+  int slot = 0;  // ring slot of stage t
   for (int64_t j = 0; j < my_groups; ++j) {
-  for (int s = 0; s < S; ++s, ++t) {
+  for (int s = 0; s < S; ++s, ++t, slot = slot + 1 == D ? 0 : slot + 1) {
     // stage t landed (stages t+1 .. t+D-2 may stay in flight), every wave done with the slot
     // about to be refilled (read at t-1)
     if (D == 3 && t + 1 < T) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STAGE) : "memory");
@@ -2552,14 +2562,14 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
-    if (t + D - 1 < T) issue(t + D - 1);
+    if (t + D - 1 < T) issue();  // stage t + D - 1
     // fragment reads in inline asm: hipcc cannot tell them apart from the DMA in flight into
     // another slot and would wait vmcnt(0) before a plain LDS read (draining the ring every step).
     // The asm wait names every loaded register, so no MFMA is scheduled above it.
     // all the stage's fragment reads issued at once; half h's MFMAs start when its reads are in
     // (LDS returns in order: lgkmcnt(reads of the later halves))
-    const uint32_t sa = GTA_LDS_ADDR(lds + (t % D) * STAGE + (wv * 2) * KH * 1024) + static_cast<uint32_t>(lane) * 16u;
-    const uint32_t sb = GTA_LDS_ADDR(lds + (t % D) * STAGE + A_BYTES) + static_cast<uint32_t>(lane) * 16u;
+    const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * 2) * KH * 1024) + static_cast<uint32_t>(lane) * 16u;
+    const uint32_t sb = GTA_LDS_ADDR(lds + slot * STAGE + A_BYTES) + static_cast<uint32_t>(lane) * 16u;
     f32x4 a4[KH][2], b4[KH][NT];
 #pragma unroll
     for (int h = 0; h < KH; ++h) {
@@ -2709,7 +2719,7 @@ struct Tuning {
   int mm_ring = 1;          // fp32 UPDATE on k_mm_ring (LDS-DMA ring) instead of k_mm_rows
   int64_t mm_ring_blocks_per_cu = 0;  // k_mm_ring persistent grid: blocks per CU (0 = what LDS allows)
   int mm_ring_form = 0;      // k_mm_ring stages: 0 = 16 k x 3 stages, 1 = 32 k x 2, 2 = 32 k x 3
-  int mm_ring_prio = 1;      // k_mm_ring: raise the wave priority around its MFMA block (+2-3 %, r02_mm_ab)
+  int mm_ring_prio = 0;      // k_mm_ring: raise the wave priority around its MFMA block (+-3 %: noise, r02_mm_ab*)
   int mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
   int mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
   int64_t mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
