@@ -75,6 +75,9 @@ class AggregatePlan:
         check(L.gta_aggregate_plan_build(_ptr(graph.indptr), graph.n_rows, graph.nnz, self.chunk,
                                          _ptr(self.buf), int(nbytes), _stream(graph.device)), "plan_build")
         self._ws = {}
+        # rows split over several wavefronts (read once, at build): none -> aggregate() runs the
+        # one-wave-per-row form, which needs no combine launch (small graphs: Cora)
+        self.splits = self.n_split()
 
     def workspace(self, F):
         if F not in self._ws:
@@ -128,6 +131,8 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
         return out
     if isinstance(plan, int):
         plan = graph.plan(plan)
+        if plan.splits == 0:  # no row is split: the per-row form (same sums, no combine launch)
+            plan = None
     pbuf = ws = None
     chunk = 0
     if plan is not None:
@@ -454,7 +459,9 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
 
 MM_FORM = "rows"  # "rows": gta_update_mm_t (x read once per output); "tile": gta_update_mm 64x64 tiles
 MM_SPLIT_MAX_BLOCKS = 128  # split K when the row-streaming grid has fewer blocks than this (of 256 CUs)
-MM_ROWS_MIN_M = 32768  # below this the 128-row groups are too few to fill 256 CUs: 64x64 tiles win
+MM_ROWS_MIN_M = 0  # smallest M for the row-streaming entry (k_mm_ring / k_mm_rows / library); below, the
+                   # 64x64-tile kernel. With the ring the row form wins at every M measured: GCN Cora's
+                   # [2708 x 128].[128 x 64] took the forward 0.093 -> 0.081 ms (profiles/r02_layer_bench_mmrows.log)
 _WT_CACHE = {}
 
 
