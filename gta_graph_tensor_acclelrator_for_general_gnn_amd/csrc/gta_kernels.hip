@@ -2726,6 +2726,7 @@ struct Tuning {
   int apply_edge_form = 1;  // 1: row-sweep K3 kernels (cols / pack); 0: the generic per-element kernel
   int esm_lane = 1;        // edge-per-lane edge-softmax when H in {4,8,16} and rows are 16-B aligned
   int esm_keep = 4;        // chunks of 64 edges held in VGPRs by the edge-per-lane form (2 or 4)
+  int seg_phase = 0;         // single-launch blocked aggregate: 0 = items + reduce, 1 = items only, 2 = reduce only
   int seg_fuse = 0;          // k_agg_h32 with the in-launch ordered reduce (no k_seg_reduce pass): bitwise equal,
                              // but 5.28 vs 4.93 ms on Reddit (the per-item drain + ticket costs more than the
                              // pass it removes; profiles/r02_fused_reduce_ab.json); 2 = the same at 6 waves/SIMD
@@ -2755,6 +2756,7 @@ const Knob* find_knob(const char* key) {
       {"seg_lanes", &Tuning::seg_lanes, nullptr},
       {"seg_lean", &Tuning::seg_lean, nullptr},
       {"seg_fuse", &Tuning::seg_fuse, nullptr},
+      {"seg_phase", &Tuning::seg_phase, nullptr},
       {"att_lean", &Tuning::att_lean, nullptr},
       {"att_direct", &Tuning::att_direct, nullptr},
       {"plan_len_sort", &Tuning::plan_len_sort, nullptr},
@@ -3037,8 +3039,9 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     const int lph = w ? static_cast<int>((F / heads) / vq) : 0;
     const bool quarter = tuning().seg_quarter && (vq == 4 || vq == 8 || vq == 16) && ldx % 4 == 0 && aligned(x, 16) &&
                          (!w || ((F / heads) % vq == 0 && lph >= 1 && 16 % lph == 0));
-    if (items == 0) {
-      // no edges: no items; the reduce below writes the (empty) rows
+    const int phase = tuning().seg_phase;
+    if (items == 0 || phase == 2) {
+      // no edges: no items; the reduce below writes the (empty) rows (phase 2: the reduce only)
     } else if (quarter) {
       const dim3 g4(static_cast<unsigned>((items + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock)));
 #define GTA_SEG4(VW_, U_)                                                                                   \
@@ -3124,6 +3127,7 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
 #undef GTA_SEG2D
     GTA_LAUNCHED("k_agg_seg2d");
     }
+    if (phase == 1) return GTA_OK;  // the item launch only; a later phase-2 call reduces
     const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
     if (vw == 2) k_seg_reduce<2><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, ri);
     else if (vw == 4) k_seg_reduce<4><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, ri);
