@@ -13,7 +13,7 @@ sys.path.insert(0, ROOT)
 from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops  # noqa: E402
 
 FORMS = {"ring": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 0},
-         "ring256": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 3},
+         "ring_prio": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 0, "mm_ring_prio": 1},
          "rows": {"mm_blaslt": 0, "mm_ring": 0},
          "hipblaslt": {"mm_blaslt": 1, "mm_ring": 0, "mm_blaslt_tune": 1},
          "hipblaslt_top1": {"mm_blaslt": 1, "mm_ring": 0, "mm_blaslt_tune": 0}}
