@@ -2386,8 +2386,15 @@ template <int NT, bool A4 = false, int KH = 1, int D = 3>  // A4: x rows not 16-
 __global__ void __launch_bounds__(kBlock, (KH == 1 ? 3 : (D == 2 ? 2 : 1)))  // waves per SIMD = blocks per CU (LDS)
 k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const float* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
-          int vec_store, int tuning_prio = 0) {
+          int vec_store, int tuning_prio = 0, int kslice = 0, int64_t slice_stride = 0) {
   static_assert(NT == 4 || NT == 8, "B fragments split evenly over the 4 waves");
+  if (kslice > 0) {  // split K: block row y takes k in [y * kslice, +kslice) into output slice y
+    const int k0 = static_cast<int>(blockIdx.y) * kslice;
+    x += k0;
+    wt += k0;
+    K = min(kslice, K - k0);
+    out += static_cast<int64_t>(blockIdx.y) * slice_stride;
+  }
   static_assert(KH == 1 || KH == 2, "16- or 32-k stages");
   constexpr int KS = 16 * KH, BN = 16 * NT;
   // stage image: A [wave][i][h] then B [c][h], 1 KiB fragments (16 rows x 16 k)
@@ -2547,7 +2554,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
       }
     }
   };
-  zero_acc();  // (the host sends K >= 32: every group has stages)
+  zero_acc();  // (a K < 16 slice has no stages: T = 0, the tail does it all)
 #pragma unroll
   for (int p = 0; p + 1 < D; ++p)
     if (p < T) issue();
@@ -3643,18 +3650,34 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
     return fail(GTA_ERR_ARG, "update_mm_t_split: workspace too small");
   if (nsl > 65535) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t_split: too many slices");
   float* ws = static_cast<float*>(workspace);
+  const int nt = N <= 16 ? 1 : N <= 32 ? 2 : N <= 64 ? 4 : 8;
+  const int64_t groups = (M + 127) / 128;
+  const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
+  hipStream_t s = S(stream);
   if (tuning().mm_blaslt && dtype == GTA_F32 && !row_idx && sf == GTA_SF_NONE && M >= tuning().mm_blaslt_min_m &&
       blaslt_f32(static_cast<const float*>(x), ldx, M, K, static_cast<const float*>(wt), ldwt, N, out, ldo, S(stream))) {
     GTA_LAUNCHED("hipblaslt_matmul");
     return GTA_OK;
   }
-  const int nt = N <= 16 ? 1 : N <= 32 ? 2 : N <= 64 ? 4 : 8;
-  const int64_t groups = (M + 127) / 128;
-  const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
+  if (tuning().mm_ring && dtype == GTA_F32 && nt >= 4 && aligned(x, 4) && aligned(wt, 16) && ldwt % 4 == 0 &&
+      ks % 4 == 0 && N % 4 == 0 && aligned(ws, 16)) {
+    // the LDS-DMA ring per K slice (one 128-row group per block: grid = groups x slices), then the
+    // ordered slice sum; for what the library does not take (gathered rows, SF, M < 1024). GCN Cora's
+    // [2708 x 1433].[1433 x 128]: hipBLASLt 24-29 us, ring slices + sum 41 (33.7 + 7.0), k_mm_rows slices 46
+    const dim3 gr(static_cast<unsigned>(groups * ncb), static_cast<unsigned>(nsl));
+    const bool a16 = aligned(x, 16) && ldx % 4 == 0;
+#define GTA_RINGS(NT_, A4_)                                                                                    \
+  k_mm_ring<NT_, A4_><<<gr, dim3(kBlock), 0, s>>>(static_cast<const float*>(x), ldx, row_idx, M, static_cast<int>(K), \
+                                                  static_cast<const float*>(wt), ldwt, static_cast<int>(N), GTA_SF_NONE, \
+                                                  ws, N, 1, tuning().mm_ring_prio, static_cast<int>(ks), M * N)
+    if (nt == 8) { if (a16) { GTA_RINGS(8, false); } else { GTA_RINGS(8, true); } }
+    else { if (a16) { GTA_RINGS(4, false); } else { GTA_RINGS(4, true); } }
+#undef GTA_RINGS
+    GTA_LAUNCHED("k_mm_ring<split>");
+  } else {
   const dim3 gr(static_cast<unsigned>(groups * ncb), static_cast<unsigned>(nsl));
   const bool pf = tuning().mm_prefetch == 2 || (tuning().mm_prefetch == 1 && (dtype != GTA_BF16 || ks % 32 == 0));
   const int ki = static_cast<int>(K);
-  hipStream_t s = S(stream);
 #define GTA_MMS(TA_, WT_, NT_)                                                                                    \
   if (pf) k_mm_rows<TA_, WT_, NT_, true><<<gr, dim3(kBlock), 0, s>>>(static_cast<const TA_*>(x), ldx, row_idx, M, ki, \
       static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N, tuning().mm_vstore);                                 \
@@ -3668,6 +3691,7 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
 #undef GTA_MMS_NT
 #undef GTA_MMS
   GTA_LAUNCHED("k_mm_rows<split>");
+  }
   const int64_t total = M * N;
   k_mm_slices_sum<<<dim3(static_cast<unsigned>(std::min<int64_t>((total + kBlock - 1) / kBlock, 4096))), dim3(kBlock), 0,
                     s>>>(ws, static_cast<int>(nsl), M, static_cast<int>(N), sf, out, ldo);

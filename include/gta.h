@@ -242,7 +242,10 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
  * into slices of ceil(K / splits) rounded up to 32; each slice's partial [M, N] goes to the
  * workspace (gta_update_mm_t_split_workspace_bytes) and a second kernel adds the slices in order
  * and applies sf.  Deterministic; the contraction order differs from gta_update_mm_t (fp32
- * rounding only).  Same reference as gta_update_mm. */
+ * rounding only).  A plain fp32 product goes to hipBLASLt as in gta_update_mm_t; otherwise fp32
+ * with N > 32 (N % 4 == 0, 16-B aligned wt rows) runs every slice on k_mm_ring (one 128-row
+ * group per block), else k_mm_rows per slice: the same slices bitwise.  Same reference as
+ * gta_update_mm. */
 int64_t gta_update_mm_t_split_workspace_bytes(int64_t M, int64_t K, int64_t N, int64_t splits);
 int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                           int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, int64_t splits,

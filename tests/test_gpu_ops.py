@@ -829,6 +829,38 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     _check(outs[1], ref, np.abs(xs).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "k_mm_ring")
 
 
+@pytest.mark.parametrize("M,K,N,gathered,sf", [(2708, 1433, 128, False, None), (2708, 1433, 128, True, "RELU"),
+                                               (2708, 1432, 64, False, None), (1000, 1350, 64, False, None),
+                                               (600, 1000, 200, False, "ELU"), (900, 700, 66, False, None)])
+def test_update_mm_split_ring_bitwise(dev, M, K, N, gathered, sf):
+    """Split-K UPDATE with every K slice on k_mm_ring (one 128-row group per block, grid.y = the
+    slices) == the k_mm_rows slices bitwise, both within the fp64 bound: x rows 4-B (K = 1433, 1350)
+    and 16-B aligned (1432), a last slice shorter than one 16-k stage (K = 1350: 14 x 96 + 6), two
+    column blocks (N = 200), gathered rows, SF after the slice sum; N = 66 (not a multiple of 4)
+    stays on k_mm_rows."""
+    assert ops._mm_splits(M, K, N) > 1
+    rng = np.random.default_rng(M + K + N)
+    x = torch.from_numpy(rng.standard_normal((M + 5, K)).astype(np.float32))
+    w = torch.from_numpy((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32))
+    idx = torch.from_numpy(rng.integers(0, M + 5, M).astype(np.int32)) if gathered else None
+    xd, wd = x.to(dev), w.to(dev)
+    idd = None if idx is None else idx.to(dev)
+    outs = []
+    try:
+        ops.set_debug("mm_blaslt", 0)
+        for ring in (0, 1):
+            ops.set_debug("mm_ring", ring)
+            outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
+    finally:
+        ops.set_debug("mm_ring", 1)
+        ops.set_debug("mm_blaslt", 1)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    xs = x.numpy()[idx.numpy()] if gathered else x.numpy()[:M]
+    ref = isa_ref.mm(xs, w.numpy(), sf_kind=sf)
+    _check(outs[1], ref, np.abs(xs).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "split k_mm_ring")
+
+
 @pytest.mark.parametrize("n", [1, 37])
 def test_degenerate_graphs_every_op(dev, n):
     """Graphs with no edges at all (and a single node): every op returns its defined value -- zero
