@@ -861,6 +861,49 @@ def test_update_mm_split_ring_bitwise(dev, M, K, N, gathered, sf):
     _check(outs[1], ref, np.abs(xs).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "split k_mm_ring")
 
 
+@pytest.mark.parametrize("F,heads,n_cols", [(128, 8, (1 << 23) + 77), (64, 4, (1 << 24) + 33)])
+def test_aggregate_tables_past_32bit_offsets(dev, F, heads, n_cols):
+    """Maximum sizes: gathered tables past the lean kernels' 32-bit addressing (2^23 + 77 rows of
+    512 B = 4 GiB + 39 KB of byte offsets; 2^24 + 33 rows, past __umul24's 24-bit source ids).
+    The host guards send every entry -- row-chunk plan, one wave per row, column-blocked, fused
+    GAT attention -- to its 64-bit form; all match the fp64 oracle, with sources in the table's
+    last rows (row 0 gathers the last 40) and a 700-edge row split across items and blocks."""
+    rng = np.random.default_rng(F)
+    n_rows = 3000
+    deg = rng.integers(0, 40, n_rows)
+    deg[0], deg[7], deg[9] = 40, 700, 0
+    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    ix = np.concatenate([np.sort(rng.integers(0, n_cols, d)) for d in deg]).astype(np.int32)
+    ix[:40] = np.arange(n_cols - 40, n_cols, dtype=np.int32)
+    g = G.from_numpy(ip, ix, device=dev, n_cols=n_cols)
+    torch.manual_seed(F)
+    xd = torch.randn(n_cols, F, device=dev)  # 4.3 GB
+    uniq, local = np.unique(ix, return_inverse=True)  # the oracle sees only the gathered rows
+    xs = xd[torch.from_numpy(uniq.astype(np.int64)).to(dev)].cpu().numpy().astype(np.float64)
+    lx = local.astype(np.int32)
+    w = rng.random((g.nnz, heads)).astype(np.float32)
+    wd = torch.from_numpy(w).to(dev)
+    ref = isa_ref.aggregate(ip, lx, xs, "src", w)
+    scale = isa_ref.aggregate(ip, lx, np.abs(xs), "src", w)
+    for name, y in (("plan", ops.aggregate(g, xd, "src", wd, plan=64)),
+                    ("per-row", ops.aggregate(g, xd, "src", wd)),
+                    ("blocked", ops.aggregate_blocked(g, xd, wd, blocks=4))):
+        _check(y, ref, scale, f"{name} F={F} past 32-bit offsets")
+    if F == 128:
+        a = rng.standard_normal((n_cols, heads)).astype(np.float32)  # only gathered b rows matter
+        ad, bd = torch.from_numpy(a).to(dev), torch.from_numpy(a[::-1].copy()).to(dev)
+        y, sums = ops.gat_aggregate_blocked(g, xd, ad, bd, normalize=True, want_sums=True, blocks=4)
+        rows = np.arange(n_rows)
+        bs = a[::-1][uniq].astype(np.float64)
+        aa = a[rows].astype(np.float64)
+        gref, gsum = isa_ref.gat_aggregate(ip, lx, xs, aa, bs, "EXP_LEAKY_RELU", True)
+        _check(sums, gsum, gsum, "gat sums past 32-bit offsets")
+        v, _ = isa_ref.edge_softmax(ip, lx, aa, bs, "EXP_LEAKY_RELU", False)
+        sc = isa_ref.aggregate(ip, lx, np.abs(xs), "src", v)
+        sc = sc / np.repeat(np.where(gsum > 0, gsum, 1.0), F // heads, axis=1) * 4
+        _check(y, gref, sc, "gat y past 32-bit offsets")
+
+
 @pytest.mark.parametrize("n", [1, 37])
 def test_degenerate_graphs_every_op(dev, n):
     """Graphs with no edges at all (and a single node): every op returns its defined value -- zero
