@@ -1146,7 +1146,12 @@ def execute(tile_size_list, dataset, network, layer, isReorder, isSinput=False, 
     form) and model_cycles (model="full"; exact restatement of the cycle loop,
     Python-speed, meant for Cora/Flickr-sized graphs).  `res.simulate_tuple()`
     is what simulate() would have returned.  trace: True (events in res.trace) or a path for a
-    Chrome trace JSON of the measured per-op device time, as the reference's chrome_timeline.json."""
+    Chrome trace JSON of the measured per-op device time, as the reference's chrome_timeline.json.
+
+    From the second call with the same stream, CSR and input tensor objects on (graphs of at most
+    AUTO_GRAPH_MAX_EDGES edges), the execution replays a captured HIP graph: the outputs are then
+    the graph's own tensors and the next such call overwrites them -- clone what must outlive it
+    (AUTO_GRAPH = False keeps every call eager, with fresh outputs)."""
     op_path = op_path or ir.op_yaml_path(network, dataset, layer, isReorder, op_root)
     inst_path = inst_path or ir.inst_path(network, dataset, layer, isReorder, inst_root)
     sem, g, records, s = _load(network, isReorder, semantics, op_path, inst_path)
