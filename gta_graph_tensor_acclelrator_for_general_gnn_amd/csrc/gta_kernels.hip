@@ -2383,7 +2383,7 @@ __device__ __forceinline__ void ds_read16_dyn(f32x4& v, uint32_t a, int c) {  //
 
 // KH: 16-k halves per ring stage (1: 16-k stages, 2: 32-k stages, half the barriers); D: stages
 template <int NT, bool A4 = false, int KH = 1, int D = 3>  // A4: x rows not 16-B aligned (K = 602): 4-B A DMA
-__global__ void __launch_bounds__(kBlock, (KH == 1 ? 3 : (D == 2 ? 2 : 1)))  // waves per SIMD = blocks per CU (LDS)
+__global__ void __launch_bounds__(kBlock, (KH == 1 ? (D == 2 ? 4 : 3) : (D == 2 ? 2 : 1)))  // waves per SIMD = blocks per CU (LDS)
 k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const float* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
           int vec_store, int tuning_prio = 0, int kslice = 0, int64_t slice_stride = 0) {
@@ -2725,8 +2725,9 @@ struct Tuning {
                             // can differ between processes: ranks could disagree bitwise); 0: its first choice
   int mm_ring = 1;          // fp32 UPDATE on k_mm_ring (LDS-DMA ring) instead of k_mm_rows
   int64_t mm_ring_blocks_per_cu = 0;  // k_mm_ring persistent grid: blocks per CU (0 = what LDS allows)
-  int mm_ring_form = 0;      // k_mm_ring stages: 0 = 16 k x 3 stages, 1 = 32 k x 2, 2 = 32 k x 3
+  int mm_ring_form = 0;      // k_mm_ring stages: 0 = 16 k x 3 stages, 1 = 32 k x 2, 2 = 32 k x 3, 3 = 16 k x 2
   int mm_ring_prio = 0;      // k_mm_ring: raise the wave priority around its MFMA block (+-3 %: noise, r02_mm_ab*)
+  int mm_ring_a16u = 1;      // k_mm_ring: 16-B A DMA pieces also when x rows are only 4-B aligned (K = 602)
   int mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
   int mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
   int64_t mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
@@ -2779,6 +2780,7 @@ const Knob* find_knob(const char* key) {
       {"mm_ring_blocks_per_cu", nullptr, &Tuning::mm_ring_blocks_per_cu},
       {"mm_ring_form", &Tuning::mm_ring_form, nullptr},
       {"mm_ring_prio", &Tuning::mm_ring_prio, nullptr},
+      {"mm_ring_a16u", &Tuning::mm_ring_a16u, nullptr},
       {"mm_blocks_per_cu", nullptr, &Tuning::mm_blocks_per_cu},
       {"apply_edge_form", &Tuning::apply_edge_form, nullptr},
       {"esm_lane", &Tuning::esm_lane, nullptr},
@@ -3577,12 +3579,12 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
     // persistent: at most 3 blocks per CU (48 KiB of LDS each at N = 128), every block the same
     // number of row groups (+-1)
     const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
-    const int64_t lds_blocks = tuning().mm_ring_form == 1 ? 2 : tuning().mm_ring_form == 2 ? 1 : 3;  // LDS per CU
+    const int64_t lds_blocks = tuning().mm_ring_form == 1 ? 2 : tuning().mm_ring_form == 2 ? 1 : tuning().mm_ring_form == 3 ? 4 : 3;  // LDS per CU
     const int64_t per_cu = tuning().mm_ring_blocks_per_cu > 0 ? tuning().mm_ring_blocks_per_cu : lds_blocks;
     const int64_t slots = std::max<int64_t>(1, 256 * per_cu / ncb);
     const int64_t rounds = (groups + slots - 1) / slots;
     const dim3 gr(static_cast<unsigned>(((groups + rounds - 1) / rounds) * ncb));
-    const bool a16 = aligned(x, 16) && ldx % 4 == 0;  // 16-B A pieces
+    const bool a16 = (aligned(x, 16) && ldx % 4 == 0) || tuning().mm_ring_a16u;  // 16-B A pieces
     const int form = tuning().mm_ring_form;  // 0: 16-k stages x 3; 1: 32-k stages x 2; 2: 32-k stages x 3
 #define GTA_RING(NT_, A4_, KH_, D_)                                                                              \
   k_mm_ring<NT_, A4_, KH_, D_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const float*>(x), ldx, row_idx, M, \
@@ -3590,7 +3592,8 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
                                                                    ldwt, static_cast<int>(N), sf, out, ldo,          \
                                                                    tuning().mm_vstore, tuning().mm_ring_prio)
 #define GTA_RING_F(NT_, A4_) \
-  if (form == 1) GTA_RING(NT_, A4_, 2, 2); else if (form == 2) GTA_RING(NT_, A4_, 2, 3); else GTA_RING(NT_, A4_, 1, 3)
+  if (form == 1) GTA_RING(NT_, A4_, 2, 2); else if (form == 2) GTA_RING(NT_, A4_, 2, 3); \
+  else if (form == 3) GTA_RING(NT_, A4_, 1, 2); else GTA_RING(NT_, A4_, 1, 3)
     if (nt == 8) { if (a16) { GTA_RING_F(8, false); } else { GTA_RING_F(8, true); } }
     else { if (a16) { GTA_RING_F(4, false); } else { GTA_RING_F(4, true); } }
 #undef GTA_RING_F
@@ -3665,7 +3668,7 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
     // ordered slice sum; for what the library does not take (gathered rows, SF, M < 1024). GCN Cora's
     // [2708 x 1433].[1433 x 128]: hipBLASLt 24-29 us, ring slices + sum 41 (33.7 + 7.0), k_mm_rows slices 46
     const dim3 gr(static_cast<unsigned>(groups * ncb), static_cast<unsigned>(nsl));
-    const bool a16 = aligned(x, 16) && ldx % 4 == 0;
+    const bool a16 = (aligned(x, 16) && ldx % 4 == 0) || tuning().mm_ring_a16u;
 #define GTA_RINGS(NT_, A4_)                                                                                    \
   k_mm_ring<NT_, A4_><<<gr, dim3(kBlock), 0, s>>>(static_cast<const float*>(x), ldx, row_idx, M, static_cast<int>(K), \
                                                   static_cast<const float*>(wt), ldwt, static_cast<int>(N), GTA_SF_NONE, \

@@ -12,12 +12,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops  # noqa: E402
 
-FORMS = {"ring": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 0},
-         "ring_prio": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 0, "mm_ring_prio": 1},
+FORMS = {"ring": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 0, "mm_ring_a16u": 0},
+         "ring_d2": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 3},
+         "ring_a16u": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 0, "mm_ring_a16u": 1},
          "rows": {"mm_blaslt": 0, "mm_ring": 0},
          "hipblaslt": {"mm_blaslt": 1, "mm_ring": 0, "mm_blaslt_tune": 1},
          "hipblaslt_top1": {"mm_blaslt": 1, "mm_ring": 0, "mm_blaslt_tune": 0}}
-DEFAULTS = {"mm_blaslt": 1, "mm_ring": 1, "mm_blaslt_tune": 0, "mm_ring_form": 0, "mm_ring_prio": 0}
+DEFAULTS = {"mm_blaslt": 1, "mm_ring": 1, "mm_blaslt_tune": 0, "mm_ring_form": 0, "mm_ring_prio": 0,
+            "mm_ring_a16u": 1}
 
 
 def main():
