@@ -2719,8 +2719,11 @@ struct Tuning {
   int plan_len_sort = 1;   // blocked plan: each block's items sorted by length (matched half-wave pairs)
   int att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
   int att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
-  int mm_blaslt = 1;        // plain fp32 UPDATE with M >= mm_blaslt_min_m on hipBLASLt (gta_update_mm_t)
+  int mm_blaslt = 1;        // plain fp32 UPDATE with mm_blaslt_min_m <= M <= mm_blaslt_max_m on hipBLASLt
   int64_t mm_blaslt_min_m = 1024;
+  int64_t mm_blaslt_max_m = 65535;  // from 65,536 rows (>= 512 row groups: >= 2 ring blocks per CU) k_mm_ring takes
+                                    // the product: 0.92-0.95x the library's first choice on Reddit / products shapes,
+                                    // equal on Flickr's, and bitwise the same in every process (profiles/r02_mm_ring_*)
   int mm_blaslt_tune = 0;  // 1: time the heuristic's top candidates at a shape's first use (faster, but the pick
                             // can differ between processes: ranks could disagree bitwise); 0: its first choice
   int mm_ring = 1;          // fp32 UPDATE on k_mm_ring (LDS-DMA ring) instead of k_mm_rows
@@ -2774,6 +2777,7 @@ const Knob* find_knob(const char* key) {
       {"mm_prefetch", &Tuning::mm_prefetch, nullptr},
       {"mm_blaslt", &Tuning::mm_blaslt, nullptr},
       {"mm_blaslt_min_m", nullptr, &Tuning::mm_blaslt_min_m},
+      {"mm_blaslt_max_m", nullptr, &Tuning::mm_blaslt_max_m},
       {"mm_blaslt_tune", &Tuning::mm_blaslt_tune, nullptr},
       {"mm_vstore", &Tuning::mm_vstore, nullptr},
       {"mm_ring", &Tuning::mm_ring, nullptr},
@@ -3568,6 +3572,7 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   if (dtype != GTA_F32 && dtype != GTA_BF16 && dtype != GTA_F32_BF16) return fail(GTA_ERR_ARG, "update_mm_t: bad dtype");
   if (M == 0) return GTA_OK;
   if (tuning().mm_blaslt && dtype == GTA_F32 && !row_idx && sf == GTA_SF_NONE && M >= tuning().mm_blaslt_min_m &&
+      M <= tuning().mm_blaslt_max_m &&
       blaslt_f32(static_cast<const float*>(x), ldx, M, K, static_cast<const float*>(wt), ldwt, N, out, ldo, S(stream))) {
     GTA_LAUNCHED("hipblaslt_matmul");
     return GTA_OK;
@@ -3576,14 +3581,16 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   const int64_t groups = (M + 127) / 128;
   if (tuning().mm_ring && dtype == GTA_F32 && nt >= 4 && K >= 32 && aligned(x, 4) && aligned(wt, 16) &&
       ldwt % 4 == 0) {
-    // persistent: at most 3 blocks per CU (48 KiB of LDS each at N = 128), every block the same
-    // number of row groups (+-1)
+    // persistent: at most 3 blocks per CU (48 KiB of LDS each at N = 128), every slot of every CU
+    // filled, so each CU gets the same number of row groups (+-1).  (Shrinking the grid to
+    // ceil(groups / rounds) blocks, every block the same count, left some CUs with one block more
+    // than others: at M = 232,965 95 CUs ran 9 groups while 161 ran 6, 84 TF/s against 98 with
+    // 2 blocks per CU, profiles/r02_mm_ring_probe.json.)
     const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
     const int64_t lds_blocks = tuning().mm_ring_form == 1 ? 2 : tuning().mm_ring_form == 2 ? 1 : tuning().mm_ring_form == 3 ? 4 : 3;  // LDS per CU
     const int64_t per_cu = tuning().mm_ring_blocks_per_cu > 0 ? tuning().mm_ring_blocks_per_cu : lds_blocks;
     const int64_t slots = std::max<int64_t>(1, 256 * per_cu / ncb);
-    const int64_t rounds = (groups + slots - 1) / slots;
-    const dim3 gr(static_cast<unsigned>(((groups + rounds - 1) / rounds) * ncb));
+    const dim3 gr(static_cast<unsigned>(std::min(groups, slots) * ncb));
     const bool a16 = (aligned(x, 16) && ldx % 4 == 0) || tuning().mm_ring_a16u;  // 16-B A pieces
     const int form = tuning().mm_ring_form;  // 0: 16-k stages x 3; 1: 32-k stages x 2; 2: 32-k stages x 3
 #define GTA_RING(NT_, A4_, KH_, D_)                                                                              \
@@ -3658,6 +3665,7 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
   const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
   hipStream_t s = S(stream);
   if (tuning().mm_blaslt && dtype == GTA_F32 && !row_idx && sf == GTA_SF_NONE && M >= tuning().mm_blaslt_min_m &&
+      M <= tuning().mm_blaslt_max_m &&
       blaslt_f32(static_cast<const float*>(x), ldx, M, K, static_cast<const float*>(wt), ldwt, N, out, ldo, S(stream))) {
     GTA_LAUNCHED("hipblaslt_matmul");
     return GTA_OK;

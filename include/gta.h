@@ -228,8 +228,11 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
  * through a 3-stage ring (persistent blocks, the ring running on across row groups);
  * otherwise k_mm_rows (x fragments straight to registers, wt staged per K chunk).  Both
  * contract k in the same order: bitwise equal to each other, fp32 rounding away from
- * gta_update_mm.  A plain fp32 product (GTA_F32, row_idx NULL, GTA_SF_NONE, M >= 1024) runs
- * on hipBLASLt instead, with the library heuristic's FIRST choice for the shape: the same
+ * gta_update_mm.  x rows need only 4-B alignment (K = 602: 16-B DMA pieces at 8-B aligned
+ * addresses).  From 65,536 rows every fp32 product runs k_mm_ring (>= 2 blocks per CU).  A plain
+ * fp32 product (GTA_F32, row_idx NULL, GTA_SF_NONE) with 1024 <= M < 65,536 (tuning knobs
+ * mm_blaslt_min_m / mm_blaslt_max_m) runs on hipBLASLt instead, where the ring cannot fill the
+ * chip, with the library heuristic's FIRST choice for the shape: the same
  * algorithm in every process, so ranks agree bitwise (tuning knob mm_blaslt_tune = 1 times the
  * top candidates instead: faster, but the pick may then differ between processes).  The
  * library's per-device handle and workspace are created at the device's first plain fp32 call;

@@ -16,10 +16,10 @@ FORMS = {"ring": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 0, "mm_ring_a16u
          "ring_d2": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 3},
          "ring_a16u": {"mm_blaslt": 0, "mm_ring": 1, "mm_ring_form": 0, "mm_ring_a16u": 1},
          "rows": {"mm_blaslt": 0, "mm_ring": 0},
-         "hipblaslt": {"mm_blaslt": 1, "mm_ring": 0, "mm_blaslt_tune": 1},
-         "hipblaslt_top1": {"mm_blaslt": 1, "mm_ring": 0, "mm_blaslt_tune": 0}}
+         "hipblaslt": {"mm_blaslt": 1, "mm_ring": 0, "mm_blaslt_tune": 1, "mm_blaslt_max_m": 1 << 62},
+         "hipblaslt_top1": {"mm_blaslt": 1, "mm_ring": 0, "mm_blaslt_tune": 0, "mm_blaslt_max_m": 1 << 62}}
 DEFAULTS = {"mm_blaslt": 1, "mm_ring": 1, "mm_blaslt_tune": 0, "mm_ring_form": 0, "mm_ring_prio": 0,
-            "mm_ring_a16u": 1}
+            "mm_ring_a16u": 1, "mm_blaslt_max_m": 65535}
 
 
 def main():

@@ -797,9 +797,10 @@ def test_aggregate_blocked_fused_reduce_bitwise(dev, heads, accumulate):
 def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     """k_mm_ring (fp32 UPDATE through the 3-stage LDS-DMA ring, the default for plain fp32 GEMMs)
     == k_mm_rows bitwise (same per-lane k order and MFMA chain), and both within the fp64 bound:
-    K tails, rows past M, columns past N (two column blocks at N = 200), gathered rows, SF epilogues,
-    x rows not 16-B aligned (K = 602, 1433: the 4-B A-DMA form).  Shapes with enough row groups not
-    to take the split-K form."""
+    K tails (register steps of 16 k), rows past M, columns
+    past N (two column blocks at N = 200), gathered rows, SF epilogues, x rows not 16-B aligned
+    (K = 602, 1433: 16-B DMA pieces at 8-B aligned addresses by default, the 4-B A-DMA form with
+    mm_ring_a16u = 0), every stage form.  Shapes with enough row groups not to take the split-K form."""
     assert ops._mm_splits(M, K, N) == 1
     rng = np.random.default_rng(M + K + N)
     x = torch.from_numpy(rng.standard_normal((M + 5, K)).astype(np.float32))
@@ -812,13 +813,16 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     try:
         ops.MM_ROWS_MIN_M = 0
         ops.set_debug("mm_blaslt", 0)
-        for ring, form in ((0, 0), (1, 0), (1, 1), (1, 2)):  # k_mm_rows, then the ring's three stage forms
+        # k_mm_rows, then the ring's four stage forms, then the 4-B A-DMA path
+        for ring, form, a16u in ((0, 0, 1), (1, 0, 1), (1, 1, 1), (1, 2, 1), (1, 3, 1), (1, 0, 0)):
             ops.set_debug("mm_ring", ring)
             ops.set_debug("mm_ring_form", form)
+            ops.set_debug("mm_ring_a16u", a16u)
             outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
     finally:
         ops.set_debug("mm_ring", 1)
         ops.set_debug("mm_ring_form", 0)
+        ops.set_debug("mm_ring_a16u", 1)
         ops.set_debug("mm_blaslt", 1)
         ops.MM_ROWS_MIN_M = old_min
     torch.cuda.synchronize()
@@ -827,6 +831,30 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     xs = x.numpy()[idx.numpy()] if gathered else x.numpy()[:M]
     ref = isa_ref.mm(xs, w.numpy(), sf_kind=sf)
     _check(outs[1], ref, np.abs(xs).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "k_mm_ring")
+
+
+@pytest.mark.parametrize("M,K", [(70000, 602), (65536, 100)])
+def test_update_mm_default_is_the_ring(dev, M, K):
+    """From 65,536 rows the DEFAULT plain fp32 UPDATE (no knobs touched) is the hand-written
+    k_mm_ring, not the library: bitwise equal to k_mm_rows (the library's contraction order
+    differs), and within the fp64 bound."""
+    rng = np.random.default_rng(M + K)
+    x = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32))
+    w = torch.from_numpy((rng.standard_normal((K, 128)) / np.sqrt(K)).astype(np.float32))
+    xd, wd = x.to(dev), w.to(dev)
+    y = ops.update_mm(xd, wd)
+    try:
+        ops.set_debug("mm_blaslt", 0)
+        ops.set_debug("mm_ring", 0)
+        y_rows = ops.update_mm(xd, wd)
+    finally:
+        ops.set_debug("mm_ring", 1)
+        ops.set_debug("mm_blaslt", 1)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y_rows)
+    rows = np.arange(0, M, 97)
+    ref = isa_ref.mm(x.numpy()[rows], w.numpy())
+    _check(y[rows], ref, np.abs(x.numpy()[rows]).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "default UPDATE")
 
 
 @pytest.mark.parametrize("M,K,N,gathered,sf", [(2708, 1433, 128, False, None), (2708, 1433, 128, True, "RELU"),
