@@ -237,7 +237,9 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
  * top candidates instead: faster, but the pick may then differ between processes).  The
  * library's per-device handle and workspace are created at the device's first plain fp32 call;
  * a call made while the stream is being captured into a graph never creates them (nor times
- * anything) and runs the hand-written kernel instead.  Also applies to gta_update_mm_t_split. */
+ * anything) and runs the hand-written kernel instead.  The device's first plain fp32 call of that
+ * size range must not overlap a GLOBAL-mode capture running on another stream (hipMalloc of the
+ * workspace would invalidate it): warm up outside captures, as executor.GraphedRun does.  Also applies to gta_update_mm_t_split. */
 int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                     int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream);
 
