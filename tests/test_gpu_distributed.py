@@ -75,3 +75,20 @@ def test_two_rank_bench_full_size(mode):
     assert rec["n_gpus"] == 2 and rec["config"]["mode"] == mode and rec["config"]["world_size_seen"] == 2
     assert rec["config"]["N"] == 232965 and rec["config"]["E"] == 114615892
     assert rec["parity"]["ok"] and rec["parity"]["max_err_over_bound"] <= 1.0, rec["parity"]
+
+
+@pytest.mark.gpu
+def test_rccl_collectives_as_bench_makes_them():
+    """RCCL itself (backend "nccl") on the box's GPU: bench.py's reduce-scatter / all-gather /
+    all-reduce calls with its chunk-major layouts, in a torch.distributed.run process group of one
+    rank per GPU (one GPU here: world 1, the group and the async work handles still go through RCCL)."""
+    import torch
+    n = torch.cuda.device_count()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(min(n, 2)),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
+           os.path.join(ROOT, "scripts", "rccl_smoke.py")]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
+    res = json.loads(line)
+    assert res["backend"] == "nccl" and res["reduce_scatter_ok"] and res["all_gather_ok"] and res["all_reduce_ok"]
