@@ -421,6 +421,25 @@ def main():
         b.record(stream)
     torch.cuda.synchronize()
     kern_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    # the same launches split by phase (knob seg_phase: 1 = the gather items only, 2 = the ordered
+    # reduce only, reading the slabs the items just wrote): per-kernel times for the roofline
+    phase_ms = None
+    if agg.impl == "blocked":
+        pev = {1: [], 2: []}
+        try:
+            for _ in range(n_evt):
+                for ph in (1, 2):
+                    ops.set_debug("seg_phase", ph)
+                    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                    a.record(stream)
+                    for c in range(len(agg.parts)):
+                        agg.launch(c)
+                    b.record(stream)
+                    pev[ph].append((a, b))
+        finally:
+            ops.set_debug("seg_phase", 0)
+        torch.cuda.synchronize()
+        phase_ms = {ph: float(np.mean([a.elapsed_time(b) for a, b in v])) for ph, v in pev.items()}
 
     # timed region: K steps, barrier + sync on both sides, max over ranks
     if world > 1:
@@ -484,6 +503,11 @@ def main():
             roof["traffic_split"] = {"agg": pmc["agg_bytes"], "reduce": pmc["reduce_bytes"],
                                      "read_factor": pmc["read_factor"], "write_factor": pmc["write_factor"]}
             roof["traffic_method"] = pmc["method"]
+            if phase_ms is not None:  # each kernel alone: its PMC bytes over its own HIP-event time
+                roof["per_kernel"] = {
+                    name: {"ms": phase_ms[ph], "traffic": byt, "achieved": byt / (phase_ms[ph] / 1e3) / 1e9,
+                           "frac": byt / (phase_ms[ph] / 1e3) / 1e9 / PEAK_HBM_GBS}
+                    for name, ph, byt in (("k_agg_h32", 1, pmc["agg_bytes"]), ("k_seg_reduce", 2, pmc["reduce_bytes"]))}
 
     if mode == "single":
         par = "one GPU, whole graph"
