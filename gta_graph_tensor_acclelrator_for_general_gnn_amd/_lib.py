@@ -10,7 +10,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgta.so")
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # enum mirrors of include/gta.h
 GTA_F32, GTA_BF16, GTA_F32_BF16 = 0, 1, 2
@@ -53,6 +53,11 @@ SIGNATURES = {
     "gta_tile_nnz": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
     "gta_debug_set": (_i32, [_cp, _i64]),
     "gta_debug_get": (_i32, [_cp, ctypes.POINTER(_i64)]),
+    "gta_tuning_create": (_vp, []),
+    "gta_tuning_destroy": (None, [_vp]),
+    "gta_tuning_set": (_i32, [_vp, _cp, _i64]),
+    "gta_tuning_get": (_i32, [_vp, _cp, ctypes.POINTER(_i64)]),
+    "gta_tuning_attach": (_i32, [_vp, _vp]),
 }
 
 _lock = threading.Lock()

@@ -10,6 +10,7 @@
 #include <hipblaslt/hipblaslt.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdint>
 #include <map>
 #include <mutex>
@@ -2743,10 +2744,36 @@ struct Tuning {
                              // pass it removes; profiles/r02_fused_reduce_ab.json); 2 = the same at 6 waves/SIMD
 };
 
-Tuning& tuning() {
+Tuning& thread_tuning() {  // gta_debug_set / gta_debug_get: the calling thread's knobs
   thread_local Tuning t;
   return t;
 }
+
+// Knob sets attached to streams (gta_tuning_attach): a call on an attached stream reads a copy
+// of that set, taken at the call's entry, from whichever thread it comes; other calls read the
+// calling thread's knobs.  g_attached_n keeps the common case (nothing attached) lock-free.
+std::mutex g_attach_mu;
+std::map<void*, Tuning> g_attached;
+std::atomic<int> g_attached_n{0};
+thread_local const Tuning* t_call = nullptr;
+
+struct CallTuning {
+  const Tuning* prev = t_call;
+  Tuning snap;
+  explicit CallTuning(void* stream) {
+    if (g_attached_n.load(std::memory_order_acquire) == 0) return;
+    std::lock_guard<std::mutex> lk(g_attach_mu);
+    auto it = g_attached.find(stream);
+    if (it == g_attached.end()) return;
+    snap = it->second;
+    t_call = &snap;
+  }
+  ~CallTuning() { t_call = prev; }
+  CallTuning(const CallTuning&) = delete;
+  CallTuning& operator=(const CallTuning&) = delete;
+};
+
+const Tuning& tuning() { return t_call ? *t_call : thread_tuning(); }
 
 // Tuning hooks (gta.h): the calling thread's knobs, by name
 struct Knob {
@@ -2809,15 +2836,50 @@ const char* gta_last_error(void) { return g_err.c_str(); }
 int gta_debug_set(const char* key, int64_t value) {
   const Knob* kb = find_knob(key);
   if (!kb) return fail(GTA_ERR_ARG, std::string("gta_debug_set: unknown key ") + (key ? key : ""));
-  if (kb->i32) tuning().*(kb->i32) = static_cast<int>(value);
-  else tuning().*(kb->i64) = value;
+  if (kb->i32) thread_tuning().*(kb->i32) = static_cast<int>(value);
+  else thread_tuning().*(kb->i64) = value;
   return GTA_OK;
 }
 
 int gta_debug_get(const char* key, int64_t* value) {
   const Knob* kb = find_knob(key);
   if (!kb || !value) return fail(GTA_ERR_ARG, std::string("gta_debug_get: unknown key ") + (key ? key : ""));
-  *value = kb->i32 ? static_cast<int64_t>(tuning().*(kb->i32)) : tuning().*(kb->i64);
+  *value = kb->i32 ? static_cast<int64_t>(thread_tuning().*(kb->i32)) : thread_tuning().*(kb->i64);
+  return GTA_OK;
+}
+
+}  // extern "C"
+
+struct gta_tuning {  // a knob set (gta.h): the defaults until gta_tuning_set
+  Tuning t;
+};
+
+extern "C" {
+
+gta_tuning* gta_tuning_create(void) { return new (std::nothrow) gta_tuning{}; }
+
+void gta_tuning_destroy(gta_tuning* h) { delete h; }
+
+int gta_tuning_set(gta_tuning* h, const char* key, int64_t value) {
+  const Knob* kb = find_knob(key);
+  if (!h || !kb) return fail(GTA_ERR_ARG, std::string("gta_tuning_set: bad handle or unknown key ") + (key ? key : ""));
+  if (kb->i32) h->t.*(kb->i32) = static_cast<int>(value);
+  else h->t.*(kb->i64) = value;
+  return GTA_OK;
+}
+
+int gta_tuning_get(const gta_tuning* h, const char* key, int64_t* value) {
+  const Knob* kb = find_knob(key);
+  if (!h || !kb || !value) return fail(GTA_ERR_ARG, std::string("gta_tuning_get: bad arguments ") + (key ? key : ""));
+  *value = kb->i32 ? static_cast<int64_t>(h->t.*(kb->i32)) : h->t.*(kb->i64);
+  return GTA_OK;
+}
+
+int gta_tuning_attach(void* stream, const gta_tuning* h) {
+  std::lock_guard<std::mutex> lk(g_attach_mu);
+  if (h) g_attached[stream] = h->t;
+  else g_attached.erase(stream);
+  g_attached_n.store(static_cast<int>(g_attached.size()), std::memory_order_release);
   return GTA_OK;
 }
 
@@ -2833,6 +2895,7 @@ int64_t gta_aggregate_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t chunk
 
 int gta_aggregate_plan_build(const int64_t* indptr, int64_t n_rows, int64_t nnz, int64_t chunk, void* plan,
                              int64_t plan_bytes, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (!indptr || !plan || n_rows <= 0 || chunk <= 0 || (chunk % kWave) != 0)
     return fail(GTA_ERR_ARG, "plan_build: need indptr, plan, n_rows > 0 and chunk a positive multiple of 64");
   const int64_t mi = max_items_for(n_rows, nnz, chunk);
@@ -2851,6 +2914,7 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
                      const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
                   const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
                   int64_t plan_chunk, void* workspace, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n_rows < 0 || nnz < 0 || F <= 0) return fail(GTA_ERR_ARG, "aggregate: bad sizes");
   if (x_mode != GTA_IDX_EDGE && x_mode != GTA_IDX_SRC && x_mode != GTA_IDX_DST)
     return fail(GTA_ERR_ARG, "aggregate: bad x_mode");
@@ -2959,6 +3023,7 @@ int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t nnz, int64_t bl
 int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
                                      int64_t nnz, int64_t blocks, int64_t item_edges, int64_t row_edges, void* plan,
                                      int64_t plan_bytes, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (!indptr || !plan || n_rows <= 0 || n_cols <= 0 || nnz < 0 || blocks < 1 || blocks > 63 || item_edges < 1 ||
       row_edges < 0)
     return fail(GTA_ERR_ARG, "blocked_plan_build: bad arguments");
@@ -3017,6 +3082,7 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
                           const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
                           const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
                           int64_t blocks, int64_t item_edges, void* workspace, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n_rows < 0 || nnz < 0 || F <= 0 || blocks < 1 || blocks > 63 || item_edges < 1)
     return fail(GTA_ERR_ARG, "aggregate_blocked: bad sizes");
   if (n_rows == 0) return GTA_OK;
@@ -3183,6 +3249,7 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
                               const float* b_src, int64_t ldb, int64_t heads, int sf, int normalize, float* y,
                               int64_t ldy, float* sums, const void* plan, int64_t blocks, int64_t item_edges,
                               void* workspace, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n_rows < 0 || nnz < 0 || blocks < 1 || blocks > 63 || heads <= 0 || lda < heads || ldb < heads ||
       item_edges < 1)
     return fail(GTA_ERR_ARG, "gat_aggregate_blocked: bad sizes");
@@ -3253,12 +3320,14 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
 
 int gta_gather_add(const int64_t* indptr, int64_t n_rows, int64_t nnz, const float* xe, int64_t ldxe, int64_t F,
                    float* y, int64_t ldy, int accumulate, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   return gta_aggregate(indptr, nullptr, n_rows, nnz, GTA_IDX_EDGE, xe, ldxe, F, nullptr, 0, 0, nullptr, y, ldy,
                           accumulate, nullptr, 0, nullptr, stream);
 }
 
 int gta_scatter(int dir, const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, const void* x,
                 int64_t ldx, int64_t F, int dtype, void* out, int64_t ldo, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n_rows < 0 || nnz < 0 || F <= 0) return fail(GTA_ERR_ARG, "scatter: bad sizes");
   if (dir != GTA_DIR_R && dir != GTA_DIR_C) return fail(GTA_ERR_ARG, "scatter: bad dir");
   const int esz = (dtype == GTA_BF16) ? 2 : (dtype == GTA_F32 ? 4 : 0);
@@ -3303,6 +3372,7 @@ static int check_bcast(int64_t Fa, int64_t Fb, bool has_b, int64_t* Fo) {
 int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
                    const float* a, int a_mode, int64_t lda, int64_t Fa, const float* b, int b_mode, int64_t ldb,
                    int64_t Fb, float* out, int64_t ldo, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n_rows < 0 || nnz < 0 || Fa <= 0) return fail(GTA_ERR_ARG, "apply_edge: bad sizes");
   if (n_rows == 0 || nnz == 0) return GTA_OK;  // no edge: nothing to write (operands may be NULL)
   if (!indptr || !a || !out) return fail(GTA_ERR_ARG, "apply_edge: bad arguments");
@@ -3343,6 +3413,7 @@ int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indice
 
 int gta_apply_node(int bin, int sf, int64_t n, const float* a, int64_t lda, int64_t Fa, const float* b, int64_t ldb,
                    int64_t Fb, float* out, int64_t ldo, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n < 0 || Fa <= 0) return fail(GTA_ERR_ARG, "apply_node: bad sizes");
   if (n == 0) return GTA_OK;
   if (!a || !out) return fail(GTA_ERR_ARG, "apply_node: bad arguments");
@@ -3371,6 +3442,7 @@ int gta_apply_node(int bin, int sf, int64_t n, const float* a, int64_t lda, int6
 int gta_edge_softmax(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
                      const float* a_dst, int64_t lda, const float* b_src, int64_t ldb, int64_t heads, int sf,
                      int normalize, float* out, float* sums, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (!indptr || !a_dst || !b_src || n_rows < 0 || nnz < 0 || (nnz > 0 && (!indices || !out)))
     return fail(GTA_ERR_ARG, "edge_softmax: bad arguments");
   if (heads <= 0 || heads > kWave || (heads & (heads - 1)))
@@ -3407,6 +3479,7 @@ int gta_edge_softmax(const int64_t* indptr, const int32_t* indices, int64_t n_ro
 
 int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* w,
                   int64_t ldw, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (M < 0 || K <= 0 || N <= 0) return fail(GTA_ERR_ARG, "update_mm: bad sizes");
   if (M == 0) return GTA_OK;
   if (!x || !w || !out) return fail(GTA_ERR_ARG, "update_mm: bad arguments");
@@ -3565,6 +3638,7 @@ bool blaslt_f32(const float* x, int64_t ldx, int64_t M, int64_t K, const float* 
 
 int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                     int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (M < 0 || K <= 0 || N <= 0 || ldwt < K) return fail(GTA_ERR_ARG, "update_mm_t: bad sizes");
   if (M == 0) return GTA_OK;
   if (!x || !wt || !out) return fail(GTA_ERR_ARG, "update_mm_t: bad arguments");
@@ -3650,6 +3724,7 @@ int64_t gta_update_mm_t_split_workspace_bytes(int64_t M, int64_t K, int64_t N, i
 int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                           int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, int64_t splits,
                           void* workspace, int64_t workspace_bytes, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (M < 0 || K <= 0 || N <= 0 || ldwt < K || splits < 1) return fail(GTA_ERR_ARG, "update_mm_t_split: bad sizes");
   if (M == 0) return GTA_OK;
   if (!x || !wt || !out || !workspace) return fail(GTA_ERR_ARG, "update_mm_t_split: bad arguments");
@@ -3712,6 +3787,7 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
 
 int gta_tile_nnz(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols, int64_t T,
                  int32_t* counts, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (!indptr || !counts || n_rows < 0 || n_cols <= 0 || T <= 0)
     return fail(GTA_ERR_ARG, "tile_nnz: bad arguments");
   if (n_rows == 0) return GTA_OK;

@@ -512,3 +512,45 @@ def get_debug(key):
     v = ctypes.c_int64(0)
     check(_L().gta_debug_get(key.encode(), ctypes.byref(v)), "debug_get")
     return int(v.value)
+
+
+class Tuning:
+    """A libgta knob set scoped to a STREAM (include/gta.h gta_tuning_*): attach(stream) copies
+    these values onto the stream, and every call made on it -- from any thread -- then reads them
+    instead of the calling thread's knobs (set_debug).  Change a value, attach again to apply it;
+    detach(stream) drops the stream's set.  Unknown keys raise GTAError."""
+
+    def __init__(self, **knobs):
+        self._lib = _L()
+        self._h = self._lib.gta_tuning_create()
+        if not self._h:
+            raise _lib.GTAError("gta_tuning_create failed")
+        for k, v in knobs.items():
+            self.set(k, v)
+
+    def set(self, key, value):
+        check(self._lib.gta_tuning_set(self._h, key.encode(), int(value)), "tuning_set")
+        return self
+
+    def get(self, key):
+        import ctypes
+        v = ctypes.c_int64(0)
+        check(self._lib.gta_tuning_get(self._h, key.encode(), ctypes.byref(v)), "tuning_get")
+        return int(v.value)
+
+    @staticmethod
+    def _ptr(stream):
+        """A torch.cuda.Stream, or a raw hipStream_t value (int; 0 = the null stream)."""
+        return stream.cuda_stream if hasattr(stream, "cuda_stream") else int(stream)
+
+    def attach(self, stream):
+        check(self._lib.gta_tuning_attach(self._ptr(stream), self._h), "tuning_attach")
+
+    @classmethod
+    def detach(cls, stream):
+        check(_L().gta_tuning_attach(cls._ptr(stream), None), "tuning_attach")
+
+    def __del__(self):
+        h, self._h = getattr(self, "_h", None), None
+        if h:
+            self._lib.gta_tuning_destroy(h)

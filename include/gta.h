@@ -37,8 +37,9 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 3  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
-                              hooks, blocked workspace holds per-row arrival counters */
+#define GTA_ABI_VERSION 4  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+                              hooks, blocked workspace holds per-row arrival counters; 4: knob sets
+                              attached to streams (gta_tuning_*) */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -78,6 +79,20 @@ const char* gta_last_error(void);
  * values, so the library keeps no process-wide mutable state.  Unknown key: GTA_ERR_ARG. */
 int gta_debug_set(const char* key, int64_t value);
 int gta_debug_get(const char* key, int64_t* value);
+
+/* Knob sets scoped to a STREAM (ABI 4): a handle holds a full set of knobs (the defaults until
+ * set); gta_tuning_attach(stream, h) copies h's values onto the stream, and from then on every
+ * call made on that stream -- from any thread -- reads that copy, taken at the call's entry,
+ * instead of the calling thread's knobs.  h may be changed or destroyed after attaching (attach
+ * again to apply changes); h == NULL detaches.  Streams without an attached set use the calling
+ * thread's knobs (gta_debug_set), so concurrent calls on different streams never see each
+ * other's settings. */
+typedef struct gta_tuning gta_tuning;
+gta_tuning* gta_tuning_create(void);
+void gta_tuning_destroy(gta_tuning* h);
+int gta_tuning_set(gta_tuning* h, const char* key, int64_t value);
+int gta_tuning_get(const gta_tuning* h, const char* key, int64_t* value);
+int gta_tuning_attach(void* stream, const gta_tuning* h);
 
 /* ---- K1 SCATTER (node -> edge copy) -------------------------------------
  * out[e, :] = x[dir==R ? dst(e) : src(e), :]          (bit-exact copy)

@@ -77,3 +77,24 @@ def test_tuning_knobs_are_per_thread(lib):
         ops.set_debug("no_such_knob", 1)
     with pytest.raises(_lib.GTAError):
         ops.get_debug("no_such_knob")
+
+
+def test_tuning_handles(lib):
+    """ABI 4 knob sets (gta_tuning_*): a handle starts at the defaults, holds its own values apart
+    from the thread's knobs, rejects unknown keys, and attaches to / detaches from a stream key
+    (the pointer is only a key here: no device work)."""
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
+    thread_val = ops.get_debug("seg_lean")
+    t = ops.Tuning(seg_lean=1 - thread_val, mm_blaslt_max_m=1 << 40)
+    assert t.get("seg_lean") == 1 - thread_val and t.get("mm_blaslt_max_m") == 1 << 40
+    assert ops.Tuning().get("mm_blaslt_max_m") == 65535  # a fresh handle holds the defaults
+    assert ops.get_debug("seg_lean") == thread_val        # the thread's knobs are untouched
+    with pytest.raises(_lib.GTAError):
+        t.set("no_such_knob", 1)
+    with pytest.raises(_lib.GTAError):
+        t.get("no_such_knob")
+    fake_stream = 0x1234560
+    t.attach(fake_stream)
+    del t                                                # the stream holds a copy: safe to destroy
+    ops.Tuning.detach(fake_stream)
+    ops.Tuning.detach(fake_stream)                       # detaching twice is harmless

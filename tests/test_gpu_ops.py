@@ -857,6 +857,52 @@ def test_update_mm_default_is_the_ring(dev, M, K):
     _check(y[rows], ref, np.abs(x.numpy()[rows]).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "default UPDATE")
 
 
+def test_tuning_attached_to_a_stream(dev):
+    """ABI 4: a knob set attached to a stream governs every call on that stream, from any thread,
+    and nothing else.  Observable through the UPDATE route at 70,000 rows: the default is the ring
+    (bitwise k_mm_rows); a set with mm_blaslt_max_m raised sends it to the library (other rounding,
+    bitwise equal to the same route chosen by the thread knob)."""
+    import threading
+    rng = np.random.default_rng(7)
+    x = torch.from_numpy(rng.standard_normal((70000, 602)).astype(np.float32)).to(dev)
+    w = torch.from_numpy((rng.standard_normal((602, 128)) / np.sqrt(602)).astype(np.float32)).to(dev)
+    y_ring = ops.update_mm(x, w)
+    try:
+        ops.set_debug("mm_blaslt_max_m", 1 << 40)
+        y_lib = ops.update_mm(x, w)
+    finally:
+        ops.set_debug("mm_blaslt_max_m", 65535)
+    torch.cuda.synchronize()
+    assert not torch.equal(y_ring, y_lib)  # the two routes round differently
+    s = torch.cuda.Stream(dev)
+    t = ops.Tuning(mm_blaslt_max_m=1 << 40)
+    t.attach(s)
+    try:
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(s):
+            y_att = ops.update_mm(x, w)
+        out = {}
+
+        def other():
+            with torch.cuda.stream(s):
+                out["y"] = ops.update_mm(x, w)
+            s.synchronize()
+        th = threading.Thread(target=other)
+        th.start()
+        th.join()
+        y_plain = ops.update_mm(x, w)  # the current stream: nothing attached
+        s.synchronize()
+        torch.cuda.synchronize()
+        assert torch.equal(y_att, y_lib) and torch.equal(out["y"], y_lib)
+        assert torch.equal(y_plain, y_ring)
+    finally:
+        ops.Tuning.detach(s)
+    with torch.cuda.stream(s):
+        y_det = ops.update_mm(x, w)
+    s.synchronize()
+    assert torch.equal(y_det, y_ring)
+
+
 @pytest.mark.parametrize("M,K,N,gathered,sf", [(2708, 1433, 128, False, None), (2708, 1433, 128, True, "RELU"),
                                                (2708, 1432, 64, False, None), (1000, 1350, 64, False, None),
                                                (600, 1000, 200, False, "ELU"), (900, 700, 66, False, None)])
