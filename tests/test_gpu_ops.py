@@ -857,6 +857,40 @@ def test_update_mm_default_is_the_ring(dev, M, K):
     _check(y[rows], ref, np.abs(x.numpy()[rows]).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "default UPDATE")
 
 
+@pytest.mark.parametrize("K,off", [(602, 1), (500, 3), (128, 1)])
+def test_update_mm_ring_4b_aligned_rows(dev, K, off):
+    """x a column window of a wider table (ldx = K + 4 + off, base off * 4 B into the row): every
+    row start only 4-B aligned, as the ring's 16-B A DMA pieces allow.  Ring (16-B and 4-B A
+    pieces) == k_mm_rows bitwise, within the fp64 bound."""
+    M, N = 40000, 128  # enough row groups for the one-pass ring (no split-K)
+    rng = np.random.default_rng(K + off)
+    big = torch.from_numpy(rng.standard_normal((M, K + 4 + off)).astype(np.float32))
+    w = torch.from_numpy((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32))
+    bd, wd = big.to(dev), w.to(dev)
+    xd = bd[:, off:off + K]
+    assert xd.stride(0) == K + 4 + off and xd.data_ptr() % 16 != 0 and ops._mm_splits(M, K, N) == 1
+    outs = []
+    old_min = ops.MM_ROWS_MIN_M
+    try:
+        ops.MM_ROWS_MIN_M = 0
+        ops.set_debug("mm_blaslt", 0)
+        for ring, a16u in ((0, 1), (1, 1), (1, 0)):
+            ops.set_debug("mm_ring", ring)
+            ops.set_debug("mm_ring_a16u", a16u)
+            outs.append(ops.update_mm(xd, wd))
+    finally:
+        ops.set_debug("mm_ring", 1)
+        ops.set_debug("mm_ring_a16u", 1)
+        ops.set_debug("mm_blaslt", 1)
+        ops.MM_ROWS_MIN_M = old_min
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
+    xs = big.numpy()[:, off:off + K]
+    ref = isa_ref.mm(xs, w.numpy())
+    _check(outs[1], ref, np.abs(xs).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "ring, 4-B aligned rows")
+
+
 def test_tuning_attached_to_a_stream(dev):
     """ABI 4: a knob set attached to a stream governs every call on that stream, from any thread,
     and nothing else.  Observable through the UPDATE route at 70,000 rows: the default is the ring
