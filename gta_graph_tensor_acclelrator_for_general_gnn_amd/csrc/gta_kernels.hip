@@ -11,6 +11,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <cstdint>
 #include <map>
 #include <mutex>
@@ -2383,8 +2384,10 @@ __device__ __forceinline__ void ds_read16_dyn(f32x4& v, uint32_t a, int c) {  //
 }
 
 // KH: 16-k halves per ring stage (1: 16-k stages, 2: 32-k stages, half the barriers); D: stages
-template <int NT, bool A4 = false, int KH = 1, int D = 3>  // A4: x rows not 16-B aligned (K = 602): 4-B A DMA
-__global__ void __launch_bounds__(kBlock, (KH == 1 ? (D == 2 ? 4 : 3) : (D == 2 ? 2 : 1)))  // waves per SIMD = blocks per CU (LDS)
+// FR: 16-row A fragments per wave (2: 128-row groups; 1: 64-row groups, twice as many work units
+// for the per-CU balance, half the MFMAs per B-fragment read)
+template <int NT, bool A4 = false, int KH = 1, int D = 3, int FR = 2>  // A4: x rows not 16-B aligned: 4-B A DMA
+__global__ void __launch_bounds__(kBlock, (FR == 1 ? 4 : (KH == 1 ? (D == 2 ? 4 : 3) : (D == 2 ? 2 : 1))))  // waves per SIMD = blocks per CU (LDS)
 k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const float* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
           int vec_store, int tuning_prio = 0, int kslice = 0, int64_t slice_stride = 0) {
@@ -2397,10 +2400,11 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     out += static_cast<int64_t>(blockIdx.y) * slice_stride;
   }
   static_assert(KH == 1 || KH == 2, "16- or 32-k stages");
-  constexpr int KS = 16 * KH, BN = 16 * NT;
+  static_assert(FR == 1 || FR == 2, "one or two A fragments per wave");
+  constexpr int KS = 16 * KH, BN = 16 * NT, GR = 64 * FR;  // GR: rows per group
   // stage image: A [wave][i][h] then B [c][h], 1 KiB fragments (16 rows x 16 k)
-  constexpr int A_BYTES = 4 * 2 * KH * 1024, STAGE = A_BYTES + NT * KH * 1024;
-  constexpr int PER_STAGE = KH * ((A4 ? 8 : 2) + NT / 4);  // DMA instructions per wave per stage
+  constexpr int A_BYTES = 4 * FR * KH * 1024, STAGE = A_BYTES + NT * KH * 1024;
+  constexpr int PER_STAGE = KH * ((A4 ? 4 * FR : FR) + NT / 4);  // DMA instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char lds[D * STAGE];
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = wave_id_uniform();
@@ -2411,7 +2415,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   // them (stage t = (group j, 16-k step s)), so the next group's first stages land while this
   // group finishes and no block pays a prologue after the first
   const int64_t grp0 = blockIdx.x / ncb, gstep = gridDim.x / ncb;
-  const int64_t n_groups = (M + 127) / 128;
+  const int64_t n_groups = (M + GR - 1) / GR;
   const int64_t my_groups = grp0 < n_groups ? (n_groups - grp0 + gstep - 1) / gstep : 0;
   const int S = K / KS;  // whole stages per group (a K tail: register steps of 16 k)
   const int64_t T = my_groups * S;
@@ -2425,10 +2429,10 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   // the fragment image, so DMA lane L loads x[row L/4][k0 + 4p + L%4]; 16-B form: lane (g, r16)
   // loads x[row r16][k0 + 4g .. +3], its own MFMA fragment
   auto a_row = [&](int64_t j, int i, int sub) __attribute__((always_inline)) -> const float* {
-    const int64_t m = min<int64_t>((grp0 + j * gstep) * 128 + wv * 32 + 16 * i + sub, M - 1);
+    const int64_t m = min<int64_t>((grp0 + j * gstep) * GR + wv * (16 * FR) + 16 * i + sub, M - 1);
     return x + (row_idx ? static_cast<int64_t>(row_idx[m]) : m) * ldx;
   };
-  const float* asrc[2];
+  const float* asrc[FR];
   int64_t asrc_j = -1;
   // the next stage to DMA as (group, stage in group, ring slot), advanced by one per call: no
   // 64-bit division per stage (its ~150 scalar instructions per stage were measurable)
@@ -2439,7 +2443,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     const int k = iss_s * KS;
     if (j != asrc_j) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) asrc[i] = a_row(j, i, A4 ? lane >> 2 : r16) + (A4 ? (lane & 3) : 4 * g);
+      for (int i = 0; i < FR; ++i) asrc[i] = a_row(j, i, A4 ? lane >> 2 : r16) + (A4 ? (lane & 3) : 4 * g);
       asrc_j = j;
     }
     char* base = lds + iss_slot * STAGE;
@@ -2451,8 +2455,8 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
 #pragma unroll
     for (int h = 0; h < KH; ++h) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        char* dst = base + ((wv * 2 + i) * KH + h) * 1024;
+      for (int i = 0; i < FR; ++i) {
+        char* dst = base + ((wv * FR + i) * KH + h) * 1024;
         if constexpr (A4) {
 #pragma unroll
           for (int p = 0; p < 4; ++p)
@@ -2468,27 +2472,27 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
                                          GTA_TO_LDS(base + A_BYTES + ((wv * (NT / 4) + q) * KH + h) * 1024), 16, 0, 0);
     }
   };
-  f32x4 acc[2][NT];
+  f32x4 acc[FR][NT];
   auto zero_acc = [&]() __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FR; ++i)
 #pragma unroll
       for (int c = 0; c < NT; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
-  auto mma = [&](const float (&av)[2][4], const float4& b4, int c) {
+  auto mma = [&](const float (&av)[FR][4], const float4& b4, int c) {
     const float bj[4] = {b4.x, b4.y, b4.z, b4.w};
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int i = 0; i < 2; ++i) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][j], bj[j], acc[i][c], 0, 0, 0);
+      for (int i = 0; i < FR; ++i) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][j], bj[j], acc[i][c], 0, 0, 0);
   };
   const bool vstore = vec_store && ldo % 4 == 0 && aligned(out, 16);
   auto epilogue = [&](int64_t j) __attribute__((always_inline)) {
-    const int64_t mw = (grp0 + j * gstep) * 128 + wv * 32;
+    const int64_t mw = (grp0 + j * gstep) * GR + wv * (16 * FR);
     if (vstore) {  // quad-transposed 16-B row stores (k_mm_rows' epilogue)
       const int p = r16 & 3, q = r16 >> 2;
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FR; ++i)
 #pragma unroll
         for (int c = 0; c < NT; ++c) {
           float v[4];
@@ -2520,7 +2524,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
         }
     } else {
 #pragma unroll
-      for (int i = 0; i < 2; ++i)
+      for (int i = 0; i < FR; ++i)
 #pragma unroll
         for (int c = 0; c < NT; ++c)
 #pragma unroll
@@ -2542,9 +2546,9 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
         if (k0 + 3 < K) v.w = p[3];
         return v;
       };
-      float av[2][4];
+      float av[FR][4];
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
+      for (int i = 0; i < FR; ++i) {
         const float4 a4 = ld4(a_row(j, i, r16) + k0);
         av[i][0] = a4.x; av[i][1] = a4.y; av[i][2] = a4.z; av[i][3] = a4.w;
       }
@@ -2576,20 +2580,22 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     // The asm wait names every loaded register, so no MFMA is scheduled above it.
     // all the stage's fragment reads issued at once; half h's MFMAs start when its reads are in
     // (LDS returns in order: lgkmcnt(reads of the later halves))
-    const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * 2) * KH * 1024) + static_cast<uint32_t>(lane) * 16u;
+    const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * KH * 1024) + static_cast<uint32_t>(lane) * 16u;
     const uint32_t sb = GTA_LDS_ADDR(lds + slot * STAGE + A_BYTES) + static_cast<uint32_t>(lane) * 16u;
-    f32x4 a4[KH][2], b4[KH][NT];
+    f32x4 a4[KH][FR], b4[KH][NT];
 #pragma unroll
     for (int h = 0; h < KH; ++h) {
-      ds_read16_idx(a4[h][0], sa, h);
-      ds_read16_idx(a4[h][1], sa, KH + h);
+#pragma unroll
+      for (int i = 0; i < FR; ++i) ds_read16_idx(a4[h][i], sa, i * KH + h);
 #pragma unroll
       for (int c = 0; c < NT; ++c) ds_read16_idx(b4[h][c], sb, c * KH + h);
     }
 #pragma unroll
     for (int h = 0; h < KH; ++h) {
-      if (h + 1 < KH) asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a4[h][0]), "+v"(a4[h][1]) : "n"(2 + NT) : "memory");
-      else asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a4[h][0]), "+v"(a4[h][1]) :: "memory");
+      if (h + 1 < KH) asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(FR + NT) : "memory");
+      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < FR; ++i) asm volatile("" : "+v"(a4[h][i]));
 #pragma unroll
       for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(b4[h][c]));
       // j outermost: the 2 x NT accumulators are each touched once per 2*NT MFMAs; per
@@ -2600,7 +2606,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
 #pragma unroll
         for (int c = 0; c < NT; ++c)
 #pragma unroll
-          for (int i = 0; i < 2; ++i)
+          for (int i = 0; i < FR; ++i)
             acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[h][i][j], b4[h][c][j], acc[i][c], 0, 0, 0);
       if (tuning_prio) __builtin_amdgcn_s_setprio(0);
     }
@@ -2731,6 +2737,11 @@ struct Tuning {
   int64_t mm_ring_blocks_per_cu = 0;  // k_mm_ring persistent grid: blocks per CU (0 = what LDS allows)
   int mm_ring_form = 0;      // k_mm_ring stages: 0 = 16 k x 3 stages, 1 = 32 k x 2, 2 = 32 k x 3, 3 = 16 k x 2
   int mm_ring_prio = 0;      // k_mm_ring: raise the wave priority around its MFMA block (+-3 %: noise, r02_mm_ab*)
+  int mm_ring_fr = 0;        // k_mm_ring A fragments per wave: 2 = 128-row groups, 1 = 64-row groups (form 0),
+                             // 0 = auto: 64-row groups for K <= 256 when 128-row groups load the CUs unevenly,
+                             // or below 512 128-row groups (K = 128 / 256 at 232,965 rows: 77 -> 87 / 90 -> 96
+                             // TF/s; 16,384 rows 40 -> 69; K = 602 and 2.45 M-row K = 100 stay on 128-row
+                             // groups: 95 against 93, 69 against 64; profiles/r02_mm_ring_probe_fr.json)
   int mm_ring_a16u = 1;      // k_mm_ring: 16-B A DMA pieces also when x rows are only 4-B aligned (K = 602)
   int mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
   int mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
@@ -2812,6 +2823,7 @@ const Knob* find_knob(const char* key) {
       {"mm_ring_form", &Tuning::mm_ring_form, nullptr},
       {"mm_ring_prio", &Tuning::mm_ring_prio, nullptr},
       {"mm_ring_a16u", &Tuning::mm_ring_a16u, nullptr},
+      {"mm_ring_fr", &Tuning::mm_ring_fr, nullptr},
       {"mm_blocks_per_cu", nullptr, &Tuning::mm_blocks_per_cu},
       {"apply_edge_form", &Tuning::apply_edge_form, nullptr},
       {"esm_lane", &Tuning::esm_lane, nullptr},
@@ -3661,20 +3673,30 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
     // than others: at M = 232,965 95 CUs ran 9 groups while 161 ran 6, 84 TF/s against 98 with
     // 2 blocks per CU, profiles/r02_mm_ring_probe.json.)
     const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
-    const int64_t lds_blocks = tuning().mm_ring_form == 1 ? 2 : tuning().mm_ring_form == 2 ? 1 : tuning().mm_ring_form == 3 ? 4 : 3;  // LDS per CU
+    const int form = tuning().mm_ring_form;  // 0: 16-k stages x 3; 1: 32-k stages x 2; 2: 32-k stages x 3
+    // fr1: 64-row groups (one A fragment per wave, 36 KiB of LDS: 4 blocks per CU), form 0 only
+    const int frk = tuning().mm_ring_fr;
+    // auto: 64-row groups when 128-row groups leave CUs unevenly loaded (groups / 256 well short
+    // of a whole number) on a short K, where per-group start-up and epilogue weigh most, or when
+    // there are too few 128-row groups for 2 blocks per CU
+    const double per_cu2 = static_cast<double>(groups) / 256.0;
+    const bool uneven = per_cu2 / std::ceil(per_cu2) < 0.95;
+    const bool fr1 = form == 0 && (frk == 1 || (frk == 0 && ((K <= 256 && uneven) || groups < 512)));
+    const int64_t n_grp = fr1 ? (M + 63) / 64 : groups;
+    const int64_t lds_blocks = fr1 ? 4 : form == 1 ? 2 : form == 2 ? 1 : form == 3 ? 4 : 3;  // LDS per CU
     const int64_t per_cu = tuning().mm_ring_blocks_per_cu > 0 ? tuning().mm_ring_blocks_per_cu : lds_blocks;
     const int64_t slots = std::max<int64_t>(1, 256 * per_cu / ncb);
-    const dim3 gr(static_cast<unsigned>(std::min(groups, slots) * ncb));
+    const dim3 gr(static_cast<unsigned>(std::min(n_grp, slots) * ncb));
     const bool a16 = (aligned(x, 16) && ldx % 4 == 0) || tuning().mm_ring_a16u;  // 16-B A pieces
-    const int form = tuning().mm_ring_form;  // 0: 16-k stages x 3; 1: 32-k stages x 2; 2: 32-k stages x 3
-#define GTA_RING(NT_, A4_, KH_, D_)                                                                              \
-  k_mm_ring<NT_, A4_, KH_, D_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const float*>(x), ldx, row_idx, M, \
+#define GTA_RING(NT_, A4_, KH_, D_, FR_)                                                                         \
+  k_mm_ring<NT_, A4_, KH_, D_, FR_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const float*>(x), ldx, row_idx, M, \
                                                                    static_cast<int>(K), static_cast<const float*>(wt), \
                                                                    ldwt, static_cast<int>(N), sf, out, ldo,          \
                                                                    tuning().mm_vstore, tuning().mm_ring_prio)
 #define GTA_RING_F(NT_, A4_) \
-  if (form == 1) GTA_RING(NT_, A4_, 2, 2); else if (form == 2) GTA_RING(NT_, A4_, 2, 3); \
-  else if (form == 3) GTA_RING(NT_, A4_, 1, 2); else GTA_RING(NT_, A4_, 1, 3)
+  if (fr1) GTA_RING(NT_, A4_, 1, 3, 1); else if (form == 1) GTA_RING(NT_, A4_, 2, 2, 2); \
+  else if (form == 2) GTA_RING(NT_, A4_, 2, 3, 2); else if (form == 3) GTA_RING(NT_, A4_, 1, 2, 2); \
+  else GTA_RING(NT_, A4_, 1, 3, 2)
     if (nt == 8) { if (a16) { GTA_RING_F(8, false); } else { GTA_RING_F(8, true); } }
     else { if (a16) { GTA_RING_F(4, false); } else { GTA_RING_F(4, true); } }
 #undef GTA_RING_F

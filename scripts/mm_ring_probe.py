@@ -12,9 +12,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops  # noqa: E402
 
-CASES = [(232965, 602, 128), (232965, 592, 128), (232965, 608, 128), (65536, 602, 128), (16384, 602, 128),
-         (232965, 128, 128), (232965, 256, 128)]
-FORMS = {"ring": {"mm_blaslt": 0}, "ring_bpc2": {"mm_blaslt": 0, "mm_ring_blocks_per_cu": 2},
+CASES = [(232965, 602, 128), (232965, 602, 256), (89250, 500, 128), (65536, 602, 128), (16384, 602, 128),
+         (232965, 128, 128), (232965, 256, 128), (2449029, 100, 128), (2449029, 128, 128), (899756, 500, 128)]
+FORMS = {"ring": {"mm_blaslt": 0}, "ring_fr2": {"mm_blaslt": 0, "mm_ring_fr": 2},
+         "ring_fr1": {"mm_blaslt": 0, "mm_ring_fr": 1},
+         "ring_bpc2": {"mm_blaslt": 0, "mm_ring_blocks_per_cu": 2},
          "ring_bpc1": {"mm_blaslt": 0, "mm_ring_blocks_per_cu": 1}, "blaslt_top1": {"mm_blaslt": 1, "mm_blaslt_max_m": 1 << 62}}
 
 
@@ -32,6 +34,7 @@ def main():
                 ops.set_debug("mm_blaslt", 1)
                 ops.set_debug("mm_blaslt_max_m", 65535)
                 ops.set_debug("mm_ring_blocks_per_cu", 0)
+                ops.set_debug("mm_ring_fr", 0)
                 for k, v in knobs.items():
                     ops.set_debug(k, v)
                 ops.update_mm(x, w)
@@ -49,6 +52,7 @@ def main():
     ops.set_debug("mm_blaslt", 1)
     ops.set_debug("mm_blaslt_max_m", 65535)
     ops.set_debug("mm_ring_blocks_per_cu", 0)
+    ops.set_debug("mm_ring_fr", 0)
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "mm_ring_probe.json"), "w") as f:
         json.dump(out, f, indent=1)

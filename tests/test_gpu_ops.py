@@ -814,15 +814,19 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
         ops.MM_ROWS_MIN_M = 0
         ops.set_debug("mm_blaslt", 0)
         # k_mm_rows, then the ring's four stage forms, then the 4-B A-DMA path
-        for ring, form, a16u in ((0, 0, 1), (1, 0, 1), (1, 1, 1), (1, 2, 1), (1, 3, 1), (1, 0, 0)):
+        # then 64-row groups (one A fragment per wave), with 16-B and 4-B A pieces
+        for ring, form, a16u, fr in ((0, 0, 1, 2), (1, 0, 1, 2), (1, 1, 1, 2), (1, 2, 1, 2), (1, 3, 1, 2),
+                                     (1, 0, 0, 2), (1, 0, 1, 1), (1, 0, 0, 1), (1, 0, 1, 0)):
             ops.set_debug("mm_ring", ring)
             ops.set_debug("mm_ring_form", form)
             ops.set_debug("mm_ring_a16u", a16u)
+            ops.set_debug("mm_ring_fr", fr)
             outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
     finally:
         ops.set_debug("mm_ring", 1)
         ops.set_debug("mm_ring_form", 0)
         ops.set_debug("mm_ring_a16u", 1)
+        ops.set_debug("mm_ring_fr", 0)
         ops.set_debug("mm_blaslt", 1)
         ops.MM_ROWS_MIN_M = old_min
     torch.cuda.synchronize()
