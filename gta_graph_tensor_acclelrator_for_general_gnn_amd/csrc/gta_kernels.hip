@@ -2742,6 +2742,8 @@ struct Tuning {
                              // or below 512 128-row groups (K = 128 / 256 at 232,965 rows: 77 -> 87 / 90 -> 96
                              // TF/s; 16,384 rows 40 -> 69; K = 602 and 2.45 M-row K = 100 stay on 128-row
                              // groups: 95 against 93, 69 against 64; profiles/r02_mm_ring_probe_fr.json)
+  int mm_ring_tail = 0;      // k_mm_ring: uneven 128-row groups on a long K: whole rounds, then the rest as 64-row groups
+                             // in a second launch (bitwise equal; measured 94.7 vs 96.8 TF/s at K = 602: off)
   int mm_ring_a16u = 1;      // k_mm_ring: 16-B A DMA pieces also when x rows are only 4-B aligned (K = 602)
   int mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
   int mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
@@ -2824,6 +2826,7 @@ const Knob* find_knob(const char* key) {
       {"mm_ring_prio", &Tuning::mm_ring_prio, nullptr},
       {"mm_ring_a16u", &Tuning::mm_ring_a16u, nullptr},
       {"mm_ring_fr", &Tuning::mm_ring_fr, nullptr},
+      {"mm_ring_tail", &Tuning::mm_ring_tail, nullptr},
       {"mm_blocks_per_cu", nullptr, &Tuning::mm_blocks_per_cu},
       {"apply_edge_form", &Tuning::apply_edge_form, nullptr},
       {"esm_lane", &Tuning::esm_lane, nullptr},
@@ -3679,28 +3682,44 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
     // auto: 64-row groups when 128-row groups leave CUs unevenly loaded (groups / 256 well short
     // of a whole number) on a short K, where per-group start-up and epilogue weigh most, or when
     // there are too few 128-row groups for 2 blocks per CU
-    const double per_cu2 = static_cast<double>(groups) / 256.0;
+    const double per_cu2 = static_cast<double>(groups * ncb) / 256.0;
     const bool uneven = per_cu2 / std::ceil(per_cu2) < 0.95;
     const bool fr1 = form == 0 && (frk == 1 || (frk == 0 && ((K <= 256 && uneven) || groups < 512)));
     const int64_t n_grp = fr1 ? (M + 63) / 64 : groups;
     const int64_t lds_blocks = fr1 ? 4 : form == 1 ? 2 : form == 2 ? 1 : form == 3 ? 4 : 3;  // LDS per CU
     const int64_t per_cu = tuning().mm_ring_blocks_per_cu > 0 ? tuning().mm_ring_blocks_per_cu : lds_blocks;
     const int64_t slots = std::max<int64_t>(1, 256 * per_cu / ncb);
-    const dim3 gr(static_cast<unsigned>(std::min(n_grp, slots) * ncb));
     const bool a16 = (aligned(x, 16) && ldx % 4 == 0) || tuning().mm_ring_a16u;  // 16-B A pieces
-#define GTA_RING(NT_, A4_, KH_, D_, FR_)                                                                         \
-  k_mm_ring<NT_, A4_, KH_, D_, FR_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const float*>(x), ldx, row_idx, M, \
-                                                                   static_cast<int>(K), static_cast<const float*>(wt), \
-                                                                   ldwt, static_cast<int>(N), sf, out, ldo,          \
-                                                                   tuning().mm_vstore, tuning().mm_ring_prio)
+    const float* xf = static_cast<const float*>(x);
+    const float* wf = static_cast<const float*>(wt);
+    auto run = [&](const float* xp, const int32_t* rp, int64_t MM, float* op, bool f1, int64_t blocks) {
+      const dim3 gr(static_cast<unsigned>(blocks));
+#define GTA_RING(NT_, A4_, KH_, D_, FR_)                                                                          \
+  k_mm_ring<NT_, A4_, KH_, D_, FR_><<<gr, dim3(kBlock), 0, S(stream)>>>(xp, ldx, rp, MM, static_cast<int>(K), wf, ldwt, \
+                                                                        static_cast<int>(N), sf, op, ldo,            \
+                                                                        tuning().mm_vstore, tuning().mm_ring_prio)
 #define GTA_RING_F(NT_, A4_) \
-  if (fr1) GTA_RING(NT_, A4_, 1, 3, 1); else if (form == 1) GTA_RING(NT_, A4_, 2, 2, 2); \
+  if (f1) GTA_RING(NT_, A4_, 1, 3, 1); else if (form == 1) GTA_RING(NT_, A4_, 2, 2, 2); \
   else if (form == 2) GTA_RING(NT_, A4_, 2, 3, 2); else if (form == 3) GTA_RING(NT_, A4_, 1, 2, 2); \
   else GTA_RING(NT_, A4_, 1, 3, 2)
-    if (nt == 8) { if (a16) { GTA_RING_F(8, false); } else { GTA_RING_F(8, true); } }
-    else { if (a16) { GTA_RING_F(4, false); } else { GTA_RING_F(4, true); } }
+      if (nt == 8) { if (a16) { GTA_RING_F(8, false); } else { GTA_RING_F(8, true); } }
+      else { if (a16) { GTA_RING_F(4, false); } else { GTA_RING_F(4, true); } }
 #undef GTA_RING_F
 #undef GTA_RING
+    };
+    // uneven 128-row groups on a long K: whole rounds of 128-row groups (every block the same
+    // count), then the remainder rows as 64-row groups in a second launch at 4 blocks per CU, so no
+    // CU runs a whole extra 128-row group (same k order: bitwise equal to one launch)
+    const int64_t M1 = (groups / slots) * slots * 128;
+    if (!fr1 && form == 0 && frk == 0 && tuning().mm_ring_tail && uneven && tuning().mm_ring_blocks_per_cu == 0 &&
+        M1 > 0 && M1 < M) {
+      run(xf, row_idx, M1, out, false, slots * ncb);
+      const int64_t M2 = M - M1, slots1 = std::max<int64_t>(1, 256 * 4 / ncb);
+      run(row_idx ? xf : xf + M1 * ldx, row_idx ? row_idx + M1 : nullptr, M2, out + M1 * ldo, true,
+          std::min((M2 + 63) / 64, slots1) * ncb);
+    } else {
+      run(xf, row_idx, M, out, fr1, std::min(n_grp, slots) * ncb);
+    }
     GTA_LAUNCHED("k_mm_ring");
     return GTA_OK;
   }

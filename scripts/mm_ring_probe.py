@@ -14,7 +14,8 @@ from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops  # noqa: E402
 
 CASES = [(232965, 602, 128), (232965, 602, 256), (89250, 500, 128), (65536, 602, 128), (16384, 602, 128),
          (232965, 128, 128), (232965, 256, 128), (2449029, 100, 128), (2449029, 128, 128), (899756, 500, 128)]
-FORMS = {"ring": {"mm_blaslt": 0}, "ring_fr2": {"mm_blaslt": 0, "mm_ring_fr": 2},
+FORMS = {"ring": {"mm_blaslt": 0}, "ring_tail": {"mm_blaslt": 0, "mm_ring_tail": 1},
+         "ring_fr2": {"mm_blaslt": 0, "mm_ring_fr": 2},
          "ring_fr1": {"mm_blaslt": 0, "mm_ring_fr": 1},
          "ring_bpc2": {"mm_blaslt": 0, "mm_ring_blocks_per_cu": 2},
          "ring_bpc1": {"mm_blaslt": 0, "mm_ring_blocks_per_cu": 1}, "blaslt_top1": {"mm_blaslt": 1, "mm_blaslt_max_m": 1 << 62}}
@@ -35,6 +36,7 @@ def main():
                 ops.set_debug("mm_blaslt_max_m", 65535)
                 ops.set_debug("mm_ring_blocks_per_cu", 0)
                 ops.set_debug("mm_ring_fr", 0)
+                ops.set_debug("mm_ring_tail", 0)
                 for k, v in knobs.items():
                     ops.set_debug(k, v)
                 ops.update_mm(x, w)

@@ -837,25 +837,31 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     _check(outs[1], ref, np.abs(xs).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "k_mm_ring")
 
 
-@pytest.mark.parametrize("M,K", [(70000, 602), (65536, 100)])
+@pytest.mark.parametrize("M,K", [(70000, 602), (65536, 100), (120000, 602), (120000, 128)])
 def test_update_mm_default_is_the_ring(dev, M, K):
     """From 65,536 rows the DEFAULT plain fp32 UPDATE (no knobs touched) is the hand-written
     k_mm_ring, not the library: bitwise equal to k_mm_rows (the library's contraction order
-    differs), and within the fp64 bound."""
+    differs), and within the fp64 bound.  120,000 rows: 938 128-row groups over 768 block slots,
+    so K = 128 runs 64-row groups throughout; with knob mm_ring_tail K = 602 runs whole rounds + the
+    remainder as 64-row groups (two launches), bitwise the same."""
     rng = np.random.default_rng(M + K)
     x = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32))
     w = torch.from_numpy((rng.standard_normal((K, 128)) / np.sqrt(K)).astype(np.float32))
     xd, wd = x.to(dev), w.to(dev)
     y = ops.update_mm(xd, wd)
     try:
+        ops.set_debug("mm_ring_tail", 1)
+        y_tail = ops.update_mm(xd, wd)
+        ops.set_debug("mm_ring_tail", 0)
         ops.set_debug("mm_blaslt", 0)
         ops.set_debug("mm_ring", 0)
         y_rows = ops.update_mm(xd, wd)
     finally:
+        ops.set_debug("mm_ring_tail", 0)
         ops.set_debug("mm_ring", 1)
         ops.set_debug("mm_blaslt", 1)
     torch.cuda.synchronize()
-    assert torch.equal(y, y_rows)
+    assert torch.equal(y, y_rows) and torch.equal(y_tail, y_rows)
     rows = np.arange(0, M, 97)
     ref = isa_ref.mm(x.numpy()[rows], w.numpy())
     _check(y[rows], ref, np.abs(x.numpy()[rows]).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "default UPDATE")
