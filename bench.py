@@ -26,9 +26,13 @@ Printed JSON (rank 0):
                 by the oracle (oracle/isa_ref.aggregate), |err| <= 1e-5 * sum|terms| + 1e-6 each
   roofline      the aggregate launch pair (k_agg_h32 + k_seg_reduce) at N = 1: traffic = HBM-side bytes
                 per launch from two rocprofv3 --pmc passes run by this bench on its own kernels
-                (FETCH_SIZE, WRITE_SIZE; the read side scaled by a factor calibrated in the same pass
-                on a known-byte gather, MI355X_MICROARCH.md §HBM); achieved = traffic / HIP-event
-                kernel time, frac = achieved / 8 TB/s.  alg_* = the SURVEY §8d byte model (548 B/edge:
+                (FETCH_SIZE, WRITE_SIZE).  Two read factors, each calibrated in the same pass on known
+                bytes (MI355X_MICROARCH.md §HBM): streaming reads on a float4 copy (k_apply_node4),
+                gathered 512-B rows on a permutation gather with 16-B lanes; k_agg_h32's FETCH is split
+                into its known streams (indices, alpha, item records: streaming factor) and the rest
+                (its X gathers: gather factor); k_seg_reduce's partial-row reads take the streaming
+                factor; writes take the copy's write factor.  achieved = traffic / HIP-event kernel
+                time, frac = achieved / 8 TB/s.  alg_* = the SURVEY §8d byte model (548 B/edge:
                 every gathered X row), frac_l2 = its rate against the L2-served gather ceiling.
   cpu_baseline  oracle/spmm_ref.c (fp32, OpenMP, every core of sched_getaffinity) on a bounded row
                 sample of the same workload, rank 0 at N = 1.
@@ -182,24 +186,39 @@ def build(args, world, rank, dev, backend, note):
 # PMC traffic (rocprofv3 --pmc on this very bench, child processes started before the GPU is used)
 # ----------------------------------------------------------------------------------------------
 def pmc_child(args):
-    """Runs under rocprofv3 --pmc: a known-byte calibration gather, then the metric launches."""
+    """Runs under rocprofv3 --pmc: the known-byte calibration launches, then the metric launches.
+    Writes the metric plan's item count (its known stream bytes) to <pmc dir>/meta.json."""
     dev = torch.device("cuda", 0)
     torch.cuda.set_device(dev)
-    # calibration: a permutation gather (1 edge per row, every X row read once, 1 GiB table > Infinity Cache)
     n = CALIB_ROWS
-    ip = torch.arange(n + 1, device=dev, dtype=torch.int64)
-    perm = torch.argsort(G.hash32(torch.arange(n, device=dev, dtype=torch.int64), 7, 9)).to(torch.int32)
-    gc = G.Graph(ip, perm)
+    # streaming calibration: a float4 copy of a 1 GiB table (k_apply_node4, 16-B lanes, read once, written once)
     xc = torch.ones(n, F, device=dev)
     yc = torch.empty(n, F, device=dev)
     for _ in range(2):
-        ops.aggregate(gc, xc, "src", None, out=yc)
+        ops.apply_node(None, None, xc, out=yc)
+    # gather calibration: a permutation gather (1 edge per row, every X row read once, 1 GiB table >
+    # Infinity Cache), 32 lanes x float4 per 512-B row as k_agg_h32 reads them
+    ip = torch.arange(n + 1, device=dev, dtype=torch.int64)
+    perm = torch.argsort(G.hash32(torch.arange(n, device=dev, dtype=torch.int64), 7, 9)).to(torch.int32)
+    gc = G.Graph(ip, perm)
+    ops.set_debug("agg_lpe", 32)
+    try:
+        for _ in range(2):
+            ops.aggregate(gc, xc, "src", None, out=yc)
+    finally:
+        ops.set_debug("agg_lpe", 0)
     torch.cuda.synchronize()
     del xc, yc, gc
     shard, agg, *_ = build(args, 1, 0, dev, "none", lambda m: None)
     for _ in range(args.steps):
         agg.step()
     torch.cuda.synchronize()
+    if args.pmc_meta:
+        gg = agg.parts[0][2]
+        plan = gg.blocked_plan(agg.blocks) if agg.impl == "blocked" else None
+        with open(args.pmc_meta, "w") as fh:
+            json.dump({"nnz": int(gg.nnz), "n_rows": int(gg.n_rows), "heads": HEADS,
+                       "n_items": int(plan.n_items) if plan is not None else 0}, fh)
     return 0
 
 
@@ -215,8 +234,9 @@ def _counter_rows(d, counter):
 
 
 def _split(rows):
-    """-> (calibration dispatches, [(agg, reduce)] metric launch pairs) from ordered counter rows."""
-    calib, pairs, cur = [], [], None
+    """-> (stream calibration dispatches, gather calibration dispatches, [(agg, reduce)] metric
+    launch pairs) from ordered counter rows."""
+    copy, gather, pairs, cur = [], [], [], None
     for _, name, v in rows:
         if "k_agg_h32" in name or "k_agg_seg" in name:
             cur = [v, 0.0]
@@ -224,9 +244,11 @@ def _split(rows):
             cur[1] = v
             pairs.append(tuple(cur))
             cur = None
-        elif ("k_aggregate" in name or "k_agg_lean" in name) and not pairs and cur is None:
-            calib.append(v)
-    return calib, pairs
+        elif "k_apply_node4" in name and not pairs and cur is None:
+            copy.append(v)
+        elif "k_aggregate" in name and not pairs and cur is None:
+            gather.append(v)
+    return copy, gather, pairs
 
 
 def collect_pmc(args, out_dir):
@@ -237,12 +259,13 @@ def collect_pmc(args, out_dir):
         return {"error": "rocprofv3 not found"}
     os.makedirs(out_dir, exist_ok=True)
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    meta_path = os.path.join(out_dir, "meta.json")
     res = {}
     for counter in ("FETCH_SIZE", "WRITE_SIZE"):
         d = os.path.join(out_dir, counter.lower())
         shutil.rmtree(d, ignore_errors=True)
         cmd = [exe, "--kernel-trace", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
-               sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3",
+               sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--pmc-meta", meta_path,
                "--n", str(args.n), "--e", str(args.e), "--blocks", str(args.blocks), "--impl", args.impl]
         t0 = time.time()
         try:
@@ -252,26 +275,50 @@ def collect_pmc(args, out_dir):
             return {"error": f"rocprofv3 --pmc {counter} timed out"}
         if p.returncode != 0:
             return {"error": f"rocprofv3 --pmc {counter} rc={p.returncode}: {p.stderr[-400:]}"}
-        calib, pairs = _split(_counter_rows(d, counter))
-        if not calib or not pairs:
+        copy, gather, pairs = _split(_counter_rows(d, counter))
+        if not copy or not gather or not pairs:
             return {"error": f"{counter}: no calibration/metric dispatches in {d}"}
         pairs = pairs[1:] if len(pairs) > 1 else pairs   # the first launch runs on cold caches
-        res[counter] = {"calib_kb": calib[-1], "agg_kb": float(np.mean([a for a, _ in pairs])),
+        res[counter] = {"copy_kb": copy[-1], "gather_kb": gather[-1],
+                        "agg_kb": float(np.mean([a for a, _ in pairs])),
                         "reduce_kb": float(np.mean([b for _, b in pairs])), "launches": len(pairs),
                         "pass_s": round(time.time() - t0, 1)}
-    n = CALIB_ROWS
-    calib_read = n * (4 * F + 4) + (n + 1) * 8     # X rows once + col idx + indptr
-    calib_write = n * 4 * F                          # Y
-    kr = calib_read / (res["FETCH_SIZE"]["calib_kb"] * 1024.0)
-    kw = calib_write / (res["WRITE_SIZE"]["calib_kb"] * 1024.0)
+    try:
+        meta = json.load(open(meta_path))
+    except (OSError, ValueError):
+        return {"error": "pmc child wrote no plan metadata"}
+    return pmc_traffic(res, meta)
+
+
+def pmc_traffic(res, meta, n=CALIB_ROWS):
+    """Per-launch bytes from the counter means (res[counter][...] in KB) and the plan metadata:
+      read factors   kr_s = copy bytes read / copy FETCH; kr_g = permutation-gather X bytes / (gather
+                     FETCH - its index + indptr streams / kr_s); write factor kw = copy bytes / copy WRITE
+      k_agg_h32      streams S = 4 E (indices) + 4 H E (alpha) + 16 items (item records), read once;
+                     gathers = (FETCH - S / kr_s) * kr_g; + WRITE * kw (partial rows)
+      k_seg_reduce   FETCH * kr_s (partial rows, item lists) + WRITE * kw (y)
+    Recomputable from the committed CSVs (profiles/r03_pmc_*)."""
     fe, wr = res["FETCH_SIZE"], res["WRITE_SIZE"]
-    agg = (fe["agg_kb"] * kr + wr["agg_kb"] * kw) * 1024.0
-    red = (fe["reduce_kb"] * kr + wr["reduce_kb"] * kw) * 1024.0
+    kb = 1024.0
+    copy_bytes = n * 4 * F
+    kr_s = copy_bytes / (fe["copy_kb"] * kb)
+    kw = copy_bytes / (wr["copy_kb"] * kb)
+    g_stream = n * 4 + (n + 1) * 8                   # permutation gather: col idx + indptr
+    kr_g = copy_bytes / (fe["gather_kb"] * kb - g_stream / kr_s)
+    E, H, items = meta["nnz"], meta["heads"], meta["n_items"]
+    streams = 4.0 * E + 4.0 * H * E + 16.0 * items
+    gathers = (fe["agg_kb"] * kb - streams / kr_s) * kr_g
+    agg = streams + gathers + wr["agg_kb"] * kb * kw
+    red = fe["reduce_kb"] * kb * kr_s + wr["reduce_kb"] * kb * kw
     return {"bytes_per_launch": agg + red, "agg_bytes": agg, "reduce_bytes": red,
-            "read_factor": kr, "write_factor": kw, "passes": res,
+            "agg_split": {"streams": streams, "gathers": gathers, "writes": wr["agg_kb"] * kb * kw},
+            "read_factor_stream": kr_s, "read_factor_gather": kr_g, "write_factor": kw, "meta": meta,
+            "passes": res,
             "method": "rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes) on this bench's own launches; "
-                      "bytes = FETCH_SIZE*1024*read_factor + WRITE_SIZE*1024*write_factor, factors calibrated "
-                      "on a permutation gather of known bytes (1 GiB table, 512-B rows) in the same pass; "
+                      "read factors calibrated in the same pass: streaming (kr_s, float4 copy of a 1 GiB table) "
+                      "and gathered 512-B rows (kr_g, permutation gather with 16-B lanes, its index streams "
+                      "taken out at kr_s); k_agg_h32 = known streams (indices, alpha, item records) + "
+                      "(FETCH - streams/kr_s)*kr_g + WRITE*kw; k_seg_reduce = FETCH*kr_s + WRITE*kw; "
                       "counts L2<->fabric bytes (Infinity-Cache hits included); first launch skipped"}
 
 
@@ -367,6 +414,7 @@ def main():
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
     ap.add_argument("--pmc-dir", default="", help="keep the --pmc CSVs here (default: a temp dir)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-meta", default="", help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
         return pmc_child(args)
@@ -501,7 +549,12 @@ def main():
             roof["achieved"] = pmc["bytes_per_launch"] / (kern_ms / 1e3) / 1e9
             roof["frac"] = roof["achieved"] / PEAK_HBM_GBS
             roof["traffic_split"] = {"agg": pmc["agg_bytes"], "reduce": pmc["reduce_bytes"],
-                                     "read_factor": pmc["read_factor"], "write_factor": pmc["write_factor"]}
+                                     "agg_split": pmc["agg_split"],
+                                     "read_factor_stream": pmc["read_factor_stream"],
+                                     "read_factor_gather": pmc["read_factor_gather"],
+                                     "write_factor": pmc["write_factor"]}
+            roof["pmc_counters_kb"] = pmc["passes"]
+            roof["pmc_meta"] = pmc["meta"]
             roof["traffic_method"] = pmc["method"]
             if phase_ms is not None:  # each kernel alone: its PMC bytes over its own HIP-event time
                 roof["per_kernel"] = {

@@ -31,8 +31,7 @@ def needs_build(out=OUT):
 def build(force=False, verbose=True):
     if not force and not needs_build():
         return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", OUT + ".tmp", SRC,
-           "-L/opt/rocm/lib", "-lhipblaslt", "-Wl,-rpath,/opt/rocm/lib"]
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared", "-o", OUT + ".tmp", SRC]
     if verbose:
         print(" ".join(cmd), flush=True)
     subprocess.run(cmd, check=True)

@@ -7,8 +7,6 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 
-#include <hipblaslt/hipblaslt.h>
-
 #include <algorithm>
 #include <atomic>
 #include <cmath>
@@ -16,7 +14,6 @@
 #include <map>
 #include <mutex>
 #include <string>
-#include <tuple>
 
 #include "../../include/gta.h"
 
@@ -396,49 +393,27 @@ __device__ __forceinline__ void bcast_all(const float* wa, float* out) {
   }
 }
 
-// Column-blocked form (SEG = true): launch b of B handles, for every row (heaviest
-// first, `perm`), only its edges whose source lies in column block b --
-// seg[r][b] .. seg[r][b+1] within the row's sorted column list -- and adds the
-// partial into y[r] (the first launch writes).  All waves of a launch gather
-// from one n_cols/B slice of X, which stays resident in each XCD's 4 MB L2.
-struct SegItem {  // one (column block, row) work item: 16 B, loaded with one dwordx4
+struct SegItem {  // one (column block, row) work item of the blocked plan: 16 B, loaded with one dwordx4
   int64_t beg;
   int32_t row;
   int32_t len;
 };
 
-struct SegView {
-  const int32_t* perm;  // rows, heaviest first
-  const int32_t* seg;   // [n_rows][B+1] offsets within each row
-  int B;
-  int b;
-};
-
-template <int VW, int GL, bool SEG>
+template <int VW, int GL>
 __global__ void __launch_bounds__(kBlock)
 k_agg_lean(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows, PlanView plan,
            int use_plan, int64_t chunk, const float* __restrict__ x, int64_t ldx, int F,
            const float* __restrict__ w, int64_t ldw, const float* __restrict__ row_scale,
-           float* __restrict__ y, int64_t ldy, int accumulate, float* __restrict__ partial, SegView sv) {
+           float* __restrict__ y, int64_t ldy, int accumulate, float* __restrict__ partial) {
   constexpr int U = (GL > 8) ? GL : 8;               // edges per unrolled step
   constexpr int NWL = (GL > 0) ? U / GL : 0;         // weight loads per step
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t item = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
-  const int64_t n_items = (use_plan && !SEG) ? plan.hdr[0] : n_rows;
+  const int64_t n_items = use_plan ? plan.hdr[0] : n_rows;
   if (item >= n_items) return;
   int64_t row, eb, ee;
   bool split = false;
-  if (SEG) {
-    row = sv.perm[item];
-    const int32_t* sg = sv.seg + row * (sv.B + 1);
-    const int64_t base = indptr[row];
-    eb = base + sg[sv.b];
-    ee = base + sg[sv.b + 1];
-    if (sv.b > 0) {
-      if (eb == ee) return;  // nothing of this row in this column block
-      accumulate = 1;
-    }
-  } else if (use_plan) {
+  if (use_plan) {
     row = plan.item_row[item];
     eb = plan.item_beg[item];
     const int64_t rb = indptr[row], re = indptr[row + 1];
@@ -513,104 +488,6 @@ k_agg_lean(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indic
       for (int k = 0; k < VW; ++k) o.v[k] = scale * acc[k];
     }
     o.store(yp);
-  }
-}
-
-// Persistent column-blocked launch b: each wave walks rows it, it+W, it+2W, ...
-// (heaviest first), prefetching the next row's metadata (perm -> indptr, segment
-// bounds) one and two rows ahead so the dependent-load chain overlaps the current
-// row's gathers; y[row] old value is loaded at row start and added at the end.
-template <int VW, int GL>
-__global__ void __launch_bounds__(kBlock)
-k_agg_seg(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
-          const float* __restrict__ x, int64_t ldx, const float* __restrict__ w, int64_t ldw,
-          const float* __restrict__ row_scale, float* __restrict__ y, int64_t ldy, int accumulate, SegView sv) {
-  constexpr int U = (GL > 8) ? GL : 8;
-  constexpr int NWL = (GL > 0) ? U / GL : 0;
-  const int lane = threadIdx.x & (kWave - 1);
-  const int64_t W = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
-  const int64_t first = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
-  const int col = lane * VW;
-  const int head = (GL > 0) ? lane / GL : 0;
-  const int gsub = (GL > 0) ? lane % GL : 0;
-  const int S1 = sv.B + 1;
-  const bool acc_in = accumulate || sv.b > 0;
-  // pipeline: r1 = row of item it (meta loaded), r2 = row of item it+W (perm loaded)
-  int64_t it = first;
-  if (it >= n_rows) return;
-  int r1 = sv.perm[it];
-  int64_t b1 = indptr[r1];
-  int s1a = sv.seg[static_cast<int64_t>(r1) * S1 + sv.b], s1b = sv.seg[static_cast<int64_t>(r1) * S1 + sv.b + 1];
-  int r2 = (it + W < n_rows) ? sv.perm[it + W] : 0;
-  for (; it < n_rows; it += W) {
-    const int row = r1;
-    const int64_t eb = b1 + s1a, ee = b1 + s1b;
-    // prefetch: metadata of item it+W (row r2), perm of item it+2W
-    int64_t nb1 = 0;
-    int ns1a = 0, ns1b = 0, nr2 = 0;
-    if (it + W < n_rows) {
-      nb1 = indptr[r2];
-      ns1a = sv.seg[static_cast<int64_t>(r2) * S1 + sv.b];
-      ns1b = sv.seg[static_cast<int64_t>(r2) * S1 + sv.b + 1];
-      if (it + 2 * W < n_rows) nr2 = sv.perm[it + 2 * W];
-    }
-    if (eb < ee || !acc_in) {
-      float* yp = y + static_cast<int64_t>(row) * ldy + col;
-      Vec<VW> old;
-      if (acc_in) old.load(yp);
-      float acc[VW];
-#pragma unroll
-      for (int k = 0; k < VW; ++k) acc[k] = 0.f;
-      int idxv = (eb < ee) ? indices[min(eb + lane, ee - 1)] : 0;
-      for (int64_t e0 = eb; e0 < ee; e0 += kWave) {
-        const int n = static_cast<int>(min<int64_t>(kWave, ee - e0));
-        const int idxn = indices[min(e0 + kWave + lane, ee - 1)];
-        const float* wblk = (GL > 0) ? w + e0 * ldw : nullptr;
-        int s = 0;
-        for (; s + U <= n; s += U) {
-          Vec<VW> xv[U];
-#pragma unroll
-          for (int u = 0; u < U; ++u) {
-            const int64_t xr = __builtin_amdgcn_readlane(idxv, s + u);
-            xv[u].load(x + xr * ldx + col);
-          }
-          if (GL > 0) {
-            float wa[NWL > 0 ? NWL : 1], wu[U];
-#pragma unroll
-            for (int q = 0; q < NWL; ++q) wa[q] = wblk[static_cast<int64_t>(s + q * GL + gsub) * ldw + head];
-            bcast_all<(GL > 0 ? GL : 1), U>(wa, wu);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-              for (int k = 0; k < VW; ++k) acc[k] = fmaf(wu[u], xv[u].v[k], acc[k]);
-          } else {
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-              for (int k = 0; k < VW; ++k) acc[k] += xv[u].v[k];
-          }
-        }
-        for (; s < n; ++s) {
-          const int64_t xr = __builtin_amdgcn_readlane(idxv, s);
-          Vec<VW> xv;
-          xv.load(x + xr * ldx + col);
-          const float wv = (GL > 0) ? wblk[static_cast<int64_t>(s) * ldw + head] : 1.f;
-#pragma unroll
-          for (int k = 0; k < VW; ++k) acc[k] = (GL > 0) ? fmaf(wv, xv.v[k], acc[k]) : acc[k] + xv.v[k];
-        }
-        idxv = idxn;
-      }
-      const float scale = row_scale ? row_scale[row] : 1.f;
-      Vec<VW> o;
-#pragma unroll
-      for (int k = 0; k < VW; ++k) o.v[k] = (acc_in ? old.v[k] : 0.f) + scale * acc[k];
-      o.store(yp);
-    }
-    r1 = r2;
-    b1 = nb1;
-    s1a = ns1a;
-    s1b = ns1b;
-    r2 = nr2;
   }
 }
 
@@ -833,63 +710,14 @@ __device__ __forceinline__ float quad_bcast(float v) {  // lane (l & ~3) | SEL o
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), SEL * 0x55, 0xF, 0xF, false));
 }
 
-// In-launch ordered reduce (FUSE): instead of a k_seg_reduce pass, the LAST item of a row to
-// finish sums the row's partials in its fixed (block, part) order and writes y.  Hand-off
-// (cdna_hip_programming.md §5 split-K recipe, sc1 form; MI355X_MICROARCH.md § visibility): every
-// item stores its 512-B partial write-through (buffer store, sc1), the storing wave drains
-// (s_waitcnt vmcnt(0)), then one lane per half-wave adds 1 to the row's agent-scope counter;
-// the half-wave whose add returns (items - 1) is the last arriver and reads the row's partials
-// with sc1 loads (L1 bypassed; no other workgroup reads a slab line before its row's counter is
-// complete, and the launch boundary invalidates the L2s, so no XCD holds a stale copy).  The
-// sum order is the row's item list whatever the arrival order: bitwise equal to k_seg_reduce.
-// A row's only item (low-degree rows) writes y directly (0 + p, as the reduce would).
-// Counters are zeroed, and rows without items written, by k_fuse_prep ahead of every launch.
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-struct FuseArgs {
-  const int64_t* row_ptr;    // items of row r: row_items[row_ptr[r] .. row_ptr[r + 1])
-  const int32_t* row_items;  // (block, part) order
-  int32_t* cnt;              // arrival counter per row
-  const float* row_scale;
-  float* y;
-  int64_t ldy;
-  int accumulate;
-  uint32_t slab_bytes;       // slab range of the buffer descriptor (< 2^32)
-};
-
-__global__ void __launch_bounds__(kBlock)
-k_fuse_prep(int64_t n_rows, int F, FuseArgs fa) {
-  const int64_t r = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
-  if (r >= n_rows) return;
-  fa.cnt[r] = 0;
-  if (fa.row_ptr[r + 1] != fa.row_ptr[r]) return;
-  const float v = (fa.row_scale ? fa.row_scale[r] : 1.f) * 0.f;  // k_seg_reduce's scale * (empty sum)
-  float* yp = fa.y + r * fa.ldy;
-  for (int c = 0; c < F; ++c) yp[c] = fa.accumulate ? yp[c] + v : v;
-}
-
-// y row epilogue of the ordered reduce: y = scale * s, or y += scale * s (k_seg_reduce's form)
-__device__ __forceinline__ void fuse_store_row(const FuseArgs& fa, int64_t row, int col, const float (&s)[4]) {
-  const float scale = fa.row_scale ? fa.row_scale[row] : 1.f;
-  float4* yp = reinterpret_cast<float4*>(fa.y + row * fa.ldy + col);
-  float4 o;
-  if (fa.accumulate) {
-    o = *yp;
-    o.x += scale * s[0]; o.y += scale * s[1]; o.z += scale * s[2]; o.w += scale * s[3];
-  } else {
-    o.x = scale * s[0]; o.y = scale * s[1]; o.z = scale * s[2]; o.w = scale * s[3];
-  }
-  *yp = o;
-}
-
 // W1 (WEIGHTED with one weight per edge, e.g. GCN / GraphSAGE-mean [E, 1]): the weights of a
 // 32-edge chunk arrive with its indices (lane l loads w[e + l]) and edge u's weight is broadcast
 // like its index (bcastG), instead of one load per edge per lane.
-template <bool WEIGHTED, int NT, bool W1 = false, bool FUSE = false, int MINW = 1>
-__global__ void __launch_bounds__(kBlock, MINW)  // MINW: waves per SIMD the register allocation must allow
+template <bool WEIGHTED, int NT, bool W1 = false>
+__global__ void __launch_bounds__(kBlock)
 k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
           uint32_t row_bytes, const float* __restrict__ w, int64_t ldw, float* __restrict__ slabs,
-          const SegItem* __restrict__ items, FuseArgs fa = FuseArgs{}) {
+          const SegItem* __restrict__ items) {
   constexpr int G = 32, F = 128, U = 8;
   const int lane = threadIdx.x & (kWave - 1);
   const int l32 = lane & (G - 1);
@@ -971,55 +799,6 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
     if (W1) wv = wvn;
     ic += G;
     if (WEIGHTED) wc += static_cast<int64_t>(G) * ldw;
-  }
-  if (FUSE) {
-    // Nothing of the epilogue stays live through the gather loop (the unfused kernel's 78 VGPRs,
-    // 6 waves per SIMD): the row is re-read from the item record (volatile: not kept from the
-    // first load) while the partial is stored, and its item count after.
-    if (len == 0) return;
-    const int col = l32 * 4;
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(slabs, 0, fa.slab_bytes, 0x00020000);
-    u32x4 pv;
-    pv.x = __float_as_uint(acc[0]); pv.y = __float_as_uint(acc[1]);
-    pv.z = __float_as_uint(acc[2]); pv.w = __float_as_uint(acc[3]);
-    __builtin_amdgcn_raw_buffer_store_b128(pv, rs, static_cast<int>(static_cast<uint32_t>(k) * (F * 4u) + col * 4u), 0,
-                                           16 /* sc1: write-through */);
-    const int row = *reinterpret_cast<const volatile int32_t*>(&items[k].row);
-    const int64_t j0 = fa.row_ptr[row], j1 = fa.row_ptr[row + 1];
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains before its ticket
-    if (j1 - j0 == 1) {  // the row's only item: y directly (0 + p, as the reduce would); its slab row is unread
-      const float s1[4] = {0.f + acc[0], 0.f + acc[1], 0.f + acc[2], 0.f + acc[3]};
-      fuse_store_row(fa, row, col, s1);
-      return;
-    }
-    int old = 0;
-    if (l32 == 0) old = __hip_atomic_fetch_add(fa.cnt + row, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __shfl(old, lane & G);
-    if (old != static_cast<int>(j1 - j0) - 1) return;  // not the last arriver of this row
-    float s4[4] = {0.f, 0.f, 0.f, 0.f};
-    for (int64_t j = j0; j < j1; j += G) {
-      const int n = static_cast<int>(min<int64_t>(G, j1 - j));
-      const int ids = (l32 < n) ? fa.row_items[j + l32] : 0;
-      constexpr int R = 4;  // partials in flight (the gather loop's registers are dead here)
-      for (int t = 0; t < n; t += R) {
-        u32x4 p[R];
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-          const uint32_t id = static_cast<uint32_t>(__shfl(ids, (lane & G) | ((t + u) & (G - 1))));
-          if (t + u < n)
-            p[u] = __builtin_amdgcn_raw_buffer_load_b128(rs, static_cast<int>(id * (F * 4u) + col * 4u), 0, 16 /* sc1 */);
-        }
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-          if (t + u < n) {
-            s4[0] += __uint_as_float(p[u].x); s4[1] += __uint_as_float(p[u].y);
-            s4[2] += __uint_as_float(p[u].z); s4[3] += __uint_as_float(p[u].w);
-          }
-        }
-      }
-    }
-    fuse_store_row(fa, row, col, s4);
-    return;
   }
   if (len > 0) {
     float* o = slabs + k * F + l32 * 4;
@@ -2340,19 +2119,25 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
 // Why not k_mm_rows: there each K chunk of W is staged synchronously (stage, barrier, compute)
 // and A fragments are loaded one 16-k step ahead, so at 4 waves per SIMD the MFMA pipe waits on
 // HBM latency (61 TF/s of 157 at K = 602).  Here both operands go global -> LDS by
-// global_load_lds (no VGPR staging), three 16-k stages deep, so every stage has two MFMA steps
-// of other stages (>= 4k cycles per SIMD) to land:
-//   block = 4 waves = 128 rows x BN = 16*NT columns; per 16-k stage wave w DMAs its own two
+// global_load_lds (no VGPR staging), D 16-k stages deep, so every stage has D - 1 MFMA steps of
+// other stages to land:
+//   block = 4 waves = 64*FR rows x BN = 16*NT columns; per 16-k stage wave w DMAs its own FR
 //   16-row A fragments (lane L = 16g + r holds x[row r][k0 + 4g .. +3], exactly the lane's MFMA
-//   fragment, so the ds_read is lane-linear: conflict-free) and NT/4 of the block's NT
-//   B fragments (W^T rows, same layout);
-//   per stage: counted s_waitcnt vmcnt (this wave's stage landed; the next stays in flight),
-//   lgkmcnt(0) (this wave's reads of the slot about to be refilled are done), raw s_barrier (every
-//   wave's DMA of the stage landed, every wave done with the old slot), then the DMA of stage
-//   s + 2 and the 16-k MFMA step of stage s (2 x NT x 4 v_mfma_f32_16x16x4_f32).
+//   fragment, so the ds_read is lane-linear: conflict-free; the DMA takes 16-B pieces at the 4-B /
+//   8-B aligned row starts of K = 602 / 1433 too) and NT/4 of the block's NT B fragments (W^T
+//   rows, same layout);
+//   per stage: counted s_waitcnt vmcnt (this wave's stage landed; the later stages stay in
+//   flight), lgkmcnt(0) (this wave's reads of the slot about to be refilled are done), raw s_barrier
+//   (every wave's DMA of the stage landed, every wave done with the old slot), then the DMA of
+//   stage s + D - 1 and the 16-k MFMA step of stage s (FR x NT x 4 v_mfma_f32_16x16x4_f32).
 // A K tail (K % 16) is one last step from registers with masked loads.  Rows past M and columns
 // past N read clamped rows and are not stored.  Same per-lane k order and fma chain as
-// k_mm_rows: results bitwise equal to it.  LDS: 3 x (8 + NT) KiB (48 KiB at N = 128: 3 blocks/CU).
+// k_mm_rows: results bitwise equal to it.  LDS: D x (4 FR + NT) KiB.
+//   D = 3: the persistent many-group form (48 KiB at FR = 2, N = 128: 3 blocks per CU);
+//   D = 4: two blocks per CU; D = 8: one block per CU, seven stages in flight -- the split-K
+//   form (one (row group, K slice) per block, every block resident at once) and grids of at most
+//   one block per CU, where a 3-deep ring leaves each stage waiting out an HBM round trip.
+// Split K (kslice > 0): block row y contracts k in [y * kslice, +kslice) into output slice y.
 // generic -> LDS address space, and the 32-bit LDS byte address (macros: a __device__ helper
 // taking or returning address-space-3 pointers keeps hipcc from emitting a template kernel's host stub)
 #define GTA_TO_LDS(p) ((__attribute__((address_space(3))) void*)(p))
@@ -2370,48 +2155,47 @@ __device__ __forceinline__ void ds_read16_idx(f32x4& v, uint32_t a, int c) {  //
     default: ds_read16<15 * 1024>(v, a); break;
   }
 }
-__device__ __forceinline__ void ds_read16_dyn(f32x4& v, uint32_t a, int c) {  // c: 1 KiB fragment index (unrolled)
-  switch (c) {
-    case 0: ds_read16<0>(v, a); break;
-    case 1: ds_read16<1024>(v, a); break;
-    case 2: ds_read16<2048>(v, a); break;
-    case 3: ds_read16<3072>(v, a); break;
-    case 4: ds_read16<4096>(v, a); break;
-    case 5: ds_read16<5120>(v, a); break;
-    case 6: ds_read16<6144>(v, a); break;
-    default: ds_read16<7168>(v, a); break;
+// s_waitcnt vmcnt(n * PS): everything but the last n stages of PS DMA instructions landed (n wave-uniform)
+template <int PS>
+__device__ __forceinline__ void vm_wait_stages(int n) {
+  switch (n) {
+#define GTA_VMW(N_) case N_: asm volatile("s_waitcnt vmcnt(%0)" ::"n"((N_) * PS) : "memory"); break;
+    GTA_VMW(1) GTA_VMW(2) GTA_VMW(3) GTA_VMW(4) GTA_VMW(5) GTA_VMW(6)
+#undef GTA_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
+// blocks per CU the ring's LDS allows (<= 4), the __launch_bounds__ waves per SIMD
+constexpr int ring_blocks(int NT, int D, int FR) {
+  return (160 / (D * (4 * FR + NT))) > 4 ? 4 : (160 / (D * (4 * FR + NT)));
+}
 
-// KH: 16-k halves per ring stage (1: 16-k stages, 2: 32-k stages, half the barriers); D: stages
-// FR: 16-row A fragments per wave (2: 128-row groups; 1: 64-row groups, twice as many work units
-// for the per-CU balance, half the MFMAs per B-fragment read)
-template <int NT, bool A4 = false, int KH = 1, int D = 3, int FR = 2>  // A4: x rows not 16-B aligned: 4-B A DMA
-__global__ void __launch_bounds__(kBlock, (FR == 1 ? 4 : (KH == 1 ? (D == 2 ? 4 : 3) : (D == 2 ? 2 : 1))))  // waves per SIMD = blocks per CU (LDS)
+template <int NT, int D = 3, int FR = 2>
+__global__ void __launch_bounds__(kBlock, ring_blocks(NT, D, FR))
 k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const float* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
-          int vec_store, int tuning_prio = 0, int kslice = 0, int64_t slice_stride = 0) {
+          int kslice = 0, int64_t slice_stride = 0) {
   static_assert(NT == 4 || NT == 8, "B fragments split evenly over the 4 waves");
-  if (kslice > 0) {  // split K: block row y takes k in [y * kslice, +kslice) into output slice y
+  static_assert(FR == 1 || FR == 2, "one or two A fragments per wave");
+  static_assert(D >= 3 && D <= 8, "ring depth");
+  if (kslice > 0) {
     const int k0 = static_cast<int>(blockIdx.y) * kslice;
     x += k0;
     wt += k0;
     K = min(kslice, K - k0);
     out += static_cast<int64_t>(blockIdx.y) * slice_stride;
   }
-  static_assert(KH == 1 || KH == 2, "16- or 32-k stages");
-  static_assert(FR == 1 || FR == 2, "one or two A fragments per wave");
-  constexpr int KS = 16 * KH, BN = 16 * NT, GR = 64 * FR;  // GR: rows per group
-  // stage image: A [wave][i][h] then B [c][h], 1 KiB fragments (16 rows x 16 k)
-  constexpr int A_BYTES = 4 * FR * KH * 1024, STAGE = A_BYTES + NT * KH * 1024;
-  constexpr int PER_STAGE = KH * ((A4 ? 4 * FR : FR) + NT / 4);  // DMA instructions per wave per stage
+  constexpr int KS = 16, BN = 16 * NT, GR = 64 * FR;  // GR: rows per group
+  // stage image: A [wave][i] then B [c], 1 KiB fragments (16 rows x 16 k)
+  constexpr int A_BYTES = 4 * FR * 1024, STAGE = A_BYTES + NT * 1024;
+  constexpr int PER_STAGE = FR + NT / 4;  // DMA instructions per wave per stage
   __shared__ __attribute__((aligned(16))) char lds[D * STAGE];
   const int lane = threadIdx.x & (kWave - 1);
   const int wv = wave_id_uniform();
   const int g = lane >> 4, r16 = lane & 15;
   const int ncb = (N + BN - 1) / BN;
   const int n0 = static_cast<int>(blockIdx.x % ncb) * BN;
-  // persistent: this block's 128-row groups are grp0, grp0 + gstep, ...; the ring runs on across
+  // persistent: this block's row groups are grp0, grp0 + gstep, ...; the ring runs on across
   // them (stage t = (group j, 16-k step s)), so the next group's first stages land while this
   // group finishes and no block pays a prologue after the first
   const int64_t grp0 = blockIdx.x / ncb, gstep = gridDim.x / ncb;
@@ -2425,9 +2209,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     const int n = min(n0 + 16 * (wv * (NT / 4) + t) + r16, N - 1);
     bsrc[t] = wt + static_cast<int64_t>(n) * ldwt + 4 * g;
   }
-  // A source rows of group j: A4: a 4-B DMA instruction p fills reader lanes 16p .. 16p + 15 of
-  // the fragment image, so DMA lane L loads x[row L/4][k0 + 4p + L%4]; 16-B form: lane (g, r16)
-  // loads x[row r16][k0 + 4g .. +3], its own MFMA fragment
+  // A source row of group j, fragment i, fragment row sub
   auto a_row = [&](int64_t j, int i, int sub) __attribute__((always_inline)) -> const float* {
     const int64_t m = min<int64_t>((grp0 + j * gstep) * GR + wv * (16 * FR) + 16 * i + sub, M - 1);
     return x + (row_idx ? static_cast<int64_t>(row_idx[m]) : m) * ldx;
@@ -2443,7 +2225,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     const int k = iss_s * KS;
     if (j != asrc_j) {
 #pragma unroll
-      for (int i = 0; i < FR; ++i) asrc[i] = a_row(j, i, A4 ? lane >> 2 : r16) + (A4 ? (lane & 3) : 4 * g);
+      for (int i = 0; i < FR; ++i) asrc[i] = a_row(j, i, r16) + 4 * g;
       asrc_j = j;
     }
     char* base = lds + iss_slot * STAGE;
@@ -2453,24 +2235,13 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
       ++iss_j;
     }
 #pragma unroll
-    for (int h = 0; h < KH; ++h) {
+    for (int i = 0; i < FR; ++i)
+      __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[i] + k), GTA_TO_LDS(base + (wv * FR + i) * 1024), 16, 0,
+                                       0);
 #pragma unroll
-      for (int i = 0; i < FR; ++i) {
-        char* dst = base + ((wv * FR + i) * KH + h) * 1024;
-        if constexpr (A4) {
-#pragma unroll
-          for (int p = 0; p < 4; ++p)
-            __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[i] + k + 16 * h + 4 * p), GTA_TO_LDS(dst + p * 256),
-                                             4, 0, 0);
-        } else {
-          __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[i] + k + 16 * h), GTA_TO_LDS(dst), 16, 0, 0);
-        }
-      }
-#pragma unroll
-      for (int q = 0; q < NT / 4; ++q)
-        __builtin_amdgcn_global_load_lds(const_cast<float*>(bsrc[q] + k + 16 * h),  // (a const source fails the host pass)
-                                         GTA_TO_LDS(base + A_BYTES + ((wv * (NT / 4) + q) * KH + h) * 1024), 16, 0, 0);
-    }
+    for (int q = 0; q < NT / 4; ++q)
+      __builtin_amdgcn_global_load_lds(const_cast<float*>(bsrc[q] + k),  // (a const source fails the host pass)
+                                       GTA_TO_LDS(base + A_BYTES + (wv * (NT / 4) + q) * 1024), 16, 0, 0);
   };
   f32x4 acc[FR][NT];
   auto zero_acc = [&]() __attribute__((always_inline)) {
@@ -2486,7 +2257,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
 #pragma unroll
       for (int i = 0; i < FR; ++i) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(av[i][j], bj[j], acc[i][c], 0, 0, 0);
   };
-  const bool vstore = vec_store && ldo % 4 == 0 && aligned(out, 16);
+  const bool vstore = ldo % 4 == 0 && aligned(out, 16);
   auto epilogue = [&](int64_t j) __attribute__((always_inline)) {
     const int64_t mw = (grp0 + j * gstep) * GR + wv * (16 * FR);
     if (vstore) {  // quad-transposed 16-B row stores (k_mm_rows' epilogue)
@@ -2569,8 +2340,8 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   for (int s = 0; s < S; ++s, ++t, slot = slot + 1 == D ? 0 : slot + 1) {
     // stage t landed (stages t+1 .. t+D-2 may stay in flight), every wave done with the slot
     // about to be refilled (read at t-1)
-    if (D == 3 && t + 1 < T) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER_STAGE) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int64_t later = T - 1 - t;
+    vm_wait_stages<PER_STAGE>(static_cast<int>(later < D - 2 ? later : D - 2));
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -2578,38 +2349,27 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     // fragment reads in inline asm: hipcc cannot tell them apart from the DMA in flight into
     // another slot and would wait vmcnt(0) before a plain LDS read (draining the ring every step).
     // The asm wait names every loaded register, so no MFMA is scheduled above it.
-    // all the stage's fragment reads issued at once; half h's MFMAs start when its reads are in
-    // (LDS returns in order: lgkmcnt(reads of the later halves))
-    const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * KH * 1024) + static_cast<uint32_t>(lane) * 16u;
+    const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * 1024) + static_cast<uint32_t>(lane) * 16u;
     const uint32_t sb = GTA_LDS_ADDR(lds + slot * STAGE + A_BYTES) + static_cast<uint32_t>(lane) * 16u;
-    f32x4 a4[KH][FR], b4[KH][NT];
+    f32x4 a4[FR], b4[NT];
 #pragma unroll
-    for (int h = 0; h < KH; ++h) {
+    for (int i = 0; i < FR; ++i) ds_read16_idx(a4[i], sa, i);
 #pragma unroll
-      for (int i = 0; i < FR; ++i) ds_read16_idx(a4[h][i], sa, i * KH + h);
+    for (int c = 0; c < NT; ++c) ds_read16_idx(b4[c], sb, c);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-      for (int c = 0; c < NT; ++c) ds_read16_idx(b4[h][c], sb, c * KH + h);
-    }
+    for (int i = 0; i < FR; ++i) asm volatile("" : "+v"(a4[i]));
 #pragma unroll
-    for (int h = 0; h < KH; ++h) {
-      if (h + 1 < KH) asm volatile("s_waitcnt lgkmcnt(%0)" :: "n"(FR + NT) : "memory");
-      else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(b4[c]));
+    // j outermost: the FR x NT accumulators are each touched once per FR*NT MFMAs; per
+    // accumulator the k order is k_mm_rows' (bitwise equal)
 #pragma unroll
-      for (int i = 0; i < FR; ++i) asm volatile("" : "+v"(a4[h][i]));
+    for (int jj = 0; jj < 4; ++jj)
 #pragma unroll
-      for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(b4[h][c]));
-      // j outermost: the 2 x NT accumulators are each touched once per 2*NT MFMAs; per
-      // accumulator the k order is k_mm_rows' (bitwise equal)
-      if (tuning_prio) __builtin_amdgcn_s_setprio(1);
+      for (int c = 0; c < NT; ++c)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int c = 0; c < NT; ++c)
-#pragma unroll
-          for (int i = 0; i < FR; ++i)
-            acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[h][i][j], b4[h][c][j], acc[i][c], 0, 0, 0);
-      if (tuning_prio) __builtin_amdgcn_s_setprio(0);
-    }
+        for (int i = 0; i < FR; ++i)
+          acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i][jj], b4[c][jj], acc[i][c], 0, 0, 0);
   }
   // the group's last stage is done: its K tail, its rows out, the next group's sums
   if (K % KS) tail(j);
@@ -2621,7 +2381,9 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   }
 }
 
-// out[m, n] = sf(sum_s ws[s][m][n]) in slice order (split-K UPDATE; ws slices are [M, N] dense)
+// out[m, n] = sf(sum_s ws[s][m][n]) in slice order (split-K UPDATE; ws slices are [M, N] dense).
+// Float4 form: four consecutive columns per thread, the slices' loads issued four at a time, the
+// adds in slice order (bitwise equal to the scalar form).
 __global__ void __launch_bounds__(kBlock)
 k_mm_slices_sum(const float* __restrict__ ws, int S, int64_t M, int N, int sf, float* __restrict__ out, int64_t ldo) {
   const int64_t total = M * N;
@@ -2631,6 +2393,33 @@ k_mm_slices_sum(const float* __restrict__ ws, int S, int64_t M, int N, int sf, f
     for (int k = 0; k < S; ++k) a += ws[k * total + t];
     const int64_t m = t / N;
     out[m * ldo + (t - m * N)] = sf_apply(sf, a);
+  }
+}
+
+__global__ void __launch_bounds__(kBlock)
+k_mm_slices_sum4(const float4* __restrict__ ws, int S, int64_t M, int N4, int sf, float* __restrict__ out,
+                 int64_t ldo) {
+  const int64_t total4 = M * N4;
+  for (int64_t t = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; t < total4;
+       t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
+    float4 a = make_float4(0.f, 0.f, 0.f, 0.f);
+    int k = 0;
+    for (; k + 4 <= S; k += 4) {
+      float4 v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = ws[(k + u) * total4 + t];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a.x += v[u].x; a.y += v[u].y; a.z += v[u].z; a.w += v[u].w;
+      }
+    }
+    for (; k < S; ++k) {
+      const float4 v = ws[k * total4 + t];
+      a.x += v.x; a.y += v.y; a.z += v.z; a.w += v.w;
+    }
+    const int64_t m = t / N4;
+    *reinterpret_cast<float4*>(out + m * ldo + (t - m * N4) * 4) =
+        make_float4(sf_apply(sf, a.x), sf_apply(sf, a.y), sf_apply(sf, a.z), sf_apply(sf, a.w));
   }
 }
 
@@ -2672,89 +2461,57 @@ void launch_agg(const AggArgs& a, int64_t n_items_bound, hipStream_t s) {
 }
 
 template <int LPE, int VW, int NV, int XM>
-bool dispatch_w(int wm, bool nt, const AggArgs& a, int64_t nb, hipStream_t s) {
+bool dispatch_w(int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
+  // (non-temporal index/weight loads measured +3 %: plain loads throughout)
   switch (wm) {
     case WM_NONE: launch_agg<LPE, VW, NV, XM, WM_NONE, false>(a, nb, s); return true;
-    case WM_HEAD:
-      // non-temporal index/weight streams only where they pay: the SpMM (XM_IDX) form
-      if (XM == XM_IDX && nt) launch_agg<LPE, VW, NV, XM, WM_HEAD, true>(a, nb, s);
-      else launch_agg<LPE, VW, NV, XM, WM_HEAD, false>(a, nb, s);
-      return true;
+    case WM_HEAD: launch_agg<LPE, VW, NV, XM, WM_HEAD, false>(a, nb, s); return true;
     case WM_FULL: launch_agg<LPE, VW, NV, XM, WM_FULL, false>(a, nb, s); return true;
   }
   return false;
 }
 
 template <int LPE, int VW, int NV>
-bool dispatch_x(int xm, int wm, bool nt, const AggArgs& a, int64_t nb, hipStream_t s) {
-  return xm == XM_EDGE ? dispatch_w<LPE, VW, NV, XM_EDGE>(wm, false, a, nb, s)
-                       : dispatch_w<LPE, VW, NV, XM_IDX>(wm, nt, a, nb, s);
+bool dispatch_x(int xm, int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
+  return xm == XM_EDGE ? dispatch_w<LPE, VW, NV, XM_EDGE>(wm, a, nb, s) : dispatch_w<LPE, VW, NV, XM_IDX>(wm, a, nb, s);
 }
 
 template <int VW>
-bool dispatch_lpe(int lpe, int nv, int xm, int wm, bool nt, const AggArgs& a, int64_t nb, hipStream_t s) {
+bool dispatch_lpe(int lpe, int nv, int xm, int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
   switch (lpe) {
     case 64:
-      if (nv == 1) return dispatch_x<64, VW, 1>(xm, wm, nt, a, nb, s);
-      if (nv == 2) return dispatch_x<64, VW, 2>(xm, wm, nt, a, nb, s);
-      return dispatch_x<64, VW, 4>(xm, wm, nt, a, nb, s);
-    case 32: return dispatch_x<32, VW, 1>(xm, wm, nt, a, nb, s);
-    case 16: return dispatch_x<16, VW, 1>(xm, wm, nt, a, nb, s);
-    case 8: return dispatch_x<8, VW, 1>(xm, wm, nt, a, nb, s);
-    default: return dispatch_x<4, VW, 1>(xm, wm, nt, a, nb, s);
+      if (nv == 1) return dispatch_x<64, VW, 1>(xm, wm, a, nb, s);
+      if (nv == 2) return dispatch_x<64, VW, 2>(xm, wm, a, nb, s);
+      return dispatch_x<64, VW, 4>(xm, wm, a, nb, s);
+    case 32: return dispatch_x<32, VW, 1>(xm, wm, a, nb, s);
+    case 16: return dispatch_x<16, VW, 1>(xm, wm, a, nb, s);
+    case 8: return dispatch_x<8, VW, 1>(xm, wm, a, nb, s);
+    default: return dispatch_x<4, VW, 1>(xm, wm, a, nb, s);
   }
 }
 
-// Tuning knobs (benchmark hooks, gta_debug_set): per calling THREAD, so a knob set by one thread
-// never changes another thread's concurrent calls; a call reads its own thread's values.  The
-// defaults are the measured choices.
+// Tuning knobs (gta_debug_set / gta_tuning_*): per calling THREAD, or per stream when a knob set
+// is attached to it, so a knob set by one caller never changes another's calls.  The defaults are
+// the measured choices.  Every knob selects between forms that the defaults reach on
+// some shape (the bitwise form-equality tests use them) or splits a launch for per-kernel timing;
+// variants measured slower and reachable only by a knob were removed in round 3 (their A/B numbers
+// stay in DESIGN.md).
 struct Tuning {
-  int force_lpe = 0;  // tuning hooks (gta_debug_set); 0 = automatic
-  int force_vw = 0;
-  int agg_nt = 0;     // non-temporal index/weight loads in the SpMM form
-  int agg_lean = 1;   // k_agg_lean for F = 64*VW SpMM shapes
-  int64_t seg_waves = 0;  // persistent waves of the column-blocked kernel (0 = 8 per SIMD)
-  int seg_quarter = 1;     // quarter-wave (4 items per wave) form of the blocked aggregate
-  int seg_lanes = 32;      // lanes per item of that form at F = 128: 32 (2 items/wave, measured 3 % faster) or 16
-  int seg_nt = 3;          // non-temporal bits of the multi-item forms at F = 128, U = 8: 2 = slab stores (-1 %);
-                           // k_agg_h32 (8 heads): 3 = + index loads (-0.5 %: 4.829 vs 4.852 ms), 6/7 = weight
-                           // loads too (+3 %), profiles/r02_nt_bits_ab.json
-  int seg_u = 8;           // edges per unrolled step of the quarter-wave form (F = 128: 2, 4 or 8)
+  int force_lpe = 0;       // k_aggregate lanes per edge (0 = automatic; 32 = float4 lanes at F = 128)
+  int force_vw = 0;        // k_aggregate floats per lane (0 = widest aligned)
+  int agg_lean = 1;        // k_agg_lean for F = 64*VW SpMM shapes (0: k_aggregate, the form of other shapes)
   int seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
-  int apply_node_vec = 1;  // k_apply_node4 (float4, 32-bit index math) for the common apply_node shapes
   int seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
-  int plan_len_sort = 1;   // blocked plan: each block's items sorted by length (matched half-wave pairs)
+  int seg_phase = 0;       // blocked aggregate: 0 = items + reduce, 1 = items only, 2 = reduce only (bench timing)
+  int att_lean = 1;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads (0: the generic half-wave form)
   int att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
-  int att_lean = 2;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads: 1 on, 2 + NT slab stores (default), 0 off
-  int mm_blaslt = 1;        // plain fp32 UPDATE with mm_blaslt_min_m <= M <= mm_blaslt_max_m on hipBLASLt
-  int64_t mm_blaslt_min_m = 1024;
-  int64_t mm_blaslt_max_m = 65535;  // from 65,536 rows (>= 512 row groups: >= 2 ring blocks per CU) k_mm_ring takes
-                                    // the product: 0.92-0.95x the library's first choice on Reddit / products shapes,
-                                    // equal on Flickr's, and bitwise the same in every process (profiles/r02_mm_ring_*)
-  int mm_blaslt_tune = 0;  // 1: time the heuristic's top candidates at a shape's first use (faster, but the pick
-                            // can differ between processes: ranks could disagree bitwise); 0: its first choice
-  int mm_ring = 1;          // fp32 UPDATE on k_mm_ring (LDS-DMA ring) instead of k_mm_rows
-  int64_t mm_ring_blocks_per_cu = 0;  // k_mm_ring persistent grid: blocks per CU (0 = what LDS allows)
-  int mm_ring_form = 0;      // k_mm_ring stages: 0 = 16 k x 3 stages, 1 = 32 k x 2, 2 = 32 k x 3, 3 = 16 k x 2
-  int mm_ring_prio = 0;      // k_mm_ring: raise the wave priority around its MFMA block (+-3 %: noise, r02_mm_ab*)
-  int mm_ring_fr = 0;        // k_mm_ring A fragments per wave: 2 = 128-row groups, 1 = 64-row groups (form 0),
-                             // 0 = auto: 64-row groups for K <= 256 when 128-row groups load the CUs unevenly,
-                             // or below 512 128-row groups (K = 128 / 256 at 232,965 rows: 77 -> 87 / 90 -> 96
-                             // TF/s; 16,384 rows 40 -> 69; K = 602 and 2.45 M-row K = 100 stay on 128-row
-                             // groups: 95 against 93, 69 against 64; profiles/r02_mm_ring_probe_fr.json)
-  int mm_ring_tail = 0;      // k_mm_ring: uneven 128-row groups on a long K: whole rounds, then the rest as 64-row groups
-                             // in a second launch (bitwise equal; measured 94.7 vs 96.8 TF/s at K = 602: off)
-  int mm_ring_a16u = 1;      // k_mm_ring: 16-B A DMA pieces also when x rows are only 4-B aligned (K = 602)
-  int mm_vstore = 1;        // k_mm_rows epilogue: quad-transposed 16-B row stores (0 = four dword stores)
-  int mm_prefetch = 1;      // k_mm_rows A prefetch (<= 128 VGPRs, 4 waves/SIMD): 1 auto, 2 always, 0 never
-  int64_t mm_blocks_per_cu = 0;  // k_mm_rows persistent grid: blocks per CU (0 = 8)
-  int apply_edge_form = 1;  // 1: row-sweep K3 kernels (cols / pack); 0: the generic per-element kernel
+  int apply_node_vec = 1;  // k_apply_node4 (float4, 32-bit index math) for the common apply_node shapes
+  int apply_edge_form = 1; // 1: row-sweep K3 kernels (cols / pack); 0: the generic per-element kernel
   int esm_lane = 1;        // edge-per-lane edge-softmax when H in {4,8,16} and rows are 16-B aligned
-  int esm_keep = 4;        // chunks of 64 edges held in VGPRs by the edge-per-lane form (2 or 4)
-  int seg_phase = 0;         // single-launch blocked aggregate: 0 = items + reduce, 1 = items only, 2 = reduce only
-  int seg_fuse = 0;          // k_agg_h32 with the in-launch ordered reduce (no k_seg_reduce pass): bitwise equal,
-                             // but 5.28 vs 4.93 ms on Reddit (the per-item drain + ticket costs more than the
-                             // pass it removes; profiles/r02_fused_reduce_ab.json); 2 = the same at 6 waves/SIMD
+  int mm_ring = 1;         // fp32 UPDATE on k_mm_ring (LDS-DMA ring) instead of k_mm_rows
+  int mm_ring_fr = 0;      // k_mm_ring A fragments per wave: 2 = 128-row groups, 1 = 64-row groups, 0 = auto
+  int mm_prefetch = 1;     // k_mm_rows A prefetch: 1 auto, 2 always, 0 never
+  int64_t mm_split = -1;   // UPDATE K slices: -1 auto, 0 = never split, n = n slices
 };
 
 Tuning& thread_tuning() {  // gta_debug_set / gta_debug_get: the calling thread's knobs
@@ -2799,38 +2556,19 @@ const Knob* find_knob(const char* key) {
   static const Knob knobs[] = {
       {"agg_lpe", &Tuning::force_lpe, nullptr},
       {"agg_vw", &Tuning::force_vw, nullptr},
-      {"agg_nt", &Tuning::agg_nt, nullptr},
       {"agg_lean", &Tuning::agg_lean, nullptr},
-      {"seg_waves", nullptr, &Tuning::seg_waves},
-      {"seg_nt", &Tuning::seg_nt, nullptr},
-      {"seg_u", &Tuning::seg_u, nullptr},
-      {"seg_lanes", &Tuning::seg_lanes, nullptr},
       {"seg_lean", &Tuning::seg_lean, nullptr},
-      {"seg_fuse", &Tuning::seg_fuse, nullptr},
+      {"seg_lean_w1", &Tuning::seg_lean_w1, nullptr},
       {"seg_phase", &Tuning::seg_phase, nullptr},
       {"att_lean", &Tuning::att_lean, nullptr},
       {"att_direct", &Tuning::att_direct, nullptr},
-      {"plan_len_sort", &Tuning::plan_len_sort, nullptr},
-      {"seg_lean_w1", &Tuning::seg_lean_w1, nullptr},
       {"apply_node_vec", &Tuning::apply_node_vec, nullptr},
-      {"seg_quarter", &Tuning::seg_quarter, nullptr},
-      {"mm_prefetch", &Tuning::mm_prefetch, nullptr},
-      {"mm_blaslt", &Tuning::mm_blaslt, nullptr},
-      {"mm_blaslt_min_m", nullptr, &Tuning::mm_blaslt_min_m},
-      {"mm_blaslt_max_m", nullptr, &Tuning::mm_blaslt_max_m},
-      {"mm_blaslt_tune", &Tuning::mm_blaslt_tune, nullptr},
-      {"mm_vstore", &Tuning::mm_vstore, nullptr},
-      {"mm_ring", &Tuning::mm_ring, nullptr},
-      {"mm_ring_blocks_per_cu", nullptr, &Tuning::mm_ring_blocks_per_cu},
-      {"mm_ring_form", &Tuning::mm_ring_form, nullptr},
-      {"mm_ring_prio", &Tuning::mm_ring_prio, nullptr},
-      {"mm_ring_a16u", &Tuning::mm_ring_a16u, nullptr},
-      {"mm_ring_fr", &Tuning::mm_ring_fr, nullptr},
-      {"mm_ring_tail", &Tuning::mm_ring_tail, nullptr},
-      {"mm_blocks_per_cu", nullptr, &Tuning::mm_blocks_per_cu},
       {"apply_edge_form", &Tuning::apply_edge_form, nullptr},
       {"esm_lane", &Tuning::esm_lane, nullptr},
-      {"esm_keep", &Tuning::esm_keep, nullptr},
+      {"mm_ring", &Tuning::mm_ring, nullptr},
+      {"mm_ring_fr", &Tuning::mm_ring_fr, nullptr},
+      {"mm_prefetch", &Tuning::mm_prefetch, nullptr},
+      {"mm_split", nullptr, &Tuning::mm_split},
   };
   const std::string k(key ? key : "");
   for (const Knob& kb : knobs)
@@ -2996,9 +2734,9 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
     const int64_t blocks = (bound + kWavesPerBlock - 1) / kWavesPerBlock;
     const dim3 grid(static_cast<unsigned>(blocks)), blk(kBlock);
 #define GTA_LEAN(VW_, GL_)                                                                                   \
-  k_agg_lean<VW_, GL_, false><<<grid, blk, 0, s>>>(a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, \
-                                                   a.x, a.ldx, a.F, a.w, a.ldw, a.row_scale, a.y, a.ldy,        \
-                                                   a.accumulate, a.partial, SegView{})
+  k_agg_lean<VW_, GL_><<<grid, blk, 0, s>>>(a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, \
+                                            a.x, a.ldx, a.F, a.w, a.ldw, a.row_scale, a.y, a.ldy, a.accumulate, \
+                                            a.partial)
     if (vw == 2) {
       if (gl == 0) GTA_LEAN(2, 0); else if (gl == 4) GTA_LEAN(2, 4); else if (gl == 8) GTA_LEAN(2, 8); else GTA_LEAN(2, 16);
     } else if (vw == 4) {
@@ -3010,9 +2748,9 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
     ok = true;
   }
   if (!ok) switch (vw) {
-    case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, tuning().agg_nt != 0, a, bound, s); break;
-    case 2: ok = dispatch_lpe<2>(lpe, nv, xm, wm, tuning().agg_nt != 0, a, bound, s); break;
-    default: ok = dispatch_lpe<1>(lpe, nv, xm, wm, tuning().agg_nt != 0, a, bound, s); break;
+    case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, a, bound, s); break;
+    case 2: ok = dispatch_lpe<2>(lpe, nv, xm, wm, a, bound, s); break;
+    default: ok = dispatch_lpe<1>(lpe, nv, xm, wm, a, bound, s); break;
   }
   if (!ok) return fail(GTA_ERR_UNSUPPORTED, "aggregate: no kernel variant");
   GTA_LAUNCHED("k_aggregate");
@@ -3072,7 +2810,7 @@ int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indic
   GTA_HIP(hipMemsetAsync(v.lhist, 0, 64 * kLenBins * 4, s));
   k_blocked_items<<<gk, dim3(256), 0, s>>>(indptr, n_rows, B, item_edges, row_edges, v);
   GTA_LAUNCHED("k_blocked_items");
-  if (tuning().plan_len_sort && mi > 0) {
+  if (mi > 0) {  // each block's items longest first (matched half-wave pairs; only item ids move)
     k_items_len_scan<<<1, 64, 0, s>>>(v, n_rows, B);
     GTA_LAUNCHED("k_items_len_scan");
     k_items_permute<<<dim3(static_cast<unsigned>((mi + 255) / 256)), dim3(256), 0, s>>>(v, n_rows, B);
@@ -3082,15 +2820,13 @@ int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indic
   return GTA_OK;
 }
 
-// workspace of gta_aggregate_blocked: [arrival counters, one int32 per row, padded to 256 B][slab rows]
-inline int64_t blocked_cnt_bytes(int64_t n_rows) { return (n_rows * 4 + 255) / 256 * 256; }
+// workspace of gta_aggregate_blocked: the slab rows, one [F] fp32 partial per plan item
 
 int64_t gta_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t F,
                                               int64_t item_edges) {
   if (n_rows < 0 || nnz < 0 || blocks < 1 || blocks > 63 || F <= 0 || item_edges < 1)
     return fail(GTA_ERR_ARG, "blocked_workspace_bytes: bad sizes");
-  return blocked_cnt_bytes(n_rows) +
-         blocked_max_items(n_rows, nnz, static_cast<int>(blocks), item_edges) * F * static_cast<int64_t>(sizeof(float));
+  return blocked_max_items(n_rows, nnz, static_cast<int>(blocks), item_edges) * F * static_cast<int64_t>(sizeof(float));
 }
 
 int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols, int64_t nnz,
@@ -3121,94 +2857,52 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
   const int64_t mi = blocked_max_items(n_rows, nnz, B, item_edges);
   BlockedView v = blocked_view(const_cast<void*>(plan), n_rows, B, mi);
   hipStream_t s = S(stream);
-  if (workspace) {  // single launch into per-item slab rows + ordered reduce
-    const RowItems ri{v.row_ptr, v.row_items};
-    int32_t* cnt = static_cast<int32_t*>(workspace);
-    float* slabs = reinterpret_cast<float*>(static_cast<char*>(workspace) + blocked_cnt_bytes(n_rows));
-    const int64_t items = mi;  // grid bound; the kernels stop at the plan's n_items
-    const int64_t* nit = &v.hdr[4];
-    const SegItem* its = v.items;
-    const dim3 g2(static_cast<unsigned>((items + kWavesPerBlock - 1) / kWavesPerBlock)), blk2(kBlock);
-    const int vq = static_cast<int>(F / 16);
-    const int lph = w ? static_cast<int>((F / heads) / vq) : 0;
-    const bool quarter = tuning().seg_quarter && (vq == 4 || vq == 8 || vq == 16) && ldx % 4 == 0 && aligned(x, 16) &&
-                         (!w || ((F / heads) % vq == 0 && lph >= 1 && 16 % lph == 0));
-    const int phase = tuning().seg_phase;
-    if (items == 0 || phase == 2) {
-      // no edges: no items; the reduce below writes the (empty) rows (phase 2: the reduce only)
-    } else if (quarter) {
-      const dim3 g4(static_cast<unsigned>((items + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock)));
-#define GTA_SEG4(VW_, U_)                                                                                   \
-  if (w) k_agg_seg4<VW_, U_, true><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its);     \
-  else k_agg_seg4<VW_, U_, false><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its)
-#define GTA_SEG4NT(VW_, U_, NT_)                                                                             \
-  if (w) k_agg_seg4<VW_, U_, true, NT_><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its); \
-  else k_agg_seg4<VW_, U_, false, NT_><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its)
-      if (vq == 8 && tuning().seg_lanes == 32) {  // half-wave items: 32 lanes x float4
-        const int lph32 = w ? static_cast<int>((F / heads) / 4) : 0;
-        const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
-        const bool lean = tuning().seg_lean && tuning().seg_u == 8 && n_cols < (1 << 24) &&
-                          static_cast<uint64_t>(n_cols) * static_cast<uint64_t>(ldx) * 4u < (1ull << 32) &&
-                          (!w || lph32 == 4 || (heads == 1 && tuning().seg_lean_w1 && ldw < (int64_t(1) << 24)));
-        const uint32_t rb = static_cast<uint32_t>(ldx * 4);
-        const bool fuse = lean && tuning().seg_fuse && static_cast<uint64_t>(mi) * F * 4u < (1ull << 32);
-        if (fuse) {  // in-launch ordered reduce: no k_seg_reduce pass
-          const FuseArgs fa{v.row_ptr, v.row_items, cnt, row_scale, y, ldy, accumulate,
-                            static_cast<uint32_t>(mi * F * 4)};
-          k_fuse_prep<<<dim3(static_cast<unsigned>((n_rows + kBlock - 1) / kBlock)), blk2, 0, s>>>(n_rows, 128, fa);
-          GTA_LAUNCHED("k_fuse_prep");
-          if (w && heads == 1) k_agg_h32<true, 2, true, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its, fa);
-          else if (!w) k_agg_h32<false, 2, false, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its, fa);
-          else if (tuning().seg_fuse == 2)
-            k_agg_h32<true, 2, false, true, 6><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its, fa);
-          else k_agg_h32<true, 2, false, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its, fa);
-          GTA_LAUNCHED("k_agg_h32 (fused reduce)");
-          return GTA_OK;
-        }
-        if (lean) {
-          if (w && heads == 1) k_agg_h32<true, 2, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (!w && (tuning().seg_nt & 2)) k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (!w) k_agg_h32<false, 0><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (tuning().seg_nt == 2) k_agg_h32<true, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (tuning().seg_nt == 1) k_agg_h32<true, 5><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (tuning().seg_nt == 3) k_agg_h32<true, 3><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (tuning().seg_nt == 6) k_agg_h32<true, 6><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else if (tuning().seg_nt == 7) k_agg_h32<true, 7><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-          else k_agg_h32<true, 0><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-        } else if (w && lph32 >= 1 && 32 % lph32 == 0 && (F / heads) % 4 == 0) {
-          if (tuning().seg_u == 4)
-            k_agg_seg4<4, 4, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
-                                                                         lph32, slabs, its);
-          else if (tuning().seg_u == 16)
-            k_agg_seg4<4, 16, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
-                                                                          lph32, slabs, its);
-          else if (tuning().seg_nt == 1)
-            k_agg_seg4<4, 8, true, 1, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
-                                                                         lph32, slabs, its);
-          else if (tuning().seg_nt == 2 || tuning().seg_nt == 3)  // (3: the lean kernel's default)
-            k_agg_seg4<4, 8, true, 2, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
-                                                                         lph32, slabs, its);
-          else
-            k_agg_seg4<4, 8, true, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw,
-                                                                         lph32, slabs, its);
-        }
-        else if (!w)
-          k_agg_seg4<4, 8, false, 0, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, 0,
-                                                                        slabs, its);
-        else
-          return fail(GTA_ERR_UNSUPPORTED, "aggregate_blocked: half-wave head layout");
-      } else if (vq == 4) { GTA_SEG4(4, 4); }
-      else if (vq == 8) {
-        if (tuning().seg_u == 2) { GTA_SEG4(8, 2); } else if (tuning().seg_u == 4) { GTA_SEG4(8, 4); }
-        else if (tuning().seg_nt == 1) { GTA_SEG4NT(8, 8, 1); } else if (tuning().seg_nt == 2) { GTA_SEG4NT(8, 8, 2); }
-        else if (tuning().seg_nt == 3) { GTA_SEG4NT(8, 8, 3); } else { GTA_SEG4(8, 8); }
-      }
-      else { GTA_SEG4(16, 2); }
-#undef GTA_SEG4
-#undef GTA_SEG4NT
-      GTA_LAUNCHED("k_agg_seg4");
+  if (!workspace && nnz > 0) return fail(GTA_ERR_ARG, "aggregate_blocked: needs the slab workspace");
+  // one launch over the plan's items into per-item slab rows, then the ordered reduce
+  const RowItems ri{v.row_ptr, v.row_items};
+  float* slabs = static_cast<float*>(workspace);
+  const int64_t items = mi;  // grid bound; the kernels stop at the plan's n_items
+  const int64_t* nit = &v.hdr[4];
+  const SegItem* its = v.items;
+  const dim3 g2(static_cast<unsigned>((items + kWavesPerBlock - 1) / kWavesPerBlock)), blk2(kBlock);
+  const int vq = static_cast<int>(F / 16);
+  const int lph = w ? static_cast<int>((F / heads) / vq) : 0;
+  // multi-item waves (F = 64 / 256: four 16-lane items; F = 128: two 32-lane items, one 512-B row per
+  // half-wave instruction) when rows are 16-B aligned and the heads fit the lanes; else one item per wave
+  const bool quarter = (vq == 4 || vq == 8 || vq == 16) && ldx % 4 == 0 && aligned(x, 16) &&
+                       (!w || ((F / heads) % vq == 0 && lph >= 1 && 16 % lph == 0));
+  const int phase = tuning().seg_phase;
+  if (items == 0 || phase == 2) {
+    // no edges: no items; the reduce below writes the (empty) rows (phase 2: the reduce only)
+  } else if (quarter && vq == 8) {  // F = 128: half-wave items, 32 lanes x float4
+    const int lph32 = w ? static_cast<int>((F / heads) / 4) : 0;
+    const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
+    const bool lean = tuning().seg_lean && n_cols < (1 << 24) &&
+                      static_cast<uint64_t>(n_cols) * static_cast<uint64_t>(ldx) * 4u < (1ull << 32) &&
+                      (!w || lph32 == 4 || (heads == 1 && tuning().seg_lean_w1 && ldw < (int64_t(1) << 24)));
+    const uint32_t rb = static_cast<uint32_t>(ldx * 4);
+    // NT template bits: 1 = non-temporal index loads, 2 = non-temporal slab stores (measured -0.5 % / -1 %;
+    // non-temporal weight loads +3 %: profiles/r02_nt_bits_ab.json)
+    if (lean) {
+      if (w && heads == 1) k_agg_h32<true, 2, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+      else if (w) k_agg_h32<true, 3><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+      else k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+      GTA_LAUNCHED("k_agg_h32");
     } else {
-      if (!gl_ok) return fail(GTA_ERR_UNSUPPORTED, gl_msg);
+      if (w) k_agg_seg4<4, 8, true, 2, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph32, slabs, its);
+      else k_agg_seg4<4, 8, false, 2, false, -1, 32><<<g2h, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, 0, slabs, its);
+      GTA_LAUNCHED("k_agg_seg4<half>");
+    }
+  } else if (quarter) {  // F = 64 / 256: quarter-wave items
+    const dim3 g4(static_cast<unsigned>((items + 4 * kWavesPerBlock - 1) / (4 * kWavesPerBlock)));
+#define GTA_SEG4(VW_, U_)                                                                               \
+  if (w) k_agg_seg4<VW_, U_, true><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its); \
+  else k_agg_seg4<VW_, U_, false><<<g4, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, lph, slabs, its)
+    if (vq == 4) { GTA_SEG4(4, 4); } else { GTA_SEG4(16, 2); }
+#undef GTA_SEG4
+    GTA_LAUNCHED("k_agg_seg4");
+  } else {
+    if (!gl_ok) return fail(GTA_ERR_UNSUPPORTED, gl_msg);
 #define GTA_SEG2D(VW_, GL_) \
   k_agg_seg2d<VW_, GL_><<<g2, blk2, 0, s>>>(indices, nit, x, ldx, w, ldw, slabs, its)
     if (vw == 2) {
@@ -3220,34 +2914,13 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     }
 #undef GTA_SEG2D
     GTA_LAUNCHED("k_agg_seg2d");
-    }
-    if (phase == 1) return GTA_OK;  // the item launch only; a later phase-2 call reduces
-    const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
-    if (vw == 2) k_seg_reduce<2><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, ri);
-    else if (vw == 4) k_seg_reduce<4><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, ri);
-    else k_seg_reduce<1><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, ri);
-    GTA_LAUNCHED("k_seg_reduce");
-    return GTA_OK;
   }
-  if (!gl_ok) return fail(GTA_ERR_UNSUPPORTED, gl_msg);
-  // persistent waves: enough for 8 per SIMD on every CU, never more than one per row
-  const int64_t waves = std::min<int64_t>(n_rows, tuning().seg_waves > 0 ? tuning().seg_waves : 256 * 32);
-  const dim3 grid(static_cast<unsigned>((waves + kWavesPerBlock - 1) / kWavesPerBlock)), blk(kBlock);
-  for (int b = 0; b < B; ++b) {
-    SegView sv{v.perm, v.seg, B, b};
-#define GTA_LEANSEG(VW_, GL_)                                                                        \
-  k_agg_seg<VW_, GL_><<<grid, blk, 0, s>>>(indptr, indices, n_rows, x, ldx, w, ldw, row_scale, y, ldy, \
-                                           accumulate, sv)
-    if (vw == 2) {
-      if (gl == 0) GTA_LEANSEG(2, 0); else if (gl == 4) GTA_LEANSEG(2, 4); else if (gl == 8) GTA_LEANSEG(2, 8); else GTA_LEANSEG(2, 16);
-    } else if (vw == 4) {
-      if (gl == 0) GTA_LEANSEG(4, 0); else if (gl == 4) GTA_LEANSEG(4, 4); else if (gl == 8) GTA_LEANSEG(4, 8); else GTA_LEANSEG(4, 16);
-    } else {
-      if (gl == 0) GTA_LEANSEG(1, 0); else if (gl == 4) GTA_LEANSEG(1, 4); else if (gl == 8) GTA_LEANSEG(1, 8); else GTA_LEANSEG(1, 16);
-    }
-#undef GTA_LEANSEG
-    GTA_LAUNCHED("k_agg_seg");
-  }
+  if (phase == 1) return GTA_OK;  // the item launch only; a later phase-2 call reduces
+  const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+  if (vw == 2) k_seg_reduce<2><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, ri);
+  else if (vw == 4) k_seg_reduce<4><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, ri);
+  else k_seg_reduce<1><<<g3, blk2, 0, s>>>(n_rows, slabs, row_scale, y, ldy, accumulate, ri);
+  GTA_LAUNCHED("k_seg_reduce");
   return GTA_OK;
 }
 
@@ -3297,7 +2970,7 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
   else k_agg_seg4<VW_, U_, false, 0, true><<<g4, blk, 0, s>>>(indices, nit, x, ldx, nullptr, 0, lph, slabs, \
                                                              it, att)
   const int lph32 = static_cast<int>((F / heads) / 4);
-  const bool lean = tuning().att_lean && elr && F == 128 && heads == 8 && tuning().seg_lanes == 32 && n_cols < (1 << 24) &&
+  const bool lean = tuning().att_lean && elr && F == 128 && heads == 8 && n_cols < (1 << 24) &&
                     static_cast<uint64_t>(n_cols) * static_cast<uint64_t>(ldx) * 4u < (1ull << 32) &&
                     static_cast<uint64_t>(n_cols) * static_cast<uint64_t>(ldb) * 4u < (1ull << 32);
   if (lean) {
@@ -3308,19 +2981,15 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
     const bool direct = (tuning().att_direct == 2 || (tuning().att_direct == 1 && B <= 2)) && ldy % 4 == 0 && aligned(y, 16);
     skip_single = direct;
     const int64_t* rp = direct ? v.row_ptr : nullptr;
-    if (tuning().att_lean == 2)
-      k_att_h32<2><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it, rp, normalize, y,
-                                       ldy, sums);
-    else
-      k_att_h32<0><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it, rp, normalize, y,
-                                       ldy, sums);
-  } else if (F == 128 && tuning().seg_lanes == 32 && (F / heads) % 4 == 0 && lph32 >= 1 && 32 % lph32 == 0) {
+    k_att_h32<2><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it, rp, normalize, y,
+                                     ldy, sums);  // NT bit 2: non-temporal slab stores
+  } else if (F == 128 && (F / heads) % 4 == 0 && lph32 >= 1 && 32 % lph32 == 0) {
     const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
     if (elr) k_agg_seg4<4, 8, false, 0, true, GTA_SF_EXP_LEAKY_RELU, 32><<<g2h, blk, 0, s>>>(
         indices, nit, x, ldx, nullptr, 0, lph32, slabs, it, att);
     else k_agg_seg4<4, 8, false, 0, true, -1, 32><<<g2h, blk, 0, s>>>(indices, nit, x, ldx, nullptr, 0,
                                                                       lph32, slabs, it, att);
-  } else if (vq == 4) { GTA_ATT(4, 4); } else if (vq == 8) { GTA_ATT(8, 8); } else { GTA_ATT(16, 2); }
+  } else if (vq == 4) { GTA_ATT(4, 4); } else { GTA_ATT(16, 2); }
 #undef GTA_ATT
   GTA_LAUNCHED("k_agg_seg4<att>");
   }
@@ -3471,10 +3140,8 @@ int gta_edge_softmax(const int64_t* indptr, const int32_t* indices, int64_t n_ro
 #define GTA_ESMV(H_, K_)                                                                                          \
   k_edge_softmax_v<H_, K_><<<grid, dim3(kBlock), 0, S(stream)>>>(indptr, indices, n_rows, a_dst, lda, b_src, ldb, \
                                                                  sf, normalize, out, sums)
-    const bool k4 = tuning().esm_keep >= 4 && heads <= 8;
-    if (heads == 4) { if (k4) GTA_ESMV(4, 4); else GTA_ESMV(4, 2); }
-    else if (heads == 8) { if (k4) GTA_ESMV(8, 4); else GTA_ESMV(8, 2); }
-    else GTA_ESMV(16, 2);
+    // chunks of 64 edges held in VGPRs: 4 for H <= 8, 2 at H = 16 (register budget)
+    if (heads == 4) GTA_ESMV(4, 4); else if (heads == 8) GTA_ESMV(8, 4); else GTA_ESMV(16, 2);
 #undef GTA_ESMV
     GTA_LAUNCHED("k_edge_softmax_v");
     return GTA_OK;
@@ -3521,135 +3188,50 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
   return GTA_OK;
 }
 
-// Plain fp32 UPDATE (no row gather, no SF epilogue, M >= tuning().mm_blaslt_min_m; the row-streaming and
-// split-K entry points) on hipBLASLt, the
-// vendor's tuned fp32 MFMA GEMM: measured faster than k_mm_rows on the layer shapes (Reddit
-// x.W 602 -> 128: 0.37 vs 0.58 ms; Flickr 500 -> 128: 0.12 vs 0.145 ms;
-// profiles/r01_mm_vs_library.json) -- k_mm_rows keeps the gather-GEMM, the SF epilogues, bf16 and
-// the split-K form.  Column-major view of the row-major product: out^T [N, M] = (W^T)^T-op . x^T,
-// with wt (= W^T, [N][K] row-major) read as a K x N column-major matrix, transposed by the op.
-// Descriptors and the heuristic's algorithm are cached per shape; false = the library declined
-// (the caller then runs k_mm_rows).
 namespace {
-struct BlasLtShape {
-  hipblasLtMatmulDesc_t md = nullptr;
-  hipblasLtMatrixLayout_t la = nullptr, lb = nullptr, lc = nullptr;
-  hipblasLtMatmulAlgo_t algo{};
-  bool ok = false;
-};
-constexpr uint64_t kBlasLtWorkspace = 32ull << 20;
-constexpr int kBlasLtCandidates = 8;
+// k_mm_ring launch: NT (4: N <= 64, 8: wider), ring depth D (3 / 4 / 8: blocks per CU the grid
+// needs), FR (A fragments per wave); kslice > 0: the split-K form (grid.y = K slices)
+void launch_ring(int nt, int D, int fr, dim3 gr, hipStream_t s, const float* x, int64_t ldx, const int32_t* row_idx,
+                 int64_t M, int K, const float* wt, int64_t ldwt, int N, int sf, float* out, int64_t ldo, int kslice,
+                 int64_t slice_stride) {
+#define GTA_RING(NT_, D_, FR_)                                                                              \
+  k_mm_ring<NT_, D_, FR_><<<gr, dim3(kBlock), 0, s>>>(x, ldx, row_idx, M, K, wt, ldwt, N, sf, out, ldo, kslice, \
+                                                      slice_stride)
+#define GTA_RING_D(NT_, FR_) \
+  if (D == 8) GTA_RING(NT_, 8, FR_); else if (D == 4) GTA_RING(NT_, 4, FR_); else GTA_RING(NT_, 3, FR_)
+  if (nt == 8) { if (fr == 1) { GTA_RING_D(8, 1); } else { GTA_RING_D(8, 2); } }
+  else { if (fr == 1) { GTA_RING_D(4, 1); } else { GTA_RING_D(4, 2); } }
+#undef GTA_RING_D
+#undef GTA_RING
+}
 
-bool blaslt_f32(const float* x, int64_t ldx, int64_t M, int64_t K, const float* wt, int64_t ldwt, int64_t N,
-                float* out, int64_t ldo, hipStream_t s) {
-  static std::mutex mu;
-  static std::map<int, std::pair<hipblasLtHandle_t, void*>> handles;  // per device: handle, workspace
-  static std::map<std::tuple<int, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int>, BlasLtShape> shapes;
-  std::lock_guard<std::mutex> lock(mu);
-  // the device the stream belongs to (not the calling thread's current device)
-  int dev = 0;
-  if (hipStreamGetDevice(s, &dev) != hipSuccess && hipGetDevice(&dev) != hipSuccess) return false;
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  if (hipStreamIsCapturing(s, &cap) != hipSuccess) return false;
-  const bool capturing = cap != hipStreamCaptureStatusNone;
-  auto h = handles.find(dev);
-  if (h == handles.end()) {
-    // a device's first use allocates (handle, workspace): never inside a graph capture -- the
-    // caller then runs the hand-written kernel instead (gta.h)
-    if (capturing) return false;
-    int cur = 0;
-    if (hipGetDevice(&cur) != hipSuccess || (cur != dev && hipSetDevice(dev) != hipSuccess)) return false;
-    hipblasLtHandle_t hd = nullptr;
-    void* ws = nullptr;
-    bool made = hipblasLtCreate(&hd) == HIPBLAS_STATUS_SUCCESS;
-    if (made && hipMalloc(&ws, kBlasLtWorkspace) != hipSuccess) {
-      hipblasLtDestroy(hd);
-      made = false;
-    }
-    if (cur != dev) (void)hipSetDevice(cur);
-    if (!made) return false;
-    h = handles.emplace(dev, std::make_pair(hd, ws)).first;
-  }
-  const int tune = tuning().mm_blaslt_tune;
-  const auto key = std::make_tuple(dev, M, K, N, ldx, ldwt, ldo, tune);
-  if (tune && capturing && shapes.find(key) == shapes.end()) return false;  // timing needs a live stream
-  auto it = shapes.find(key);
-  if (it == shapes.end()) {
-    BlasLtShape sh;
-    const hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
-    bool ok = hipblasLtMatmulDescCreate(&sh.md, HIPBLAS_COMPUTE_32F, HIP_R_32F) == HIPBLAS_STATUS_SUCCESS &&
-              hipblasLtMatmulDescSetAttribute(sh.md, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta)) ==
-                  HIPBLAS_STATUS_SUCCESS &&
-              hipblasLtMatmulDescSetAttribute(sh.md, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb)) ==
-                  HIPBLAS_STATUS_SUCCESS &&
-              hipblasLtMatrixLayoutCreate(&sh.la, HIP_R_32F, K, N, ldwt) == HIPBLAS_STATUS_SUCCESS &&
-              hipblasLtMatrixLayoutCreate(&sh.lb, HIP_R_32F, K, M, ldx) == HIPBLAS_STATUS_SUCCESS &&
-              hipblasLtMatrixLayoutCreate(&sh.lc, HIP_R_32F, N, M, ldo) == HIPBLAS_STATUS_SUCCESS;
-    if (ok) {
-      hipblasLtMatmulPreference_t pref = nullptr;
-      uint64_t wsb = kBlasLtWorkspace;
-      hipblasLtMatmulHeuristicResult_t res[kBlasLtCandidates];
-      int nres = 0;
-      ok = hipblasLtMatmulPreferenceCreate(&pref) == HIPBLAS_STATUS_SUCCESS &&
-           hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsb,
-                                                 sizeof(wsb)) == HIPBLAS_STATUS_SUCCESS &&
-           hipblasLtMatmulAlgoGetHeuristic(h->second.first, sh.md, sh.la, sh.lb, sh.lc, sh.lc, pref,
-                                           tune ? kBlasLtCandidates : 1, res, &nres) ==
-               HIPBLAS_STATUS_SUCCESS &&
-           nres > 0 && res[0].state == HIPBLAS_STATUS_SUCCESS;
-      if (pref) hipblasLtMatmulPreferenceDestroy(pref);
-      if (ok) {
-        sh.algo = res[0].algo;
-        // first use of the shape: time the heuristic's candidates on the real operands and keep the
-        // fastest (not while a HIP graph is being captured: the heuristic's first choice then)
-        // (nor when out overlaps an operand: the trial runs write out)
-        const auto span = [](const float* p, int64_t rows, int64_t ld, int64_t cols) {
-          return std::make_pair(reinterpret_cast<uintptr_t>(p), reinterpret_cast<uintptr_t>(p + (rows - 1) * ld + cols));
-        };
-        const auto overlap = [](std::pair<uintptr_t, uintptr_t> a, std::pair<uintptr_t, uintptr_t> b) {
-          return a.first < b.second && b.first < a.second;
-        };
-        const auto so = span(out, M, ldo, N);
-        const bool disjoint = !overlap(so, span(x, M, ldx, K)) && !overlap(so, span(wt, N, ldwt, K));
-        if (nres > 1 && disjoint && !capturing) {
-          hipEvent_t e0, e1;
-          if (hipEventCreate(&e0) == hipSuccess && hipEventCreate(&e1) == hipSuccess) {
-            const float alpha = 1.f, beta = 0.f;
-            float best = 1e30f;
-            for (int i = 0; i < nres; ++i) {
-              if (res[i].state != HIPBLAS_STATUS_SUCCESS) continue;
-              bool run_ok = true;
-              for (int rep = 0; rep < 3 && run_ok; ++rep) {  // rep 0 warms up
-                if (rep == 1) (void)hipEventRecord(e0, s);
-                run_ok = hipblasLtMatmul(h->second.first, sh.md, &alpha, wt, sh.la, x, sh.lb, &beta, out, sh.lc,
-                                         out, sh.lc, &res[i].algo, h->second.second, kBlasLtWorkspace, s) ==
-                         HIPBLAS_STATUS_SUCCESS;
-              }
-              if (!run_ok) continue;
-              (void)hipEventRecord(e1, s);
-              float ms = 0.f;
-              if (hipEventSynchronize(e1) == hipSuccess && hipEventElapsedTime(&ms, e0, e1) == hipSuccess &&
-                  ms < best) {
-                best = ms;
-                sh.algo = res[i].algo;
-              }
-            }
-            (void)hipEventDestroy(e0);
-            (void)hipEventDestroy(e1);
-          }
-        }
-      }
-    }
-    sh.ok = ok;
-    it = shapes.emplace(key, sh).first;
-  }
-  if (!it->second.ok) return false;
-  const float alpha = 1.f, beta = 0.f;
-  const BlasLtShape& sh = it->second;
-  return hipblasLtMatmul(h->second.first, sh.md, &alpha, wt, sh.la, x, sh.lb, &beta, out, sh.lc, out, sh.lc,
-                         &sh.algo, h->second.second, kBlasLtWorkspace, s) == HIPBLAS_STATUS_SUCCESS;
+inline int mm_nt(int64_t N) { return N <= 16 ? 1 : N <= 32 ? 2 : N <= 64 ? 4 : 8; }
+
+// fp32 products the ring takes: 4-B aligned x rows (16-B DMA pieces at 4-B aligned addresses are
+// fine), W^T rows 16-B aligned (ops._transposed pads them)
+inline bool ring_ok(int dtype, int nt, const void* x, const void* wt, int64_t ldwt) {
+  return tuning().mm_ring && dtype == GTA_F32 && nt >= 4 && aligned(x, 4) && aligned(wt, 16) && ldwt % 4 == 0;
+}
+
+// K slice of the split form: a multiple of 16 (whole ring stages; k_mm_rows masks a bf16 step's
+// half past the slice end), the same for every kernel form so the forms stay bitwise equal
+inline int64_t mm_kslice(int64_t K, int64_t splits) {
+  const int64_t per = (K + splits - 1) / splits;
+  return std::max<int64_t>(16, (per + 15) / 16 * 16);
 }
 }  // namespace
+
+int64_t gta_update_mm_t_splits(int64_t M, int64_t K, int64_t N, int dtype) {
+  if (M < 0 || K <= 0 || N <= 0) return fail(GTA_ERR_ARG, "update_mm_t_splits: bad sizes");
+  if (tuning().mm_split >= 0) return std::max<int64_t>(1, tuning().mm_split);
+  const int nt = mm_nt(N);
+  const int64_t units = (M + 127) / 128 * ((N + 16 * nt - 1) / (16 * nt));  // 128-row groups x column blocks
+  if (K < 256 || units >= 128) return 1;
+  // the ring (fp32): one (group, slice) block per CU, every block resident at once; k_mm_rows
+  // (bf16 / mixed, several blocks per CU): about two per CU; slices of >= 64 k
+  const int64_t want = (dtype == GTA_F32 ? 256 : 512) / std::max<int64_t>(1, units);
+  return std::max<int64_t>(1, std::min<int64_t>({want, K / 64, dtype == GTA_F32 ? 32 : 16}));
+}
 
 int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                     int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream) {
@@ -3659,73 +3241,42 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   if (!x || !wt || !out) return fail(GTA_ERR_ARG, "update_mm_t: bad arguments");
   if (K > INT32_MAX || N > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t: K/N too large");
   if (dtype != GTA_F32 && dtype != GTA_BF16 && dtype != GTA_F32_BF16) return fail(GTA_ERR_ARG, "update_mm_t: bad dtype");
-  if (M == 0) return GTA_OK;
-  if (tuning().mm_blaslt && dtype == GTA_F32 && !row_idx && sf == GTA_SF_NONE && M >= tuning().mm_blaslt_min_m &&
-      M <= tuning().mm_blaslt_max_m &&
-      blaslt_f32(static_cast<const float*>(x), ldx, M, K, static_cast<const float*>(wt), ldwt, N, out, ldo, S(stream))) {
-    GTA_LAUNCHED("hipblaslt_matmul");
-    return GTA_OK;
-  }
-  const int nt = N <= 16 ? 1 : N <= 32 ? 2 : N <= 64 ? 4 : 8;
+  const int nt = mm_nt(N);
   const int64_t groups = (M + 127) / 128;
-  if (tuning().mm_ring && dtype == GTA_F32 && nt >= 4 && K >= 32 && aligned(x, 4) && aligned(wt, 16) &&
-      ldwt % 4 == 0) {
-    // persistent: at most 3 blocks per CU (48 KiB of LDS each at N = 128), every slot of every CU
-    // filled, so each CU gets the same number of row groups (+-1).  (Shrinking the grid to
-    // ceil(groups / rounds) blocks, every block the same count, left some CUs with one block more
-    // than others: at M = 232,965 95 CUs ran 9 groups while 161 ran 6, 84 TF/s against 98 with
-    // 2 blocks per CU, profiles/r02_mm_ring_probe.json.)
-    const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
-    const int form = tuning().mm_ring_form;  // 0: 16-k stages x 3; 1: 32-k stages x 2; 2: 32-k stages x 3
-    // fr1: 64-row groups (one A fragment per wave, 36 KiB of LDS: 4 blocks per CU), form 0 only
+  const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
+  if (K >= 32 && ring_ok(dtype, nt, x, wt, ldwt)) {
+    // 64-row groups (one A fragment per wave, twice the work units for the per-CU balance) when
+    // 128-row groups load the CUs unevenly on a short K, where per-group start-up and epilogue weigh
+    // most, or when there are too few 128-row groups for two blocks per CU (K = 128 / 256 at 232,965
+    // rows 77 -> 86 / 92 -> 96 TF/s, 16,384 rows 40 -> 69; profiles/r02_mm_ring_probe_fr.json)
     const int frk = tuning().mm_ring_fr;
-    // auto: 64-row groups when 128-row groups leave CUs unevenly loaded (groups / 256 well short
-    // of a whole number) on a short K, where per-group start-up and epilogue weigh most, or when
-    // there are too few 128-row groups for 2 blocks per CU
     const double per_cu2 = static_cast<double>(groups * ncb) / 256.0;
     const bool uneven = per_cu2 / std::ceil(per_cu2) < 0.95;
-    const bool fr1 = form == 0 && (frk == 1 || (frk == 0 && ((K <= 256 && uneven) || groups < 512)));
-    const int64_t n_grp = fr1 ? (M + 63) / 64 : groups;
-    const int64_t lds_blocks = fr1 ? 4 : form == 1 ? 2 : form == 2 ? 1 : form == 3 ? 4 : 3;  // LDS per CU
-    const int64_t per_cu = tuning().mm_ring_blocks_per_cu > 0 ? tuning().mm_ring_blocks_per_cu : lds_blocks;
-    const int64_t slots = std::max<int64_t>(1, 256 * per_cu / ncb);
-    const bool a16 = (aligned(x, 16) && ldx % 4 == 0) || tuning().mm_ring_a16u;  // 16-B A pieces
-    const float* xf = static_cast<const float*>(x);
-    const float* wf = static_cast<const float*>(wt);
-    auto run = [&](const float* xp, const int32_t* rp, int64_t MM, float* op, bool f1, int64_t blocks) {
-      const dim3 gr(static_cast<unsigned>(blocks));
-#define GTA_RING(NT_, A4_, KH_, D_, FR_)                                                                          \
-  k_mm_ring<NT_, A4_, KH_, D_, FR_><<<gr, dim3(kBlock), 0, S(stream)>>>(xp, ldx, rp, MM, static_cast<int>(K), wf, ldwt, \
-                                                                        static_cast<int>(N), sf, op, ldo,            \
-                                                                        tuning().mm_vstore, tuning().mm_ring_prio)
-#define GTA_RING_F(NT_, A4_) \
-  if (f1) GTA_RING(NT_, A4_, 1, 3, 1); else if (form == 1) GTA_RING(NT_, A4_, 2, 2, 2); \
-  else if (form == 2) GTA_RING(NT_, A4_, 2, 3, 2); else if (form == 3) GTA_RING(NT_, A4_, 1, 2, 2); \
-  else GTA_RING(NT_, A4_, 1, 3, 2)
-      if (nt == 8) { if (a16) { GTA_RING_F(8, false); } else { GTA_RING_F(8, true); } }
-      else { if (a16) { GTA_RING_F(4, false); } else { GTA_RING_F(4, true); } }
-#undef GTA_RING_F
-#undef GTA_RING
-    };
-    // uneven 128-row groups on a long K: whole rounds of 128-row groups (every block the same
-    // count), then the remainder rows as 64-row groups in a second launch at 4 blocks per CU, so no
-    // CU runs a whole extra 128-row group (same k order: bitwise equal to one launch)
-    const int64_t M1 = (groups / slots) * slots * 128;
-    if (!fr1 && form == 0 && frk == 0 && tuning().mm_ring_tail && uneven && tuning().mm_ring_blocks_per_cu == 0 &&
-        M1 > 0 && M1 < M) {
-      run(xf, row_idx, M1, out, false, slots * ncb);
-      const int64_t M2 = M - M1, slots1 = std::max<int64_t>(1, 256 * 4 / ncb);
-      run(row_idx ? xf : xf + M1 * ldx, row_idx ? row_idx + M1 : nullptr, M2, out + M1 * ldo, true,
-          std::min((M2 + 63) / 64, slots1) * ncb);
+    const int fr = (frk == 1 || (frk == 0 && ((K <= 256 && uneven) || groups < 512))) ? 1 : 2;
+    const int64_t n_grp = fr == 1 ? (M + 63) / 64 : groups;
+    const int64_t units = n_grp * ncb;
+    // ring depth by the blocks each CU runs: up to one -> 8 stages (7 in flight), two -> 4, more ->
+    // the persistent 3-deep form with every CU slot filled (each CU the same number of row groups
+    // +-1; profiles/r02_mm_ring_probe.json)
+    int D = 3;
+    int64_t blocks;
+    if (units <= 256) {
+      D = 8;
+      blocks = units;
+    } else if (units <= 512) {
+      D = 4;
+      blocks = units;
     } else {
-      run(xf, row_idx, M, out, fr1, std::min(n_grp, slots) * ncb);
+      const int64_t per_cu = nt == 8 ? (fr == 1 ? 4 : 3) : 4;  // ring_blocks(NT, 3, FR)
+      blocks = std::min(n_grp, std::max<int64_t>(1, 256 * per_cu / ncb)) * ncb;
     }
+    launch_ring(nt, D, fr, dim3(static_cast<unsigned>(blocks)), S(stream), static_cast<const float*>(x), ldx, row_idx, M,
+                static_cast<int>(K), static_cast<const float*>(wt), ldwt, static_cast<int>(N), sf, out, ldo, 0, 0);
     GTA_LAUNCHED("k_mm_ring");
     return GTA_OK;
   }
-  const int64_t per_cu = tuning().mm_blocks_per_cu > 0 ? tuning().mm_blocks_per_cu : 8;
+  const int64_t per_cu = 8;
   const int kc = (dtype == GTA_F32) ? (nt >= 8 ? 64 : 128) : (nt >= 8 ? 128 : 256);  // k_mm_rows KC
-  const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
   const int64_t cap = (K <= kc) ? std::max<int64_t>(1, 256 * per_cu / ncb) : groups;  // W staged once: persistent
   const dim3 gr(static_cast<unsigned>(std::min<int64_t>(groups, cap) * ncb));
   // prefetch the next A fragment: measured 1.2x on fp32 (K = 602) and bf16 K = 128, and 1.1x on the
@@ -3735,11 +3286,10 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
 #define GTA_MMR(TA_, WT_, NT_)                                                                                \
   if (pf) k_mm_rows<TA_, WT_, NT_, true><<<gr, dim3(kBlock), 0, S(stream)>>>(                        \
       static_cast<const TA_*>(x), ldx, row_idx, M, static_cast<int>(K), static_cast<const WT_*>(wt), ldwt,        \
-      static_cast<int>(N), sf, out, ldo, 0, 0, tuning().mm_vstore);                                                      \
+      static_cast<int>(N), sf, out, ldo, 0, 0, 1);                                                      \
   else k_mm_rows<TA_, WT_, NT_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const TA_*>(x), ldx, row_idx, M, \
                                                                     static_cast<int>(K), static_cast<const WT_*>(wt), \
-                                                                    ldwt, static_cast<int>(N), sf, out, ldo, 0, 0,  \
-                                                                    tuning().mm_vstore)
+                                                                    ldwt, static_cast<int>(N), sf, out, ldo, 0, 0, 1)
 #define GTA_MMR_NT(TA_, WT_) \
   if (nt == 1) GTA_MMR(TA_, WT_, 1); else if (nt == 2) GTA_MMR(TA_, WT_, 2); else if (nt == 4) GTA_MMR(TA_, WT_, 4); else GTA_MMR(TA_, WT_, 8)
   if (dtype == GTA_F32) { GTA_MMR_NT(float, float); }
@@ -3751,15 +3301,9 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   return GTA_OK;
 }
 
-// K slice of the split form: a multiple of 32 (whole fp32 and bf16 A fragments)
-static int64_t mm_kslice(int64_t K, int64_t splits) {
-  return std::max<int64_t>(32, ((K + splits - 1) / splits + 31) / 32 * 32);
-}
-
 int64_t gta_update_mm_t_split_workspace_bytes(int64_t M, int64_t K, int64_t N, int64_t splits) {
   if (M < 0 || K <= 0 || N <= 0 || splits < 1) return fail(GTA_ERR_ARG, "update_mm_t_split_workspace_bytes: bad sizes");
-  const int64_t nsl = (K + mm_kslice(K, splits) - 1) / mm_kslice(K, splits);
-  return nsl * M * N * static_cast<int64_t>(sizeof(float));
+  return splits * M * N * static_cast<int64_t>(sizeof(float));  // every slice rounding gives <= splits slices
 }
 
 int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
@@ -3771,35 +3315,23 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
   if (!x || !wt || !out || !workspace) return fail(GTA_ERR_ARG, "update_mm_t_split: bad arguments");
   if (K > INT32_MAX || N > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t_split: K/N too large");
   if (dtype != GTA_F32 && dtype != GTA_BF16 && dtype != GTA_F32_BF16) return fail(GTA_ERR_ARG, "update_mm_t_split: bad dtype");
-  const int64_t ks = mm_kslice(K, splits), nsl = (K + ks - 1) / ks;
-  if (workspace_bytes < nsl * M * N * static_cast<int64_t>(sizeof(float)))
+  if (workspace_bytes < splits * M * N * static_cast<int64_t>(sizeof(float)))
     return fail(GTA_ERR_ARG, "update_mm_t_split: workspace too small");
-  if (nsl > 65535) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t_split: too many slices");
   float* ws = static_cast<float*>(workspace);
-  const int nt = N <= 16 ? 1 : N <= 32 ? 2 : N <= 64 ? 4 : 8;
+  const int nt = mm_nt(N);
   const int64_t groups = (M + 127) / 128;
   const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
   hipStream_t s = S(stream);
-  if (tuning().mm_blaslt && dtype == GTA_F32 && !row_idx && sf == GTA_SF_NONE && M >= tuning().mm_blaslt_min_m &&
-      M <= tuning().mm_blaslt_max_m &&
-      blaslt_f32(static_cast<const float*>(x), ldx, M, K, static_cast<const float*>(wt), ldwt, N, out, ldo, S(stream))) {
-    GTA_LAUNCHED("hipblaslt_matmul");
-    return GTA_OK;
-  }
-  if (tuning().mm_ring && dtype == GTA_F32 && nt >= 4 && aligned(x, 4) && aligned(wt, 16) && ldwt % 4 == 0 &&
-      ks % 4 == 0 && N % 4 == 0 && aligned(ws, 16)) {
-    // the LDS-DMA ring per K slice (one 128-row group per block: grid = groups x slices), then the
-    // ordered slice sum; for what the library does not take (gathered rows, SF, M < 1024). GCN Cora's
-    // [2708 x 1433].[1433 x 128]: hipBLASLt 24-29 us, ring slices + sum 41 (33.7 + 7.0), k_mm_rows slices 46
-    const dim3 gr(static_cast<unsigned>(groups * ncb), static_cast<unsigned>(nsl));
-    const bool a16 = (aligned(x, 16) && ldx % 4 == 0) || tuning().mm_ring_a16u;
-#define GTA_RINGS(NT_, A4_)                                                                                    \
-  k_mm_ring<NT_, A4_><<<gr, dim3(kBlock), 0, s>>>(static_cast<const float*>(x), ldx, row_idx, M, static_cast<int>(K), \
-                                                  static_cast<const float*>(wt), ldwt, static_cast<int>(N), GTA_SF_NONE, \
-                                                  ws, N, 1, tuning().mm_ring_prio, static_cast<int>(ks), M * N)
-    if (nt == 8) { if (a16) { GTA_RINGS(8, false); } else { GTA_RINGS(8, true); } }
-    else { if (a16) { GTA_RINGS(4, false); } else { GTA_RINGS(4, true); } }
-#undef GTA_RINGS
+  const bool ring = ring_ok(dtype, nt, x, wt, ldwt) && N % 4 == 0 && aligned(ws, 16);
+  const int64_t ks = mm_kslice(K, splits), nsl = (K + ks - 1) / ks;
+  if (nsl > 65535) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t_split: too many slices");
+  if (ring) {
+    // every (128-row group, K slice) on its own block, one per CU with an 8-deep ring (all stages of a
+    // slice in flight from the start), then the ordered slice sum.  GCN Cora's [2708 x 1433].[1433 x 128]:
+    // 22 groups x 10 slices of 144 k
+    launch_ring(nt, 8, 2, dim3(static_cast<unsigned>(groups * ncb), static_cast<unsigned>(nsl)), s,
+                static_cast<const float*>(x), ldx, row_idx, M, static_cast<int>(K), static_cast<const float*>(wt), ldwt,
+                static_cast<int>(N), GTA_SF_NONE, ws, N, static_cast<int>(ks), M * N);
     GTA_LAUNCHED("k_mm_ring<split>");
   } else {
   const dim3 gr(static_cast<unsigned>(groups * ncb), static_cast<unsigned>(nsl));
@@ -3807,9 +3339,9 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
   const int ki = static_cast<int>(K);
 #define GTA_MMS(TA_, WT_, NT_)                                                                                    \
   if (pf) k_mm_rows<TA_, WT_, NT_, true><<<gr, dim3(kBlock), 0, s>>>(static_cast<const TA_*>(x), ldx, row_idx, M, ki, \
-      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N, tuning().mm_vstore);                                 \
+      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N, 1);                                 \
   else k_mm_rows<TA_, WT_, NT_><<<gr, dim3(kBlock), 0, s>>>(static_cast<const TA_*>(x), ldx, row_idx, M, ki,          \
-      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N, tuning().mm_vstore)
+      static_cast<const WT_*>(wt), ldwt, static_cast<int>(N), sf, ws, N, ks, M * N, 1)
 #define GTA_MMS_NT(TA_, WT_) \
   if (nt == 1) GTA_MMS(TA_, WT_, 1); else if (nt == 2) GTA_MMS(TA_, WT_, 2); else if (nt == 4) GTA_MMS(TA_, WT_, 4); else GTA_MMS(TA_, WT_, 8)
   if (dtype == GTA_F32) { GTA_MMS_NT(float, float); }
@@ -3820,8 +3352,15 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
   GTA_LAUNCHED("k_mm_rows<split>");
   }
   const int64_t total = M * N;
-  k_mm_slices_sum<<<dim3(static_cast<unsigned>(std::min<int64_t>((total + kBlock - 1) / kBlock, 4096))), dim3(kBlock), 0,
-                    s>>>(ws, static_cast<int>(nsl), M, static_cast<int>(N), sf, out, ldo);
+  if (N % 4 == 0 && ldo % 4 == 0 && aligned(out, 16) && aligned(ws, 16)) {
+    const int64_t t4 = total / 4;
+    k_mm_slices_sum4<<<dim3(static_cast<unsigned>(std::min<int64_t>((t4 + kBlock - 1) / kBlock, 4096))), dim3(kBlock), 0,
+                       s>>>(reinterpret_cast<const float4*>(ws), static_cast<int>(nsl), M, static_cast<int>(N / 4), sf,
+                            out, ldo);
+  } else {
+    k_mm_slices_sum<<<dim3(static_cast<unsigned>(std::min<int64_t>((total + kBlock - 1) / kBlock, 4096))), dim3(kBlock), 0,
+                      s>>>(ws, static_cast<int>(nsl), M, static_cast<int>(N), sf, out, ldo);
+  }
   GTA_LAUNCHED("k_mm_slices_sum");
   return GTA_OK;
 }

@@ -1003,7 +1003,10 @@ def aggregate_trace(events):
 # Flickr) are bound by.  The outputs of a replayed call are the graph's own tensors: the next
 # call with the same inputs overwrites them (clone what must survive it).  Only graphs of at most
 # AUTO_GRAPH_MAX_EDGES edges (launch-bound; larger layers are kernel-bound and a graph's private
-# memory pool would hold their intermediates); AUTO_GRAPH = False turns it off.
+# memory pool would hold their intermediates); AUTO_GRAPH = False turns it off (set_auto_graph(False)
+# also drops every captured graph).  A replay is keyed by the objects AND their storage (data_ptr,
+# shape, stride), the libgta knob state (ops.knob_epoch) and stays eager on a stream with an attached
+# knob set; weights changed in place are re-transposed into the graph's W^T before the replay.
 AUTO_GRAPH = True
 AUTO_GRAPH_MAX_EDGES = 1 << 23
 AUTO_GRAPH_MAX_ENTRIES = 32
@@ -1013,27 +1016,45 @@ _AUTO = {}
 class _AutoEntry:
     def __init__(self, refs, tensors):
         self.refs, self.tensors = refs, tensors  # strong references: ids and addresses stay unique
+        self.ptrs = {k: t.data_ptr() for k, t in tensors.items()}
         self.src = None                          # the caller's dict last seen with these tensors
         self.calls, self.run, self.failed = 0, None, False
 
 
-_AUTO_FAST = {}  # (ids of the call's objects, id of its tensors dict) -> entry: the per-call lookup
+_AUTO_FAST = {}  # (ids of the call's objects, id of its tensors dict, knob epoch) -> entry: the per-call lookup
+
+
+def clear_auto_graphs():
+    """Drop every captured graph (and the inputs, CSRs and memory pools they hold)."""
+    _AUTO.clear()
+    _AUTO_FAST.clear()
+
+
+def set_auto_graph(flag):
+    global AUTO_GRAPH
+    AUTO_GRAPH = bool(flag)
+    if not AUTO_GRAPH:
+        clear_auto_graphs()
 
 
 def _auto_graph(opgraph, stream, graph, tensors, semantics, plan_chunk):
     """-> a GraphedRun to replay for this call, or None (run eagerly)."""
+    if ops.Tuning.attached(torch.cuda.current_stream(graph.device)):
+        return None  # a knob set on this stream: every call reads it (gta.h), so no cached graph
     refs = (opgraph, stream, graph, semantics)
-    fkey = (id(opgraph), id(stream), id(graph), id(semantics), plan_chunk, id(tensors))
+    fkey = (id(opgraph), id(stream), id(graph), id(semantics), plan_chunk, id(tensors), ops.knob_epoch())
     ent = _AUTO_FAST.get(fkey)
     if ent is not None and not (ent.src is tensors and all(a is b for a, b in zip(ent.refs, refs)) and
                                 len(tensors) == len(ent.tensors) and
-                                all(tensors.get(k) is t for k, t in ent.tensors.items())):
+                                all(tensors.get(k) is t and t.data_ptr() == ent.ptrs[k]
+                                    for k, t in ent.tensors.items())):
         ent = None
     if ent is None:
         if not all(torch.is_tensor(t) and t.is_cuda for t in tensors.values()):
             return None
-        key = fkey[:5] + (tuple(sorted((k, id(t), t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype)
-                                      for k, t in tensors.items())),)
+        key = fkey[:5] + (ops.knob_epoch(),
+                          tuple(sorted((k, id(t), t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype)
+                                       for k, t in tensors.items())))
         ent = _AUTO.get(key)
         if ent is not None and not all(a is b for a, b in zip(ent.refs, refs)):
             ent = None
@@ -1061,6 +1082,8 @@ def _auto_graph(opgraph, stream, graph, tensors, semantics, plan_chunk):
 
 def run_stream(opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, sync=True, trace=False):
     dev = graph.device
+    if not AUTO_GRAPH and _AUTO:
+        clear_auto_graphs()
     if AUTO_GRAPH and not trace and dev.type == "cuda" and graph.nnz <= AUTO_GRAPH_MAX_EDGES:
         gr = _auto_graph(opgraph, stream, graph, tensors, semantics, plan_chunk)
         if gr is not None:
@@ -1169,7 +1192,9 @@ class GraphedRun:
     launch instead of one Python-driven launch per op -- the launch-bound small graphs (Cora,
     Flickr) are where it matters.  Inputs are the tensors given here (static addresses: update
     them in place between replays); outputs are the same tensors after every replay.  The
-    warm-up run builds every plan, workspace and W^T cache outside the capture."""
+    warm-up run builds every plan, workspace and W^T cache outside the capture.  The graph keeps
+    the W^T tensors it reads alive, and a weight changed in place (its version moved) is
+    re-transposed into them before the next replay."""
 
     def __init__(self, opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, warmup=2):
         if graph.device.type != "cuda":
@@ -1183,11 +1208,22 @@ class GraphedRun:
         torch.cuda.current_stream(graph.device).wait_stream(side)
         torch.cuda.synchronize(graph.device)
         self.cuda_graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.cuda_graph):
-            self.executor = Executor(opgraph, stream, graph, tensors, semantics, plan_chunk)
-            self.outputs = self.executor.run()
+        del ops._CAPTURED_WT[:]
+        try:
+            with torch.cuda.graph(self.cuda_graph):
+                self.executor = Executor(opgraph, stream, graph, tensors, semantics, plan_chunk)
+                self.outputs = self.executor.run()
+        finally:
+            taken, ops._CAPTURED_WT[:] = list(ops._CAPTURED_WT), []
+        # (weight, its W^T read by the graph, the weight version that W^T holds)
+        self._wts = [[w, wt, w._version] for w, wt in {id(wt): (w, wt) for w, wt in taken}.values()]
 
     def replay(self):
+        for ent in self._wts:
+            w, wt, ver = ent
+            if w._version != ver:  # changed in place since the capture: refresh the graph's W^T
+                wt.copy_(w.t())
+                ent[2] = w._version
         self.cuda_graph.replay()
         return self.outputs
 

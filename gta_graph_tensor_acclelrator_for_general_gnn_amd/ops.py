@@ -439,7 +439,7 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
         out = torch.empty(M, N, dtype=torch.float32, device=x.device)
     ldo = _rows(out, "out")
     dt = _lib.GTA_F32_BF16 if mixed else (_lib.GTA_F32 if x.dtype == torch.float32 else _lib.GTA_BF16)
-    splits = _mm_splits(M, K, N) if MM_FORM == "rows" else 1
+    splits = _mm_splits(M, K, N, dt) if MM_FORM == "rows" else 1
     if splits > 1:  # few rows: split K over blocks, slices summed in order (deterministic)
         wt = _transposed(w)
         nb = check(_L().gta_update_mm_t_split_workspace_bytes(M, K, N, splits), "update_mm_t_split_workspace_bytes")
@@ -458,19 +458,20 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
 
 
 MM_FORM = "rows"  # "rows": gta_update_mm_t (x read once per output); "tile": gta_update_mm 64x64 tiles
-MM_SPLIT_MAX_BLOCKS = 128  # split K when the row-streaming grid has fewer blocks than this (of 256 CUs)
-MM_ROWS_MIN_M = 0  # smallest M for the row-streaming entry (k_mm_ring / k_mm_rows / library); below, the
+MM_ROWS_MIN_M = 0  # smallest M for the row-streaming entry (k_mm_ring / k_mm_rows); below, the
                    # 64x64-tile kernel. With the ring the row form wins at every M measured: GCN Cora's
                    # [2708 x 128].[128 x 64] took the forward 0.093 -> 0.081 ms (profiles/r02_layer_bench_mmrows.log)
 _WT_CACHE = {}
+# (w, W^T) pairs handed out while a HIP graph is being captured (executor.GraphedRun takes them: the
+# graph keeps those W^T tensors alive and refreshes them when a weight changes in place)
+_CAPTURED_WT = []
 
 
-def _mm_splits(M, K, N):
-    """K slices for gta_update_mm_t_split: enough blocks for ~2 per CU, slices of >= 64 k; 1 = no split."""
-    blocks = -(-M // 128) * -(-N // 128)
-    if K < 256 or blocks >= MM_SPLIT_MAX_BLOCKS:
-        return 1
-    return max(1, min(16, -(-512 // blocks), K // 64))
+def _mm_splits(M, K, N, dtype=_lib.GTA_F32):
+    """K slices for gta_update_mm_t_split, as libgta picks them (gta_update_mm_t_splits: about one
+    (row group, slice) block per CU for fp32, slices of >= 64 k, only for K >= 256 on few row
+    groups; knob mm_split overrides); 1 = no split."""
+    return int(check(_L().gta_update_mm_t_splits(M, K, N, dtype), "update_mm_t_splits"))
 
 
 def _transposed(w):
@@ -479,6 +480,8 @@ def _transposed(w):
     by another tensor, so the address alone is never the key."""
     ent = _WT_CACHE.get(id(w))
     if ent is not None and ent[0]() is w and ent[1] == w._version:
+        if torch.cuda.is_current_stream_capturing():
+            _CAPTURED_WT.append((w, ent[2]))
         return ent[2]
     if len(_WT_CACHE) >= 64:
         _WT_CACHE.clear()
@@ -488,6 +491,8 @@ def _transposed(w):
     wt = w.new_zeros(N, ld)[:, :K]
     wt.copy_(w.t())
     _WT_CACHE[id(w)] = (weakref.ref(w), w._version, wt)
+    if torch.cuda.is_current_stream_capturing():
+        _CAPTURED_WT.append((w, wt))
     return wt
 
 
@@ -501,9 +506,18 @@ def tile_nnz(graph, T):
     return counts
 
 
+_KNOB_EPOCH = [0]  # bumped by every knob change: part of the executor's HIP-graph cache key
+_ATTACHED = set()  # raw stream handles with an attached knob set (the executor stays eager on them)
+
+
+def knob_epoch():
+    return _KNOB_EPOCH[0]
+
+
 def set_debug(key, value):
     """Set a tuning knob of libgta for the CALLING thread (include/gta.h: gta_debug_set)."""
     check(_L().gta_debug_set(key.encode(), int(value)), "debug_set")
+    _KNOB_EPOCH[0] += 1
 
 
 def get_debug(key):
@@ -518,7 +532,10 @@ class Tuning:
     """A libgta knob set scoped to a STREAM (include/gta.h gta_tuning_*): attach(stream) copies
     these values onto the stream, and every call made on it -- from any thread -- then reads them
     instead of the calling thread's knobs (set_debug).  Change a value, attach again to apply it;
-    detach(stream) drops the stream's set.  Unknown keys raise GTAError."""
+    detach(stream) drops the stream's set.  Unknown keys raise GTAError.
+    The set is keyed by the raw stream handle: detach before the stream is destroyed (a new stream
+    may reuse the handle), and attaching to the null stream (0) governs every default-stream call.
+    The executor's automatic HIP-graph replay stays eager on a stream with an attached set."""
 
     def __init__(self, **knobs):
         self._lib = _L()
@@ -545,10 +562,19 @@ class Tuning:
 
     def attach(self, stream):
         check(self._lib.gta_tuning_attach(self._ptr(stream), self._h), "tuning_attach")
+        _ATTACHED.add(self._ptr(stream))
+        _KNOB_EPOCH[0] += 1
 
     @classmethod
     def detach(cls, stream):
         check(_L().gta_tuning_attach(cls._ptr(stream), None), "tuning_attach")
+        _ATTACHED.discard(cls._ptr(stream))
+        _KNOB_EPOCH[0] += 1
+
+    @staticmethod
+    def attached(stream):
+        """True if a knob set is attached to this stream (torch.cuda.Stream or raw handle)."""
+        return Tuning._ptr(stream) in _ATTACHED
 
     def __del__(self):
         h, self._h = getattr(self, "_h", None), None

@@ -37,9 +37,10 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 4  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
-                              hooks, blocked workspace holds per-row arrival counters; 4: knob sets
-                              attached to streams (gta_tuning_*) */
+#define GTA_ABI_VERSION 5  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+                              hooks; 4: knob sets attached to streams (gta_tuning_*); 5: every UPDATE
+                              on hand-written kernels (no vendor library), gta_update_mm_t_splits,
+                              the blocked workspace is the slab rows alone and required */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -73,8 +74,8 @@ enum { GTA_SF_NONE = 0, GTA_SF_RELU = 1, GTA_SF_EXP_LEAKY_RELU = 2 /* exp(leaky_
 int gta_abi_version(void);
 const char* gta_last_error(void);
 
-/* Tuning hooks (benchmarks and kernel-form tests): named knobs that pick a kernel variant
- * (DESIGN.md §3.1 lists them).  They are per calling THREAD -- a knob set on one thread never
+/* Tuning hooks (benchmarks and kernel-form tests): named knobs that pick between kernel forms
+ * the defaults reach on some shape, or split a launch for per-kernel timing.  They are per calling THREAD -- a knob set on one thread never
  * changes another thread's concurrent calls -- and every entry point reads its own thread's
  * values, so the library keeps no process-wide mutable state.  Unknown key: GTA_ERR_ARG. */
 int gta_debug_set(const char* key, int64_t value);
@@ -133,10 +134,10 @@ int gta_aggregate_plan_build(const int64_t* indptr, int64_t n_rows, int64_t nnz,
 int64_t gta_aggregate_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t chunk, int64_t F);
 
 /* ---- K6 column-blocked form (L2-resident source slices) -----------------
- * Same y as gta_aggregate (x_mode SRC, w NULL or heads), computed as B launches:
- * launch b adds, for every row, the edges whose source column lies in
- * [b*ceil(n_cols/B), (b+1)*ceil(n_cols/B)), so all waves of a launch gather from
- * one X slice that stays resident in each XCD's 4 MB L2 -- the reference's own
+ * Same y as gta_aggregate (x_mode SRC, w NULL or heads), computed over B source-column
+ * blocks [b*ceil(n_cols/B), (b+1)*ceil(n_cols/B)): the work items of one block run
+ * together, so the waves in flight gather from one X slice that stays resident in
+ * each XCD's 4 MB L2 -- the reference's own
  * T-row x column tiling (code/preprocessing.py:26-38, interpreter TC) with the
  * column axis outermost.  Needs each CSR row's columns sorted (the plan build
  * flags unsorted rows in plan header word 3) and F = 64*VW (64/128/256) with
@@ -156,10 +157,9 @@ int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t nnz, int64_t bl
 int gta_aggregate_blocked_plan_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
                                      int64_t nnz, int64_t blocks, int64_t item_edges, int64_t row_edges,
                                      void* plan, int64_t plan_bytes, void* stream);
-/* workspace: NULL = B dependent launches accumulating into y; otherwise >=
- * gta_aggregate_blocked_workspace_bytes: one launch over the plan's items in
- * block-major order, item k writing partial row k, then an ordered reduce
- * summing each row's items in (block, part) order. */
+/* workspace >= gta_aggregate_blocked_workspace_bytes (may be NULL only when nnz == 0):
+ * one launch over the plan's items in block-major order, item k writing partial row
+ * k, then an ordered reduce summing each row's items in (block, part) order. */
 int64_t gta_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t F,
                                               int64_t item_edges);
 int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols, int64_t nnz,
@@ -237,35 +237,30 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
                   float* out, int64_t ldo, void* stream);
 
 /* Same UPDATE with W given TRANSPOSED: wt [N, K] row-major (leading dimension
- * ldwt >= K), dtype as above.  Runs a row-streaming kernel: a block owns up to 128 of
- * the N columns and walks 128-row groups, so x is read once.  fp32 with N > 32 and
- * 16-B aligned wt rows (ldwt % 4 == 0) runs k_mm_ring: x and wt go global -> LDS by DMA
- * through a 3-stage ring (persistent blocks, the ring running on across row groups);
+ * ldwt >= K), dtype as above.  Row-streaming kernels: a block owns up to 128 of the N
+ * columns and walks row groups, so x is read once.  fp32 with N > 32, K >= 32 and 16-B
+ * aligned wt rows (ldwt % 4 == 0) runs k_mm_ring: x and wt go global -> LDS by DMA through
+ * a ring of 16-k stages, 3 deep for persistent blocks over many row groups, 4 at two blocks
+ * per CU, 8 when every CU runs at most one block (x rows need only 4-B alignment);
  * otherwise k_mm_rows (x fragments straight to registers, wt staged per K chunk).  Both
  * contract k in the same order: bitwise equal to each other, fp32 rounding away from
- * gta_update_mm.  x rows need only 4-B alignment (K = 602: 16-B DMA pieces at 8-B aligned
- * addresses).  From 65,536 rows every fp32 product runs k_mm_ring (>= 2 blocks per CU).  A plain
- * fp32 product (GTA_F32, row_idx NULL, GTA_SF_NONE) with 1024 <= M < 65,536 (tuning knobs
- * mm_blaslt_min_m / mm_blaslt_max_m) runs on hipBLASLt instead, where the ring cannot fill the
- * chip, with the library heuristic's FIRST choice for the shape: the same
- * algorithm in every process, so ranks agree bitwise (tuning knob mm_blaslt_tune = 1 times the
- * top candidates instead: faster, but the pick may then differ between processes).  The
- * library's per-device handle and workspace are created at the device's first plain fp32 call;
- * a call made while the stream is being captured into a graph never creates them (nor times
- * anything) and runs the hand-written kernel instead.  The device's first plain fp32 call of that
- * size range must not overlap a GLOBAL-mode capture running on another stream (hipMalloc of the
- * workspace would invalidate it): warm up outside captures, as executor.GraphedRun does.  Also applies to gta_update_mm_t_split. */
+ * gta_update_mm.  Every form is a hand-written kernel of this library (no vendor GEMM): the
+ * result depends only on the shape and the operands, identical in every process. */
 int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                     int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, void* stream);
 
 /* Split-K form of gta_update_mm_t for few rows (M small against the chip): the K axis is cut
- * into slices of ceil(K / splits) rounded up to 32; each slice's partial [M, N] goes to the
- * workspace (gta_update_mm_t_split_workspace_bytes) and a second kernel adds the slices in order
- * and applies sf.  Deterministic; the contraction order differs from gta_update_mm_t (fp32
- * rounding only).  A plain fp32 product goes to hipBLASLt as in gta_update_mm_t; otherwise fp32
- * with N > 32 (N % 4 == 0, 16-B aligned wt rows) runs every slice on k_mm_ring (one 128-row
- * group per block), else k_mm_rows per slice: the same slices bitwise.  Same reference as
- * gta_update_mm. */
+ * into slices of ceil(K / splits) rounded up to 16 (every kernel form alike); each slice's
+ * partial [M, N] goes to the workspace (>= gta_update_mm_t_split_workspace_bytes = splits x M x N
+ * floats) and a second kernel adds the slices in order and applies sf.  Deterministic; the
+ * contraction order differs from gta_update_mm_t (fp32 rounding only).  fp32 with N > 32
+ * (N % 4 == 0, 16-B aligned wt rows) runs every (128-row group, slice) as one k_mm_ring block
+ * with an 8-deep ring (one block per CU), else k_mm_rows per slice.
+ * gta_update_mm_t_splits gives the slice count the library would pick for a shape (1 = no split:
+ * call gta_update_mm_t): about one (group, slice) block per CU for fp32, two for bf16, slices of
+ * >= 64 k, only for K >= 256 and fewer than 128 (group, column-block) units; the tuning knob
+ * mm_split overrides it.  Same reference as gta_update_mm. */
+int64_t gta_update_mm_t_splits(int64_t M, int64_t K, int64_t N, int dtype);
 int64_t gta_update_mm_t_split_workspace_bytes(int64_t M, int64_t K, int64_t N, int64_t splits);
 int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                           int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, int64_t splits,

@@ -41,9 +41,12 @@ for s in $STEPS; do
     layers)
       timeout -k 10 ${T_LAYERS:-600} python scripts/layer_bench.py ${LAYER_ARGS} > gpurun_out/layers.log 2>&1
       rc=$?; echo "layers rc=$rc"; tail -6 gpurun_out/layers.log; stop_if_fatal $rc layers ;;
-    sweep)
-      timeout -k 10 ${T_SWEEP:-600} python scripts/agg_sweep.py ${SWEEP_ARGS} > gpurun_out/sweep.log 2>&1
-      rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.log | tail -12; stop_if_fatal $rc sweep ;;
+    mm)
+      timeout -k 10 ${T_MM:-300} python scripts/mm_probe.py ${MM_ARGS} > gpurun_out/mm_probe.log 2>&1
+      rc=$?; echo "mm rc=$rc"; tail -20 gpurun_out/mm_probe.log; stop_if_fatal $rc mm ;;
+    pmcsq)
+      timeout -k 10 ${T_PMCSQ:-420} python scripts/pmc_sq.py gpurun_out/pmc_sq > gpurun_out/pmc_sq.log 2>&1
+      rc=$?; echo "pmcsq rc=$rc"; tail -3 gpurun_out/pmc_sq.log; stop_if_fatal $rc pmcsq ;;
     *) echo "unknown step $s";;
   esac
 done

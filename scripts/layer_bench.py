@@ -74,9 +74,7 @@ def main(names=None, reps=5, trace=False, graphed=False):
 
 if __name__ == "__main__":
     from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
-    if "--blaslt-tune" in sys.argv[1:]:  # time hipBLASLt's candidates per process (not the deterministic default)
-        ops.set_debug("mm_blaslt_tune", 1)
-    argv = [a for a in sys.argv[1:] if a not in ("--trace", "--hipgraph", "--blaslt-tune")]
+    argv = [a for a in sys.argv[1:] if a not in ("--trace", "--hipgraph")]
     if "--mm-rows-min" in argv:  # ops.MM_ROWS_MIN_M: smallest M for the row-streaming UPDATE entry
         i = argv.index("--mm-rows-min")
         ops.MM_ROWS_MIN_M = int(argv[i + 1])

@@ -1,41 +1,94 @@
-"""Row-streaming GEMM (k_mm_rows) on the layer shapes with the dword-store and the 16-B-store epilogue."""
+"""UPDATE GEMM timing on the layer shapes (all hand-written: k_mm_ring / k_mm_rows + split-K).
+
+For each (M, K, N, dtype): median of HIP-graph replays of one update_mm call (the launch gaps a
+layer's graph sees), and the kernel-only time from HIP events over back-to-back eager calls.
+Prints one JSON line per shape: ms, TF/s, GB/s (x + W read once, out written once).
+Usage: python scripts/mm_probe.py [--shapes cora|mid|big|gin|all] [--knob k=v ...]
+"""
+import json
 import os
 import sys
 
-import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops  # noqa: E402
 
+SHAPES = {
+    "cora": [(2708, 1433, 128, "f32"), (2708, 128, 64, "f32")],
+    "mid": [(16384, 128, 128, "f32"), (29000, 602, 128, "f32"), (44625, 500, 128, "f32"), (29000, 602, 256, "f32"),
+            (16384, 1433, 128, "f32"), (5000, 602, 128, "f32")],
+    "big": [(232965, 602, 128, "f32"), (232965, 602, 256, "f32"), (89250, 500, 128, "f32"), (232965, 128, 128, "f32"),
+            (899756, 500, 128, "f32")],
+    "gin": [(2449029, 100, 128, "mixed"), (2449029, 128, 128, "mixed"), (2449029, 100, 128, "f32"),
+            (2449029, 128, 128, "bf16")],
+}
+
+
+def one(M, K, N, dt, dev, reps=20):
+    g = torch.Generator(device="cpu").manual_seed(M + K + N)
+    x = torch.randn(M, K, generator=g).to(dev)
+    w = (torch.randn(K, N, generator=g) / K ** 0.5).to(dev)
+    if dt == "bf16":
+        x, w = x.to(torch.bfloat16), w.to(torch.bfloat16)
+    elif dt == "mixed":
+        w = w.to(torch.bfloat16)
+    out = torch.empty(M, N, device=dev)
+    for _ in range(3):
+        ops.update_mm(x, w, out=out)
+    torch.cuda.synchronize()
+    s = torch.cuda.current_stream()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(s)
+        ops.update_mm(x, w, out=out)
+        b.record(s)
+    torch.cuda.synchronize()
+    k_ms = sorted(a.elapsed_time(b) for a, b in ev)[reps // 2]
+    # HIP-graph replay of the same call (W^T cached before the capture)
+    gr = torch.cuda.CUDAGraph()
+    side = torch.cuda.Stream()
+    side.wait_stream(s)
+    with torch.cuda.stream(side):
+        ops.update_mm(x, w, out=out)
+    s.wait_stream(side)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(gr):
+        ops.update_mm(x, w, out=out)
+    for _ in range(3):
+        gr.replay()
+    torch.cuda.synchronize()
+    ev2 = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev2:
+        a.record(s)
+        gr.replay()
+        b.record(s)
+    torch.cuda.synchronize()
+    g_ms = sorted(a.elapsed_time(b) for a, b in ev2)[reps // 2]
+    ref = (x.double() @ w.double()) if M <= 50000 else None
+    err = None if ref is None else float((out.double() - ref).abs().max())
+    flop = 2.0 * M * K * N
+    byt = x.numel() * x.element_size() + w.numel() * w.element_size() + out.numel() * 4
+    return {"M": M, "K": K, "N": N, "dtype": dt, "splits": ops._mm_splits(M, K, N, {"f32": 0, "bf16": 1, "mixed": 2}[dt]),
+            "kernel_ms": round(k_ms, 4), "graph_ms": round(g_ms, 4), "TFps": round(flop / k_ms / 1e9, 1),
+            "GBps": round(byt / k_ms / 1e6, 1), "max_abs_err_vs_fp64": err}
+
 
 def main():
-    dev = torch.device("cuda:0")
-    torch.manual_seed(0)
-    for M, K, N, dt in [(89250, 64, 128, None), (89250, 500, 128, None), (232965, 602, 128, None),
-                        (2449029, 100, 128, torch.bfloat16), (2449029, 128, 128, torch.bfloat16), (2708, 1433, 128, None)]:
-        x = torch.randn(M, K, device=dev)
-        w = torch.randn(K, N, device=dev) * K ** -0.5
-        if dt is not None:
-            w = w.to(dt)
-        res = {}
-        for vs in (0, 1):
-            ops.set_debug("mm_vstore", vs)
-            ops.update_mm(x, w)
-            t = []
-            for _ in range(5):
-                a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-                a.record()
-                for _ in range(10):
-                    ops.update_mm(x, w)
-                b.record()
-                torch.cuda.synchronize()
-                t.append(a.elapsed_time(b) / 10)
-            res[vs] = float(np.median(t))
-        ops.set_debug("mm_vstore", 1)
-        print(f"M={M} K={K} N={N}: dword stores {res[0]:.3f} ms ({2 * M * K * N / res[0] / 1e9:.0f} TF), "
-              f"16-B stores {res[1]:.3f} ms ({2 * M * K * N / res[1] / 1e9:.0f} TF)", flush=True)
+    dev = torch.device("cuda", 0)
+    args = sys.argv[1:]
+    which = "all"
+    if "--shapes" in args:
+        which = args[args.index("--shapes") + 1]
+    for a in args:
+        if "=" in a and not a.startswith("--"):
+            k, v = a.split("=")
+            ops.set_debug(k, int(v))
+    names = list(SHAPES) if which == "all" else which.split(",")
+    for nm in names:
+        for shp in SHAPES[nm]:
+            print(json.dumps(one(*shp, dev)), flush=True)
 
 
 if __name__ == "__main__":

@@ -1,0 +1,67 @@
+"""SQ / TCC counters of the metric launches (k_agg_h32 + k_seg_reduce), one rocprofv3 --pmc pass
+per counter group (each within the per-block slot limits), over `bench.py --pmc-child` (the bench's
+own inputs and launches).  Per-kernel means over the launches after the first (cold) one.
+Usage: python scripts/pmc_sq.py OUT_DIR  -> OUT_DIR/<group>/... CSVs and OUT_DIR/summary.json"""
+import csv
+import glob
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GROUPS = {
+    "sq_time": ["SQ_WAVES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+                "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VMEM", "SQ_ACTIVE_INST_VALU"],
+    "sq_insts": ["SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_SALU", "SQ_INSTS_LDS",
+                 "SQ_ACTIVE_INST_LDS", "SQ_INSTS_SMEM", "GRBM_GUI_ACTIVE"],
+    "l2": ["TCC_HIT_sum", "TCC_MISS_sum", "TCP_TCC_READ_REQ_sum"],
+}
+KERNELS = ("k_agg_h32", "k_seg_reduce")
+
+
+def summarize(d):
+    per = {}
+    for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            name = row.get("Kernel_Name", "")
+            k = next((k for k in KERNELS if k in name), None)
+            if k is None:
+                continue
+            did = int(row.get("Dispatch_Id") or row.get("Correlation_Id") or 0)
+            per.setdefault((k, row["Counter_Name"]), []).append((did, float(row["Counter_Value"])))
+    out = {}
+    for (k, c), vals in per.items():
+        vals = [v for _, v in sorted(vals)]
+        vals = vals[1:] if len(vals) > 1 else vals
+        out.setdefault(k, {})[c] = sum(vals) / len(vals)
+    return out
+
+
+def main(out_dir):
+    os.makedirs(out_dir, exist_ok=True)
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    summary = {}
+    for gname, counters in GROUPS.items():
+        d = os.path.join(out_dir, gname)
+        shutil.rmtree(d, ignore_errors=True)
+        cmd = ["timeout", "-s", "KILL", "120", shutil.which("rocprofv3") or "rocprofv3", "--kernel-trace", "--pmc",
+               *counters, "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable,
+               os.path.join(ROOT, "bench.py"), "--pmc-child", "--steps", "4"]
+        p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True)
+        print(gname, "rc", p.returncode, p.stderr[-300:] if p.returncode else "", flush=True)
+        if p.returncode != 0:
+            summary[gname] = {"error": p.returncode}
+            if p.returncode in (124, 137, -9):
+                break
+            continue
+        summary[gname] = summarize(d)
+    with open(os.path.join(out_dir, "summary.json"), "w") as fh:
+        json.dump(summary, fh, indent=1)
+    print(json.dumps(summary))
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_sq"))

@@ -85,9 +85,9 @@ def test_tuning_handles(lib):
     (the pointer is only a key here: no device work)."""
     from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
     thread_val = ops.get_debug("seg_lean")
-    t = ops.Tuning(seg_lean=1 - thread_val, mm_blaslt_max_m=1 << 40)
-    assert t.get("seg_lean") == 1 - thread_val and t.get("mm_blaslt_max_m") == 1 << 40
-    assert ops.Tuning().get("mm_blaslt_max_m") == 65535  # a fresh handle holds the defaults
+    t = ops.Tuning(seg_lean=1 - thread_val, mm_split=1 << 40)
+    assert t.get("seg_lean") == 1 - thread_val and t.get("mm_split") == 1 << 40  # 64-bit knob values
+    assert ops.Tuning().get("mm_split") == -1  # a fresh handle holds the defaults
     assert ops.get_debug("seg_lean") == thread_val        # the thread's knobs are untouched
     with pytest.raises(_lib.GTAError):
         t.set("no_such_knob", 1)

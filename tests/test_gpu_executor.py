@@ -289,3 +289,55 @@ def test_repeated_execute_replays_a_hip_graph(golden_dir, manifest, cora, dev, t
     again = run()
     for k in fresh:
         assert torch.equal(again.outputs[k], fresh[k])
+    # a weight changed in place (load_state_dict / optimizer step): the replay re-transposes it into
+    # the graph's W^T instead of reading the stale one
+    wkey = sorted(k for k in tensors if k.startswith("w:"))[0]
+    tensors[wkey].mul_(-1.5)
+    fresh = executor.Executor(og, ir.Stream(ir.read_yaml("Results/Insts/GCN-cora-layer1-original.yaml")), gd,
+                              tensors, Semantics.for_network("GCN", False)).run()
+    again = run()
+    for k in fresh:
+        assert torch.equal(again.outputs[k], fresh[k])
+    # a knob change is part of the cache key: the next call runs eagerly under the new knobs
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
+    n_entries = len(executor._AUTO)
+    try:
+        ops.set_debug("mm_ring", 0)
+        later = run()
+        assert len(executor._AUTO) == n_entries + 1
+    finally:
+        ops.set_debug("mm_ring", 1)
+    for k in fresh:
+        assert torch.equal(later.outputs[k], fresh[k])  # k_mm_rows == k_mm_ring bitwise
+    executor.set_auto_graph(False)
+    try:
+        assert not executor._AUTO
+        for k, v in run().outputs.items():
+            assert torch.equal(v, fresh[k])
+    finally:
+        executor.set_auto_graph(True)
+
+
+def test_graphed_run_follows_weights_changed_in_place(golden_dir, manifest, cora, dev):
+    """GraphedRun keeps the W^T tensors its launches read and refreshes them when a weight's
+    version moves (in-place update), so replays never read a stale or freed transpose."""
+    rec = [s for s in _all_streams(manifest) if s["network"] == "GraphSAGE" and not s["reorder"]
+           and s["dataset"] == "cora"][0]
+    sem = Semantics.for_network("GraphSAGE", False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    ip, ix = cora
+    gd = G.from_numpy(ip, ix, device=dev)
+    tensors = {k: v.to(dev) for k, v in workloads.make_tensors(og, G.from_numpy(ip, ix), "GraphSAGE", seed=3).items()}
+    gr = executor.GraphedRun(og, st, gd, tensors, sem)
+    assert gr._wts, "the captured graph reads at least one cached W^T"
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
+    ops._WT_CACHE.clear()  # the cache may drop its entries: the graph still holds its own
+    for trial in range(3):
+        for k in tensors:
+            if k.startswith("w:"):
+                tensors[k].add_(0.125 * (trial + 1))
+        out = {k: v.clone() for k, v in gr.replay().items()}
+        ref = executor.Executor(og, st, gd, tensors, sem).run()
+        for k in ref:
+            assert torch.equal(out[k], ref[k]), (k, trial)

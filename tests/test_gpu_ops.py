@@ -34,6 +34,9 @@ def _graph(n, e, seed=0, kind="lognormal", heavy_row=None, empty_rows=0, dev=Non
     return gd, ip, ix
 
 
+_DT = {"f32": 0, "bf16": 1, "mixed": 2}  # include/gta.h GTA_F32 / GTA_BF16 / GTA_F32_BF16
+
+
 def _check(got, ref, scale, what):
     got = got.detach().cpu().numpy().astype(np.float64)
     err = np.abs(got - ref)
@@ -251,9 +254,9 @@ def test_update_mm_f32_x_bf16_w(dev, M, K, N):
 
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 16), (128, 4), (64, 4), (256, 16), (128, 0), (64, 0)])
 @pytest.mark.parametrize("blocks", [1, 7, 32, 63])
-@pytest.mark.parametrize("single", [True, False])
-def test_aggregate_blocked_matches_oracle(dev, F, heads, blocks, single):
-    """Column-blocked K6 (B launches over source-column slices) == fp64 oracle; rows must be column-sorted."""
+def test_aggregate_blocked_matches_oracle(dev, F, heads, blocks):
+    """Column-blocked K6 (work items over B source-column slices + ordered reduce) == fp64 oracle;
+    rows must be column-sorted."""
     n, e = 700, 20000
     g0 = G.synthetic(n, e, seed=blocks + F, device="cpu")          # sorted columns
     ip, ix = g0.numpy()
@@ -267,11 +270,11 @@ def test_aggregate_blocked_matches_oracle(dev, F, heads, blocks, single):
     x = rng.standard_normal((n, F)).astype(np.float32)
     w = rng.random((len(ix), heads)).astype(np.float32) if heads else None
     y = ops.aggregate_blocked(g, torch.from_numpy(x).to(dev), None if w is None else torch.from_numpy(w).to(dev),
-                              blocks=blocks, single_launch=single)
+                              blocks=blocks)
     ref = isa_ref.aggregate(ip, ix, x, "src", w)
     _check(y, ref, isa_ref.aggregate_abs(ip, ix, x, "src", w), f"blocked F={F} H={heads} B={blocks}")
     y2 = ops.aggregate_blocked(g, torch.from_numpy(x).to(dev), None if w is None else torch.from_numpy(w).to(dev),
-                               blocks=blocks, single_launch=single)
+                               blocks=blocks)
     assert torch.equal(y, y2)
 
 
@@ -334,12 +337,6 @@ def test_aggregate_blocked_accumulate_rowscale(dev):
     yd = torch.from_numpy(y0).to(dev)
     ops.aggregate_blocked(g, torch.from_numpy(x).to(dev), torch.from_numpy(w).to(dev),
                           row_scale=torch.from_numpy(sc).to(dev), out=yd, accumulate=True, blocks=16)
-    y2 = torch.from_numpy(y0).to(dev)
-    ops.aggregate_blocked(g, torch.from_numpy(x).to(dev), torch.from_numpy(w).to(dev),
-                          row_scale=torch.from_numpy(sc).to(dev), out=y2, accumulate=True, blocks=16,
-                          single_launch=False)
-    _check(y2, y0 + isa_ref.aggregate(ip, ix, x, "src", w, sc),
-           isa_ref.aggregate_abs(ip, ix, x, "src", w, sc) + np.abs(y0), "blocked multi acc+scale")
     ref = y0 + isa_ref.aggregate(ip, ix, x, "src", w, sc)
     _check(yd, ref, isa_ref.aggregate_abs(ip, ix, x, "src", w, sc) + np.abs(y0), "blocked acc+scale")
 
@@ -391,14 +388,11 @@ def test_edge_softmax_other_sf_and_errors(dev):
         ops.edge_softmax(g, a, b[:, :4].contiguous())
 
 
-@pytest.mark.parametrize("knobs", [{"seg_quarter": 0}, {"seg_u": 2}, {"seg_u": 4}, {"seg_nt": 2}, {"seg_nt": 6},
-                                   {"seg_nt": 7}, {"seg_lanes": 16},
-                                   {"seg_lanes": 16, "seg_u": 4}, {"seg_lean": 0}, {"seg_nt": 0}, {"seg_nt": 1},
-                                   {"seg_lean_w1": 0}, {"seg_fuse": 0}, {"seg_fuse": 2}])
+@pytest.mark.parametrize("knobs", [{"seg_lean": 0}, {"seg_lean_w1": 0}])
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 0), (64, 4), (256, 16), (128, 1)])
 def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
-    """Every form of the blocked kernel (one item per wave, quarter-wave with 2/4/8 edges per
-    step, non-temporal bits) == the fp64 oracle and == the default form bitwise."""
+    """The lean half-wave kernels (k_agg_h32, also with one weight per edge) == the generic
+    half-wave form bitwise (same per-item edge order and fma chain), and == the fp64 oracle."""
     n, e = 900, 30000
     g = G.synthetic(n, e, seed=F + heads, device=dev)
     ip, ix = g.numpy()
@@ -406,24 +400,16 @@ def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
     w = torch.from_numpy(rng.random((g.nnz, heads)).astype(np.float32)).to(dev) if heads else None
     y0 = ops.aggregate_blocked(g, x, w, blocks=8)
-    defaults = {"seg_quarter": 1, "seg_u": 8, "seg_nt": 3, "seg_lanes": 32, "seg_lean": 1, "seg_lean_w1": 1,
-                "seg_fuse": 0}
     try:
         for k, v in knobs.items():
             ops.set_debug(k, v)
-        try:
-            y = ops.aggregate_blocked(g, x, w, blocks=8)
-        except ops._lib.GTAError:
-            if "seg_quarter" in knobs and heads and ((F // heads) // (F // 64)) not in (4, 8, 16):
-                pytest.skip("the one-item-per-wave form needs (F/heads)/(F/64) in {4, 8, 16}")
-            raise
+        y = ops.aggregate_blocked(g, x, w, blocks=8)
     finally:
         for k in knobs:
-            ops.set_debug(k, defaults[k])
+            ops.set_debug(k, 1)
     xn, wn = x.cpu().numpy(), None if w is None else w.cpu().numpy()
     _check(y, isa_ref.aggregate(ip, ix, xn, "src", wn), isa_ref.aggregate_abs(ip, ix, xn, "src", wn), f"{knobs}")
-    if "seg_quarter" not in knobs:
-        assert torch.equal(y, y0)  # same per-item edge order in every quarter/half-wave form
+    assert torch.equal(y, y0)  # same per-item edge order in every half-wave form
 
 
 @pytest.mark.parametrize("form", ["rows", "tile"])
@@ -442,12 +428,10 @@ def test_update_mm_both_forms(dev, form, M, K, N, dt):
         w = w.to(torch.bfloat16)
     old = ops.MM_FORM, ops.MM_ROWS_MIN_M
     ops.MM_FORM, ops.MM_ROWS_MIN_M = form, 0
-    ops.set_debug("mm_blaslt", 0)  # the hand-written kernels, not the library path
     try:
         out = ops.update_mm(xs.to(dev), w.to(dev))
     finally:
         ops.MM_FORM, ops.MM_ROWS_MIN_M = old
-        ops.set_debug("mm_blaslt", 1)
     xr = xs.float().numpy().astype(np.float64)
     if dt != "f32":
         xr = torch.from_numpy(xr).to(torch.bfloat16).double().numpy()
@@ -471,8 +455,7 @@ def test_update_mm_weight_cache_never_stale(dev):
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 16), (128, 1), (64, 4), (64, 16), (256, 8), (256, 16)])
 @pytest.mark.parametrize("normalize", [True, False])
 @pytest.mark.parametrize("blocks", [1, 5, 16])
-@pytest.mark.parametrize("lanes", [32, 16])
-def test_gat_aggregate_blocked_matches_oracle(dev, F, heads, normalize, blocks, lanes):
+def test_gat_aggregate_blocked_matches_oracle(dev, F, heads, normalize, blocks):
     """Fused GAT attention aggregate vs the oracle's op-by-op composition (edge softmax, alpha * x,
     gather); empty rows give 0 (normalize) and a 3000-edge row spans every block."""
     n, e = 800, 20000
@@ -486,13 +469,9 @@ def test_gat_aggregate_blocked_matches_oracle(dev, F, heads, normalize, blocks, 
     x = rng.standard_normal((n, F)).astype(np.float32)
     a = rng.standard_normal((n, heads)).astype(np.float32)
     b = rng.standard_normal((n, heads)).astype(np.float32)
-    ops.set_debug("seg_lanes", lanes)
-    try:
-        y, sums = ops.gat_aggregate_blocked(g, torch.from_numpy(x).to(dev), torch.from_numpy(a).to(dev),
-                                            torch.from_numpy(b).to(dev), normalize=normalize, want_sums=True,
-                                            blocks=blocks)
-    finally:
-        ops.set_debug("seg_lanes", 32)
+    y, sums = ops.gat_aggregate_blocked(g, torch.from_numpy(x).to(dev), torch.from_numpy(a).to(dev),
+                                        torch.from_numpy(b).to(dev), normalize=normalize, want_sums=True,
+                                        blocks=blocks)
     ref, rsum = isa_ref.gat_aggregate(ip, ix, x.astype(np.float64), a.astype(np.float64), b.astype(np.float64),
                                       "EXP_LEAKY_RELU", normalize)
     _check(sums, rsum, rsum, f"gat sums F={F} H={heads}")
@@ -526,14 +505,13 @@ def test_gat_aggregate_lean_bitwise(dev, blocks, item_edges, ldb):
     plan = g.blocked_plan(blocks, item_edges)
     outs = {}
     try:
-        for lean in (0, 1, 2):
+        for lean in (0, 1):
             ops.set_debug("att_lean", lean)
             outs[lean] = ops.gat_aggregate_blocked(g, x, a, b, want_sums=True, plan=plan)
     finally:
-        ops.set_debug("att_lean", 2)
-    for lean in (1, 2):
-        assert torch.equal(outs[0][0], outs[lean][0]), lean
-        assert torch.equal(outs[0][1], outs[lean][1]), lean
+        ops.set_debug("att_lean", 1)
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
     ref, rsum = isa_ref.gat_aggregate(ip, ix, x.cpu().numpy().astype(np.float64), a.cpu().numpy().astype(np.float64),
                                       b.cpu().numpy().astype(np.float64), "EXP_LEAKY_RELU", True)
     _check(outs[1][1], rsum, rsum, "lean gat sums")
@@ -631,12 +609,12 @@ def test_update_mm_prefetch_forms(dev, pf, M, K, N, dt):
     elif dt == "mixed":
         w = w.to(torch.bfloat16)
     ops.set_debug("mm_prefetch", pf)
-    ops.set_debug("mm_blaslt", 0)  # the hand-written row kernel, not the library path
+    ops.set_debug("mm_ring", 0)  # k_mm_rows (the fp32 shapes default to the ring)
     try:
         out = ops.update_mm(x.to(dev), w.to(dev))
     finally:
         ops.set_debug("mm_prefetch", 1)
-        ops.set_debug("mm_blaslt", 1)
+        ops.set_debug("mm_ring", 1)
     xr = x.float().numpy().astype(np.float64)
     if dt != "f32":
         xr = torch.from_numpy(xr).to(torch.bfloat16).double().numpy()
@@ -658,7 +636,7 @@ def test_update_mm_split_k(dev, M, K, N, dt, gathered):
     elif dt == "mixed":
         w = w.to(torch.bfloat16)
     idx = torch.from_numpy(rng.integers(0, M + 7, M).astype(np.int32)) if gathered else None
-    assert ops._mm_splits(M, K, N) > 1
+    assert ops._mm_splits(M, K, N, _DT[dt]) > 1
     xd, wd = x.to(dev), w.to(dev)
     idd = None if idx is None else idx.to(dev)
     out = ops.update_mm(xd, wd, idd, sf="RELU", m=None if gathered else M)
@@ -671,123 +649,30 @@ def test_update_mm_split_k(dev, M, K, N, dt, gathered):
     _check(out, ref, np.abs(xs).astype(np.float64) @ np.abs(wf).astype(np.float64), f"split-K {dt}")
 
 
-@pytest.mark.parametrize("M,K,N,ldx_pad", [(40000, 602, 128, 0), (40000, 602, 256, 3), (33000, 37, 200, 1),
-                                           (89250, 500, 128, 0), (2708, 1433, 128, 0), (3000, 602, 128, 2)])
-def test_update_mm_plain_f32_library_path(dev, M, K, N, ldx_pad):
-    """Plain fp32 UPDATE with M >= 32768 runs on hipBLASLt inside libgta (gta_update_mm_t): fp64 bound,
-    strided x, and within the fp32 bound of the hand-written k_mm_rows on the same operands."""
+@pytest.mark.parametrize("M,K,N,ldx_pad", [(2708, 1433, 128, 0), (16384, 128, 128, 0), (29000, 602, 128, 0),
+                                           (44625, 500, 128, 0), (29000, 602, 256, 3), (16384, 1433, 128, 1),
+                                           (2708, 128, 64, 0), (3000, 602, 128, 2)])
+def test_update_mm_mid_rows_hand_written(dev, M, K, N, ldx_pad):
+    """Plain fp32 UPDATE at 1,024 <= M < 65,536 rows -- GCN Cora's layers, 16,384 rows, 8-way
+    Reddit (29,000) and 2-way Flickr (44,625) row shards -- on the hand-written kernels alone
+    (k_mm_ring: the 8-deep split-K form for few row groups, else the 8- / 4- / 3-deep persistent
+    ring): within the fp64 bound, deterministic, and bitwise equal to k_mm_rows on the same
+    split plan (strided x: ldx = K + pad)."""
     rng = np.random.default_rng(M + K + N)
     x = torch.from_numpy(rng.standard_normal((M, K + ldx_pad)).astype(np.float32))[:, :K]
     w = torch.from_numpy((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32))
     xd, wd = x.to(dev), w.to(dev)
     out = ops.update_mm(xd, wd)
-    ops.set_debug("mm_blaslt", 0)
+    ops.set_debug("mm_ring", 0)
     try:
         own = ops.update_mm(xd, wd)
     finally:
-        ops.set_debug("mm_blaslt", 1)
+        ops.set_debug("mm_ring", 1)
     xr, wf = x.numpy().astype(np.float64), w.numpy().astype(np.float64)
     scale = np.abs(xr) @ np.abs(wf)
-    _check(out, xr @ wf, scale, "update_mm hipBLASLt")
-    _check(own, xr @ wf, scale, "update_mm k_mm_rows")
+    _check(out, xr @ wf, scale, "update_mm k_mm_ring")
+    assert torch.equal(out, own)
     assert torch.equal(out, ops.update_mm(xd, wd))  # deterministic
-
-
-@pytest.mark.parametrize("M,K,N,dt,gathered", [(5000, 602, 128, "f32", False), (4099, 100, 130, "mixed", True),
-                                                (3001, 128, 8, "bf16", False), (2708, 1433, 128, "f32", False),
-                                                (777, 64, 200, "f32", True)])
-def test_update_mm_vector_store_bitwise(dev, M, K, N, dt, gathered):
-    """k_mm_rows' quad-transposed 16-B row-store epilogue == the four-dword-store epilogue bitwise
-    (row-streaming and split-K forms, column tails, gathered rows)."""
-    rng = np.random.default_rng(M + N)
-    x = torch.from_numpy(rng.standard_normal((M + 3, K)).astype(np.float32))
-    w = torch.from_numpy(rng.standard_normal((K, N)).astype(np.float32))
-    if dt == "bf16":
-        x, w = x.to(torch.bfloat16), w.to(torch.bfloat16)
-    elif dt == "mixed":
-        w = w.to(torch.bfloat16)
-    idx = torch.from_numpy(rng.integers(0, M + 3, M).astype(np.int32)).to(dev) if gathered else None
-    xd, wd = x.to(dev), w.to(dev)
-    outs = []
-    old_min = ops.MM_ROWS_MIN_M
-    try:
-        ops.MM_ROWS_MIN_M = 0
-        for vs in (1, 0):
-            ops.set_debug("mm_vstore", vs)
-            outs.append(ops.update_mm(xd, wd, idx, sf="RELU", m=None if gathered else M))
-    finally:
-        ops.set_debug("mm_vstore", 1)
-        ops.MM_ROWS_MIN_M = old_min
-    assert torch.equal(outs[0], outs[1])
-
-
-@pytest.mark.parametrize("blocks,item_edges,heads", [(1, 256, 8), (7, 64, 8), (20, 256, 1), (16, 1 << 30, 0)])
-def test_blocked_plan_length_sort_bitwise(dev, blocks, item_edges, heads):
-    """Sorting each block's items by length (matched half-wave pairs) moves only item ids: the
-    metric aggregate and the fused attention aggregate are bitwise unchanged."""
-    n, e, F = 4000, 120000, 128
-    g0 = G.synthetic(n, e, seed=blocks + heads, device="cpu")
-    ip, ix = g0.numpy()
-    rng = np.random.default_rng(blocks)
-    x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
-    w = torch.from_numpy(rng.random((len(ix), heads)).astype(np.float32)).to(dev) if heads else None
-    a = torch.from_numpy(rng.standard_normal((n, 8)).astype(np.float32)).to(dev)
-    b = torch.from_numpy(rng.standard_normal((n, 8)).astype(np.float32)).to(dev)
-    outs = {}
-    try:
-        for srt in (0, 1):
-            ops.set_debug("plan_len_sort", srt)
-            g = G.from_numpy(ip, ix, device=dev)  # a fresh graph: plans are cached per graph
-            plan = g.blocked_plan(blocks, item_edges)
-            outs[srt] = (ops.aggregate_blocked(g, x, w, plan=plan, blocks=blocks),
-                         ops.gat_aggregate_blocked(g, x, a, b, want_sums=True, plan=plan))
-    finally:
-        ops.set_debug("plan_len_sort", 1)
-    assert torch.equal(outs[0][0], outs[1][0])
-    assert torch.equal(outs[0][1][0], outs[1][1][0]) and torch.equal(outs[0][1][1], outs[1][1][1])
-
-
-@pytest.mark.parametrize("heads", [8, 1, 0])
-@pytest.mark.parametrize("accumulate", [False, True])
-def test_aggregate_blocked_fused_reduce_bitwise(dev, heads, accumulate):
-    """The in-launch ordered reduce (last-arriving item of a row sums its partials, seg_fuse=1 / 2)
-    == the two-launch form (k_seg_reduce, seg_fuse=0, the default) bitwise, on rows of every kind:
-    empty (scale inf: 0 * inf = NaN in both), one item (written directly), many blocks, and rows
-    split into several parts per block (item_edges 16); with row_scale and accumulate."""
-    n = 700
-    rng = np.random.default_rng(11 + heads)
-    deg = rng.integers(0, 6, n)
-    deg[::7] = 0
-    deg[3::50] = rng.integers(300, 1500, len(deg[3::50]))
-    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
-    ix = np.concatenate([np.sort(rng.choice(n, d, replace=d > n)) for d in deg]).astype(np.int32)
-    g = G.from_numpy(ip, ix).to(dev)
-    x = torch.from_numpy(rng.standard_normal((n, 128)).astype(np.float32)).to(dev)
-    w = torch.from_numpy(rng.random((g.nnz, heads)).astype(np.float32)).to(dev) if heads else None
-    scale = torch.from_numpy(np.where(deg > 0, 1.0 / np.maximum(deg, 1), np.inf).astype(np.float32)).to(dev)
-    y_init = torch.from_numpy(rng.standard_normal((n, 128)).astype(np.float32)).to(dev)
-    plan = ops.BlockedPlan(g, blocks=6, item_edges=16)
-    outs = []
-    for fuse in (0, 1, 2):
-        ops.set_debug("seg_fuse", fuse)
-        try:
-            y = y_init.clone()
-            outs.append(ops.aggregate_blocked(g, x, w, row_scale=scale, out=y, accumulate=accumulate, plan=plan))
-        finally:
-            ops.set_debug("seg_fuse", 0)
-    torch.cuda.synchronize()
-    for o in outs[1:]:
-        assert torch.equal(torch.nan_to_num(o, nan=7.0), torch.nan_to_num(outs[0], nan=7.0))
-        assert torch.equal(torch.isnan(o), torch.isnan(outs[0]))
-    xn, wn = x.cpu().numpy(), None if w is None else w.cpu().numpy()
-    ref = isa_ref.aggregate(ip, ix, xn, "src", wn) * np.where(deg > 0, 1.0 / np.maximum(deg, 1), 0)[:, None]
-    if accumulate:
-        ref = ref + y_init.cpu().numpy()
-    has = deg > 0
-    bound = 1e-5 * isa_ref.aggregate_abs(ip, ix, xn, "src", wn) + 1e-6 + (1e-6 * np.abs(ref) if accumulate else 0)
-    err = np.abs(outs[1].cpu().numpy().astype(np.float64) - ref)
-    assert np.all(err[has] <= bound[has])
-    assert torch.isnan(outs[1][torch.from_numpy(~has).to(dev)]).all()  # 0 * inf, as the reduce pass gives
 
 
 @pytest.mark.parametrize("M,K,N,gathered,sf", [(40000, 602, 128, False, None), (20000, 602, 128, True, "RELU"),
@@ -795,12 +680,12 @@ def test_aggregate_blocked_fused_reduce_bitwise(dev, heads, accumulate):
                                                (17000, 1433, 128, False, None), (777, 100, 100, True, None),
                                                (130, 48, 72, False, "ELU"), (89250, 500, 128, False, None)])
 def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
-    """k_mm_ring (fp32 UPDATE through the 3-stage LDS-DMA ring, the default for plain fp32 GEMMs)
-    == k_mm_rows bitwise (same per-lane k order and MFMA chain), and both within the fp64 bound:
-    K tails (register steps of 16 k), rows past M, columns
-    past N (two column blocks at N = 200), gathered rows, SF epilogues, x rows not 16-B aligned
-    (K = 602, 1433: 16-B DMA pieces at 8-B aligned addresses by default, the 4-B A-DMA form with
-    mm_ring_a16u = 0), every stage form.  Shapes with enough row groups not to take the split-K form."""
+    """k_mm_ring (fp32 UPDATE through the LDS-DMA ring, the default for fp32 GEMMs) == k_mm_rows
+    bitwise (same per-lane k order and MFMA chain), and both within the fp64 bound: K tails
+    (register steps of 16 k), rows past M, columns past N (two column blocks at N = 200), gathered
+    rows, SF epilogues, x rows not 16-B aligned (K = 602, 1433: 16-B DMA pieces at 8-B aligned
+    addresses), 128- and 64-row groups, ring depths 8 / 4 / 3 (one, two and more blocks per CU).
+    Shapes with enough row groups not to take the split-K form."""
     assert ops._mm_splits(M, K, N) == 1
     rng = np.random.default_rng(M + K + N)
     x = torch.from_numpy(rng.standard_normal((M + 5, K)).astype(np.float32))
@@ -812,22 +697,14 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     old_min = ops.MM_ROWS_MIN_M
     try:
         ops.MM_ROWS_MIN_M = 0
-        ops.set_debug("mm_blaslt", 0)
-        # k_mm_rows, then the ring's four stage forms, then the 4-B A-DMA path
-        # then 64-row groups (one A fragment per wave), with 16-B and 4-B A pieces
-        for ring, form, a16u, fr in ((0, 0, 1, 2), (1, 0, 1, 2), (1, 1, 1, 2), (1, 2, 1, 2), (1, 3, 1, 2),
-                                     (1, 0, 0, 2), (1, 0, 1, 1), (1, 0, 0, 1), (1, 0, 1, 0)):
+        # k_mm_rows, then the ring with 128-row groups, 64-row groups, and the automatic choice
+        for ring, fr in ((0, 0), (1, 2), (1, 1), (1, 0)):
             ops.set_debug("mm_ring", ring)
-            ops.set_debug("mm_ring_form", form)
-            ops.set_debug("mm_ring_a16u", a16u)
             ops.set_debug("mm_ring_fr", fr)
             outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
     finally:
         ops.set_debug("mm_ring", 1)
-        ops.set_debug("mm_ring_form", 0)
-        ops.set_debug("mm_ring_a16u", 1)
         ops.set_debug("mm_ring_fr", 0)
-        ops.set_debug("mm_blaslt", 1)
         ops.MM_ROWS_MIN_M = old_min
     torch.cuda.synchronize()
     for o in outs[1:]:
@@ -839,29 +716,21 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
 
 @pytest.mark.parametrize("M,K", [(70000, 602), (65536, 100), (120000, 602), (120000, 128)])
 def test_update_mm_default_is_the_ring(dev, M, K):
-    """From 65,536 rows the DEFAULT plain fp32 UPDATE (no knobs touched) is the hand-written
-    k_mm_ring, not the library: bitwise equal to k_mm_rows (the library's contraction order
-    differs), and within the fp64 bound.  120,000 rows: 938 128-row groups over 768 block slots,
-    so K = 128 runs 64-row groups throughout; with knob mm_ring_tail K = 602 runs whole rounds + the
-    remainder as 64-row groups (two launches), bitwise the same."""
+    """From 65,536 rows the DEFAULT plain fp32 UPDATE (no knobs touched) is the persistent 3-deep
+    k_mm_ring: bitwise equal to k_mm_rows and within the fp64 bound.  120,000 rows: 938 128-row
+    groups over 768 block slots, so K = 128 runs 64-row groups throughout."""
     rng = np.random.default_rng(M + K)
     x = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32))
     w = torch.from_numpy((rng.standard_normal((K, 128)) / np.sqrt(K)).astype(np.float32))
     xd, wd = x.to(dev), w.to(dev)
     y = ops.update_mm(xd, wd)
     try:
-        ops.set_debug("mm_ring_tail", 1)
-        y_tail = ops.update_mm(xd, wd)
-        ops.set_debug("mm_ring_tail", 0)
-        ops.set_debug("mm_blaslt", 0)
         ops.set_debug("mm_ring", 0)
         y_rows = ops.update_mm(xd, wd)
     finally:
-        ops.set_debug("mm_ring_tail", 0)
         ops.set_debug("mm_ring", 1)
-        ops.set_debug("mm_blaslt", 1)
     torch.cuda.synchronize()
-    assert torch.equal(y, y_rows) and torch.equal(y_tail, y_rows)
+    assert torch.equal(y, y_rows)
     rows = np.arange(0, M, 97)
     ref = isa_ref.mm(x.numpy()[rows], w.numpy())
     _check(y[rows], ref, np.abs(x.numpy()[rows]).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "default UPDATE")
@@ -870,8 +739,8 @@ def test_update_mm_default_is_the_ring(dev, M, K):
 @pytest.mark.parametrize("K,off", [(602, 1), (500, 3), (128, 1)])
 def test_update_mm_ring_4b_aligned_rows(dev, K, off):
     """x a column window of a wider table (ldx = K + 4 + off, base off * 4 B into the row): every
-    row start only 4-B aligned, as the ring's 16-B A DMA pieces allow.  Ring (16-B and 4-B A
-    pieces) == k_mm_rows bitwise, within the fp64 bound."""
+    row start only 4-B aligned, as the ring's 16-B A DMA pieces allow.  Ring == k_mm_rows bitwise,
+    within the fp64 bound."""
     M, N = 40000, 128  # enough row groups for the one-pass ring (no split-K)
     rng = np.random.default_rng(K + off)
     big = torch.from_numpy(rng.standard_normal((M, K + 4 + off)).astype(np.float32))
@@ -883,15 +752,11 @@ def test_update_mm_ring_4b_aligned_rows(dev, K, off):
     old_min = ops.MM_ROWS_MIN_M
     try:
         ops.MM_ROWS_MIN_M = 0
-        ops.set_debug("mm_blaslt", 0)
-        for ring, a16u in ((0, 1), (1, 1), (1, 0)):
+        for ring in (0, 1):
             ops.set_debug("mm_ring", ring)
-            ops.set_debug("mm_ring_a16u", a16u)
             outs.append(ops.update_mm(xd, wd))
     finally:
         ops.set_debug("mm_ring", 1)
-        ops.set_debug("mm_ring_a16u", 1)
-        ops.set_debug("mm_blaslt", 1)
         ops.MM_ROWS_MIN_M = old_min
     torch.cuda.synchronize()
     for o in outs[1:]:
@@ -903,59 +768,54 @@ def test_update_mm_ring_4b_aligned_rows(dev, K, off):
 
 def test_tuning_attached_to_a_stream(dev):
     """ABI 4: a knob set attached to a stream governs every call on that stream, from any thread,
-    and nothing else.  Observable through the UPDATE route at 70,000 rows: the default is the ring
-    (bitwise k_mm_rows); a set with mm_blaslt_max_m raised sends it to the library (other rounding,
-    bitwise equal to the same route chosen by the thread knob)."""
+    and nothing else.  Observable through seg_phase = 1 (the blocked aggregate's item launch alone:
+    y is left untouched) against the default (items + ordered reduce: y written)."""
     import threading
-    rng = np.random.default_rng(7)
-    x = torch.from_numpy(rng.standard_normal((70000, 602)).astype(np.float32)).to(dev)
-    w = torch.from_numpy((rng.standard_normal((602, 128)) / np.sqrt(602)).astype(np.float32)).to(dev)
-    y_ring = ops.update_mm(x, w)
-    try:
-        ops.set_debug("mm_blaslt_max_m", 1 << 40)
-        y_lib = ops.update_mm(x, w)
-    finally:
-        ops.set_debug("mm_blaslt_max_m", 65535)
-    torch.cuda.synchronize()
-    assert not torch.equal(y_ring, y_lib)  # the two routes round differently
+    g = G.synthetic(2000, 40000, seed=3, device=dev)
+    x = torch.randn(2000, 128, device=dev)
+    w = torch.rand(g.nnz, 8, device=dev)
+    y_ref = ops.aggregate_blocked(g, x, w, blocks=4)
+    sentinel = torch.full_like(y_ref, 7.0)
     s = torch.cuda.Stream(dev)
-    t = ops.Tuning(mm_blaslt_max_m=1 << 40)
+    t = ops.Tuning(seg_phase=1)
     t.attach(s)
     try:
         s.wait_stream(torch.cuda.current_stream(dev))
         with torch.cuda.stream(s):
-            y_att = ops.update_mm(x, w)
+            y_att = ops.aggregate_blocked(g, x, w, out=sentinel.clone(), blocks=4)
         out = {}
 
         def other():
             with torch.cuda.stream(s):
-                out["y"] = ops.update_mm(x, w)
+                out["y"] = ops.aggregate_blocked(g, x, w, out=sentinel.clone(), blocks=4)
             s.synchronize()
         th = threading.Thread(target=other)
         th.start()
         th.join()
-        y_plain = ops.update_mm(x, w)  # the current stream: nothing attached
+        y_plain = ops.aggregate_blocked(g, x, w, out=sentinel.clone(), blocks=4)  # current stream: nothing attached
         s.synchronize()
         torch.cuda.synchronize()
-        assert torch.equal(y_att, y_lib) and torch.equal(out["y"], y_lib)
-        assert torch.equal(y_plain, y_ring)
+        assert torch.equal(y_att, sentinel) and torch.equal(out["y"], sentinel)
+        assert torch.equal(y_plain, y_ref)
+        assert ops.Tuning.attached(s)
     finally:
         ops.Tuning.detach(s)
+    assert not ops.Tuning.attached(s)
     with torch.cuda.stream(s):
-        y_det = ops.update_mm(x, w)
+        y_det = ops.aggregate_blocked(g, x, w, out=sentinel.clone(), blocks=4)
     s.synchronize()
-    assert torch.equal(y_det, y_ring)
+    assert torch.equal(y_det, y_ref)
 
 
 @pytest.mark.parametrize("M,K,N,gathered,sf", [(2708, 1433, 128, False, None), (2708, 1433, 128, True, "RELU"),
                                                (2708, 1432, 64, False, None), (1000, 1350, 64, False, None),
                                                (600, 1000, 200, False, "ELU"), (900, 700, 66, False, None)])
 def test_update_mm_split_ring_bitwise(dev, M, K, N, gathered, sf):
-    """Split-K UPDATE with every K slice on k_mm_ring (one 128-row group per block, grid.y = the
-    slices) == the k_mm_rows slices bitwise, both within the fp64 bound: x rows 4-B (K = 1433, 1350)
-    and 16-B aligned (1432), a last slice shorter than one 16-k stage (K = 1350: 14 x 96 + 6), two
-    column blocks (N = 200), gathered rows, SF after the slice sum; N = 66 (not a multiple of 4)
-    stays on k_mm_rows."""
+    """Split-K UPDATE with every (128-row group, K slice) a k_mm_ring block (8-deep ring, grid.y =
+    the slices) == the k_mm_rows slices bitwise (same 16-k-multiple slices), both within the fp64
+    bound: x rows 4-B (K = 1433, 1350) and 16-B aligned (1432), K tails inside the last slice, two
+    column blocks (N = 200), gathered rows, SF after the slice sum (float4 sum kernel); N = 66 (not a
+    multiple of 4) stays on k_mm_rows and the scalar sum."""
     assert ops._mm_splits(M, K, N) > 1
     rng = np.random.default_rng(M + K + N)
     x = torch.from_numpy(rng.standard_normal((M + 5, K)).astype(np.float32))
@@ -965,13 +825,11 @@ def test_update_mm_split_ring_bitwise(dev, M, K, N, gathered, sf):
     idd = None if idx is None else idx.to(dev)
     outs = []
     try:
-        ops.set_debug("mm_blaslt", 0)
         for ring in (0, 1):
             ops.set_debug("mm_ring", ring)
             outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
     finally:
         ops.set_debug("mm_ring", 1)
-        ops.set_debug("mm_blaslt", 1)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
     xs = x.numpy()[idx.numpy()] if gathered else x.numpy()[:M]
@@ -1035,12 +893,7 @@ def test_degenerate_graphs_every_op(dev, n):
     assert torch.equal(ops.aggregate(g, x, "src", None, plan=64), torch.zeros(n, F, device=dev))
     acc = x.clone()
     assert torch.equal(ops.aggregate(g, x, "src", None, out=acc, accumulate=True), x)
-    for fuse in (0, 1):
-        ops.set_debug("seg_fuse", fuse)
-        try:
-            assert torch.equal(ops.aggregate_blocked(g, x, w8, blocks=4), torch.zeros(n, F, device=dev))
-        finally:
-            ops.set_debug("seg_fuse", 0)
+    assert torch.equal(ops.aggregate_blocked(g, x, w8, blocks=4), torch.zeros(n, F, device=dev))
     assert ops.scatter(g, x, "C").shape == (0, F)
     assert torch.equal(ops.gather_add(g, torch.zeros(0, F, device=dev)), torch.zeros(n, F, device=dev))
     assert ops.apply_edge(g, "MUL", None, torch.zeros(0, F, device=dev), "edge", x, "src").shape == (0, F)
