@@ -27,8 +27,8 @@ SIGNATURES = {
     "gta_abi_version": (_i32, []),
     "gta_last_error": (_cp, []),
     "gta_scatter": (_i32, [_i32, _vp, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _i64, _vp]),
-    "gta_aggregate": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _vp, _i64, _i32,
-                             _vp, _i64, _vp, _vp]),
+    "gta_aggregate": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _i64,
+                             _i32, _vp, _i64, _vp, _vp]),
     "gta_aggregate_plan_bytes": (_i64, [_i64, _i64, _i64]),
     "gta_aggregate_plan_build": (_i32, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
     "gta_aggregate_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
@@ -44,7 +44,7 @@ SIGNATURES = {
     "gta_apply_edge": (_i32, [_i32, _i32, _vp, _vp, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp,
                               _i64, _vp]),
     "gta_edge_softmax": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp]),
-    "gta_apply_node": (_i32, [_i32, _i32, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp]),
+    "gta_apply_node": (_i32, [_i32, _i32, _i64, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _vp, _i64, _vp]),
     "gta_update_mm": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
     "gta_update_mm_t": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
     "gta_update_mm_t_splits": (_i64, [_i64, _i64, _i64, _i32]),

@@ -4,7 +4,8 @@
   gat8-flickr  GAT layer 1 on Flickr (89,250 nodes / 899,756 edges), 8 heads, F=500
   sage-reddit  GraphSAGE-mean layer 1 on Reddit (232,965 / 114,615,892), F=602
   gin-products GIN layer 1 on an ogbn-products-shaped CSR (2,449,029 / 123,718,280), F=100,
-               both MLP GEMMs in bf16 on MFMA (fp32 accumulation)
+               node features stored in bf16 (200-B rows: BASELINE.md's "4 + 200 B (bf16)" per
+               edge), both MLP GEMMs in bf16 on MFMA, every sum in fp32
   gat8-reddit  GAT layer 1 on Reddit, 8 heads, F=602: not a BASELINE config; the full layer
                around the metric's aggregate (edge-softmax, GEMMs, aggregate, ELU)
   sgc/dgn/pna-flickr, gat8-flickr-trans
@@ -43,7 +44,8 @@ def build(name, device, seed=0, graph=None):
         meta = meta or lay.metadata
         layers.append(lay)
     dtype_w = torch.bfloat16 if c.get("bf16") else torch.float32
-    tensors = [workloads.make_tensors(lay.opgraph, g, c["network"], seed=seed + k, dtype_w=dtype_w)
+    tensors = [workloads.make_tensors(lay.opgraph, g, c["network"], seed=seed + k, dtype_w=dtype_w,
+                                      dtype_x=dtype_w if k == 0 else torch.float32)
                for k, lay in enumerate(layers)]
     return layers, g, tensors
 

@@ -101,6 +101,25 @@ template <> struct Vec<4> {
   }
 };
 
+// Vec<VW> from VW consecutive elements of a float or bf16 row (bf16 widened exactly: bits << 16)
+template <int VW>
+__device__ __forceinline__ void load_row(Vec<VW>& o, const float* p) { o.load(p); }
+template <int VW>
+__device__ __forceinline__ void load_row(Vec<VW>& o, const uint16_t* p) {
+  if constexpr (VW == 4) {
+    const uint2 u = *reinterpret_cast<const uint2*>(p);
+    o.v[0] = __uint_as_float(u.x << 16); o.v[1] = __uint_as_float(u.x & 0xffff0000u);
+    o.v[2] = __uint_as_float(u.y << 16); o.v[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else if constexpr (VW == 2) {
+    const uint32_t u = *reinterpret_cast<const uint32_t*>(p);
+    o.v[0] = __uint_as_float(u << 16); o.v[1] = __uint_as_float(u & 0xffff0000u);
+  } else {
+    o.v[0] = __uint_as_float(static_cast<uint32_t>(*p) << 16);
+  }
+}
+__device__ __forceinline__ float load_elem(const float* p) { return *p; }
+__device__ __forceinline__ float load_elem(const uint16_t* p) { return __uint_as_float(static_cast<uint32_t>(*p) << 16); }
+
 __device__ __forceinline__ int wave_id_uniform() {
   return __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
 }
@@ -211,22 +230,19 @@ __global__ void k_plan_fill(const int64_t* __restrict__ indptr, int64_t n_rows, 
 enum { XM_IDX = 0, XM_EDGE = 1 };
 enum { WM_NONE = 0, WM_HEAD = 1, WM_FULL = 2 };
 
-template <bool NT, typename T>
-__device__ __forceinline__ T ld_stream(const T* p) {
-  if constexpr (NT) return __builtin_nontemporal_load(p);
-  else return *p;
-}
-
-template <int LPE, int VW, int NV, int XMODE, int WMODE, bool NT>
+// TX: the gathered rows' element type (float, or bf16 as uint16_t: widened exactly, fp32 sums)
+template <int LPE, int VW, int NV, int XMODE, int WMODE, typename TX = float>
 __global__ void __launch_bounds__(kBlock)
 k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
             PlanView plan, int use_plan, int64_t chunk, int x_is_row,
-            const float* __restrict__ x, int64_t ldx, int F,
+            const TX* __restrict__ x, int64_t ldx, int F,
             const float* __restrict__ w, int64_t ldw, int gsz,
             const float* __restrict__ row_scale, float* __restrict__ y, int64_t ldy, int accumulate,
             float* __restrict__ partial) {
   constexpr int EPI = kWave / LPE;                 // edges per wave instruction
-  constexpr int UR = (16 / (NV * VW)) < 2 ? 2 : ((16 / (NV * VW)) > 8 ? 8 : 16 / (NV * VW));
+  // row loads in flight per lane: ~64 B of each lane's rows per unrolled step
+  constexpr int XB = NV * VW * static_cast<int>(sizeof(TX));
+  constexpr int UR = (64 / XB) < 2 ? 2 : ((64 / XB) > 8 ? 8 : 64 / XB);
   constexpr int STEP = UR * EPI;                    // edges per unrolled step
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t item = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
@@ -270,11 +286,11 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
     // this block's rows are in flight (clamped address: the load is unconditional)
     const bool use_idx = (XMODE == XM_IDX) && !x_is_row;
     int idxv = 0;
-    if (use_idx && eb < ee) idxv = ld_stream<NT>(indices + min(eb + lane, ee - 1));
+    if (use_idx && eb < ee) idxv = indices[min(eb + lane, ee - 1)];
     for (int64_t e0 = eb; e0 < ee; e0 += kWave) {
       const int n = static_cast<int>(min<int64_t>(kWave, ee - e0));
       int idxn = 0;
-      if (use_idx) idxn = ld_stream<NT>(indices + min(e0 + kWave + lane, ee - 1));
+      if (use_idx) idxn = indices[min(e0 + kWave + lane, ee - 1)];
       for (int s = 0; s < n; s += STEP) {
         Vec<VW> xv[UR][NV];
         float wh[UR][NV];
@@ -295,13 +311,13 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
           } else {
             xr = __shfl(idxv, jj);
           }
-          const float* xp = x + xr * ldx;
+          const TX* xp = x + xr * ldx;
 #pragma unroll
-          for (int v = 0; v < NV; ++v) xv[u][v].load(xp + col[v]);
+          for (int v = 0; v < NV; ++v) load_row(xv[u][v], xp + col[v]);
           if (WMODE == WM_HEAD) {
             const float* wp = w + (e0 + jj) * ldw;
 #pragma unroll
-            for (int v = 0; v < NV; ++v) wh[u][v] = ld_stream<NT>(wp + hcol[v]);
+            for (int v = 0; v < NV; ++v) wh[u][v] = wp[hcol[v]];
           } else if (WMODE == WM_FULL) {
             const float* wp = w + (e0 + jj) * ldw;
 #pragma unroll
@@ -1509,8 +1525,9 @@ k_apply_edge_pack(int bin, int sf, const int64_t* __restrict__ indptr, const int
   }
 }
 
+template <typename TA>
 __global__ void __launch_bounds__(kBlock)
-k_apply_node(int bin, int sf, int64_t n, const float* __restrict__ a, int64_t lda, int Fa,
+k_apply_node(int bin, int sf, int64_t n, const TA* __restrict__ a, int64_t lda, int Fa,
              const float* __restrict__ b, int64_t ldb, int Fb, float* __restrict__ out, int64_t ldo, int Fo) {
   const int64_t total = n * Fo;
   const int ga = Fo / Fa, gb = (b != nullptr) ? Fo / Fb : 1;
@@ -1518,7 +1535,7 @@ k_apply_node(int bin, int sf, int64_t n, const float* __restrict__ a, int64_t ld
        t += static_cast<int64_t>(gridDim.x) * blockDim.x) {
     const int64_t i = t / Fo;
     const int c = static_cast<int>(t - i * Fo);
-    float va = a[i * lda + c / ga];
+    float va = load_elem(a + i * lda + c / ga);
     if (b != nullptr) va = bin_apply(bin, va, b[i * ldb + c / gb]);
     out[i * ldo + c] = sf_apply(sf, va);
   }
@@ -1528,13 +1545,15 @@ k_apply_node(int bin, int sf, int64_t n, const float* __restrict__ a, int64_t ld
 // a and out [n, F] with F % 4 == 0 and 16-B rows, b none (BM 0), [n, F] (BM 1) or one value
 // per node b[i * ldb] (BM 2; ldb 0 = one value for all, e.g. GIN's 1 + eps).  One float4 per
 // thread step, 32-bit index math (n * F / 4 < 2^32).
-template <int BM>
+template <int BM, typename TA = float>
 __global__ void __launch_bounds__(kBlock)
-k_apply_node4(int bin, int sf, uint32_t n4, uint32_t F4, const float* __restrict__ a, int64_t lda,
+k_apply_node4(int bin, int sf, uint32_t n4, uint32_t F4, const TA* __restrict__ a, int64_t lda,
               const float* __restrict__ b, int64_t ldb, float* __restrict__ out, int64_t ldo) {
   for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < n4; t += gridDim.x * blockDim.x) {
     const uint32_t i = t / F4, c = (t - i * F4) * 4u;
-    float4 v = *reinterpret_cast<const float4*>(a + i * lda + c);
+    Vec<4> av;
+    load_row(av, a + i * lda + c);
+    float4 v = make_float4(av.v[0], av.v[1], av.v[2], av.v[3]);
     if (BM == 1) {
       const float4 w = *reinterpret_cast<const float4*>(b + i * ldb + c);
       v.x = bin_apply(bin, v.x, w.x); v.y = bin_apply(bin, v.y, w.y);
@@ -2155,6 +2174,21 @@ __device__ __forceinline__ void ds_read16_idx(f32x4& v, uint32_t a, int c) {  //
     default: ds_read16<15 * 1024>(v, a); break;
   }
 }
+__device__ __forceinline__ void ds_read16_kib(f32x4& v, uint32_t a, int c) {  // c: KiB offset < 64 (unrolled)
+  switch (c) {
+#define GTA_DSR(C_) case C_: ds_read16<(C_) * 1024>(v, a); break;
+    GTA_DSR(0) GTA_DSR(1) GTA_DSR(2) GTA_DSR(3) GTA_DSR(4) GTA_DSR(5) GTA_DSR(6) GTA_DSR(7)
+    GTA_DSR(8) GTA_DSR(9) GTA_DSR(10) GTA_DSR(11) GTA_DSR(12) GTA_DSR(13) GTA_DSR(14) GTA_DSR(15)
+    GTA_DSR(16) GTA_DSR(17) GTA_DSR(18) GTA_DSR(19) GTA_DSR(20) GTA_DSR(21) GTA_DSR(22) GTA_DSR(23)
+    GTA_DSR(24) GTA_DSR(25) GTA_DSR(26) GTA_DSR(27) GTA_DSR(28) GTA_DSR(29) GTA_DSR(30) GTA_DSR(31)
+    GTA_DSR(32) GTA_DSR(33) GTA_DSR(34) GTA_DSR(35) GTA_DSR(36) GTA_DSR(37) GTA_DSR(38) GTA_DSR(39)
+    GTA_DSR(40) GTA_DSR(41) GTA_DSR(42) GTA_DSR(43) GTA_DSR(44) GTA_DSR(45) GTA_DSR(46) GTA_DSR(47)
+    GTA_DSR(48) GTA_DSR(49) GTA_DSR(50) GTA_DSR(51) GTA_DSR(52) GTA_DSR(53) GTA_DSR(54) GTA_DSR(55)
+    GTA_DSR(56) GTA_DSR(57) GTA_DSR(58) GTA_DSR(59) GTA_DSR(60) GTA_DSR(61) GTA_DSR(62)
+#undef GTA_DSR
+    default: ds_read16<63 * 1024>(v, a); break;
+  }
+}
 // s_waitcnt vmcnt(n * PS): everything but the last n stages of PS DMA instructions landed (n wave-uniform)
 template <int PS>
 __device__ __forceinline__ void vm_wait_stages(int n) {
@@ -2381,6 +2415,231 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   }
 }
 
+// bf16 MFMA UPDATE with an LDS-DMA ring (GTA_F32_BF16: fp32 x rounded to bf16 as it leaves LDS,
+// bf16 W; GTA_BF16: bf16 x and W) -- the GIN MLP GEMMs [2.45 M x 100].[100 x 128] and
+// [2.45 M x 128].[128 x 128] (`vTCAD/GraphOP/genGraphOP.py:97-108`, applynode MM
+// `template/ISA_defination.yaml:1-31`).  These are HBM-bound streams (x read once, out written
+// once, ~2 GFLOP per GB), so what matters is bytes in flight: x goes global -> LDS by
+// global_load_lds through a D-deep ring of 32-k stages (lane L = 16g + r holds x[row r][k0 + 8g
+// .. +7], its own MFMA fragment: two 16-B pieces for fp32 x, one for bf16), while W^T -- at most
+// SB 32-k steps x BN columns, 32 KiB at K <= 128 -- is staged once per block into LDS in the same
+// fragment layout, zero past K and N.  Per stage: counted vmcnt + raw s_barrier as in k_mm_ring,
+// FR x NT v_mfma_f32_16x16x32_bf16 per wave.  A K tail (K % 32) is one register step with masked
+// loads.  Same k order, the same RNE rounding of x (to_bf16_bits) and the same zero padding as
+// k_mm_rows: results bitwise equal to it.
+template <int NT, int D, int FR, int SB, int PA>
+constexpr int ring_bf_blocks() {
+  return (160 * 1024 / (D * 4 * FR * PA * 1024 + NT * SB * 1024)) > 4 ? 4
+                                                                      : (160 * 1024 / (D * 4 * FR * PA * 1024 + NT * SB * 1024));
+}
+
+template <typename TA, int NT, int D = 3, int FR = 2, int SB = 4>
+__global__ void __launch_bounds__(kBlock, (ring_bf_blocks<NT, D, FR, SB, sizeof(TA) == 4 ? 2 : 1>()))
+k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
+             const uint16_t* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo) {
+  static_assert(NT == 4 || NT == 8, "column fragments");
+  static_assert(FR == 1 || FR == 2, "one or two A fragments per wave");
+  static_assert(D >= 3 && D <= 8, "ring depth");
+  constexpr int KS = 32, BN = 16 * NT, GR = 64 * FR;
+  constexpr int PA = sizeof(TA) == 4 ? 2 : 1;  // 16-B DMA pieces per lane per A fragment
+  constexpr int FRAG = PA * 1024, STAGE = 4 * FR * FRAG;
+  constexpr int PER_STAGE = FR * PA;           // DMA instructions per wave per stage
+  __shared__ __attribute__((aligned(16))) char lds[D * STAGE];
+  __shared__ __attribute__((aligned(16))) char bres[NT * SB * 1024];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = wave_id_uniform();
+  const int g = lane >> 4, r16 = lane & 15;
+  const int ncb = (N + BN - 1) / BN;
+  const int n0 = static_cast<int>(blockIdx.x % ncb) * BN;
+  const int64_t grp0 = blockIdx.x / ncb, gstep = gridDim.x / ncb;
+  const int64_t n_groups = (M + GR - 1) / GR;
+  const int64_t my_groups = grp0 < n_groups ? (n_groups - grp0 + gstep - 1) / gstep : 0;
+  const int S = K / KS;
+  const int64_t T = my_groups * S;
+  // W^T resident: fragment (c, s) at bres + (c * SB + s) KiB, lane L's 8 bf16 of row n0 + 16c + r16,
+  // k = 32s + 8g .. +7 (zeros past K and N)
+  for (int e = threadIdx.x; e < NT * SB * kWave; e += kBlock) {
+    const int L = e & (kWave - 1), f = e >> 6, c = f / SB, s = f - c * SB;
+    const int n = n0 + 16 * c + (L & 15), k = 32 * s + 8 * (L >> 4);
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (n < N && k < K) {
+      const uint16_t* p = wt + static_cast<int64_t>(n) * ldwt + k;
+      if (k + 8 <= K && aligned(p, 16)) {
+        v = *reinterpret_cast<const uint4*>(p);
+      } else {
+        uint16_t tmp[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) tmp[q] = (k + q < K) ? p[q] : static_cast<uint16_t>(0);
+        v = *reinterpret_cast<const uint4*>(tmp);
+      }
+    }
+    *reinterpret_cast<uint4*>(bres + f * 1024 + L * 16) = v;
+  }
+  auto a_row = [&](int64_t j, int i) __attribute__((always_inline)) -> const TA* {
+    const int64_t m = min<int64_t>((grp0 + j * gstep) * GR + wv * (16 * FR) + 16 * i + r16, M - 1);
+    return x + (row_idx ? static_cast<int64_t>(row_idx[m]) : m) * ldx;
+  };
+  const TA* asrc[FR];
+  int64_t asrc_j = -1, iss_j = 0;
+  int iss_s = 0, iss_slot = 0;
+  auto issue = [&]() __attribute__((always_inline)) {
+    const int64_t j = iss_j;
+    const int k = iss_s * KS;
+    if (j != asrc_j) {
+#pragma unroll
+      for (int i = 0; i < FR; ++i) asrc[i] = a_row(j, i) + 8 * g;
+      asrc_j = j;
+    }
+    char* base = lds + iss_slot * STAGE;
+    iss_slot = iss_slot + 1 == D ? 0 : iss_slot + 1;
+    if (++iss_s == S) {
+      iss_s = 0;
+      ++iss_j;
+    }
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+      for (int p = 0; p < PA; ++p)
+        __builtin_amdgcn_global_load_lds(const_cast<TA*>(asrc[i] + k + 4 * p),
+                                         GTA_TO_LDS(base + (wv * FR + i) * FRAG + p * 1024), 16, 0, 0);
+  };
+  f32x4 acc[FR][NT];
+  auto zero_acc = [&]() __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+      for (int c = 0; c < NT; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  };
+  // 8 values of one lane's fragment -> the bf16x8 MFMA operand (fp32: RNE as k_mm_rows rounds)
+  auto pack = [&](const float (&v)[8]) __attribute__((always_inline)) {
+    bf16x8 r;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) r[q] = static_cast<short>(to_bf16_bits(v[q]));
+    return r;
+  };
+  auto mma_step = [&](const bf16x8 (&a8)[FR], int s) __attribute__((always_inline)) {
+    const uint32_t sb = GTA_LDS_ADDR(bres + s * 1024) + static_cast<uint32_t>(lane) * 16u;
+    f32x4 b4[NT];
+#pragma unroll
+    for (int c = 0; c < NT; ++c) ds_read16_kib(b4[c], sb, c * SB);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(b4[c]));
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      const bf16x8 b8 = __builtin_bit_cast(bf16x8, b4[c]);
+#pragma unroll
+      for (int i = 0; i < FR; ++i) acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8[i], b8, acc[i][c], 0, 0, 0);
+    }
+  };
+  const bool vstore = ldo % 4 == 0 && aligned(out, 16);
+  auto epilogue = [&](int64_t j) __attribute__((always_inline)) {
+    const int64_t mw = (grp0 + j * gstep) * GR + wv * (16 * FR);
+    if (vstore) {
+      const int p = r16 & 3, q = r16 >> 2;
+#pragma unroll
+      for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int c = 0; c < NT; ++c) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = sf_apply(sf, acc[i][c][r]);
+#pragma unroll
+          for (int m2 = 0; m2 < 2; ++m2) {
+            const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
+            const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2 + 1]), 0xB1, 0xF, 0xF, false));
+            if (p & 1) v[2 * m2] = sb; else v[2 * m2 + 1] = sa;
+          }
+#pragma unroll
+          for (int m2 = 0; m2 < 2; ++m2) {
+            const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2]), 0x4E, 0xF, 0xF, false));
+            const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2 + 2]), 0x4E, 0xF, 0xF, false));
+            if (p & 2) v[m2] = sb; else v[m2 + 2] = sa;
+          }
+          const int64_t m = mw + 16 * i + 4 * g + p;
+          const int n = n0 + 16 * c + 4 * q;
+          if (m < M) {
+            if (n + 3 < N) {
+              *reinterpret_cast<float4*>(out + m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (n + r < N) out[m * ldo + n + r] = v[r];
+            }
+          }
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int c = 0; c < NT; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t m = mw + 16 * i + 4 * g + r;
+            const int n = n0 + 16 * c + r16;
+            if (m < M && n < N) out[m * ldo + n] = sf_apply(sf, acc[i][c][r]);
+          }
+    }
+  };
+  auto tail = [&](int64_t j) __attribute__((always_inline)) {  // k in [32 S, K): masked register step
+    const int k0 = S * KS + 8 * g;
+    bf16x8 a8[FR];
+#pragma unroll
+    for (int i = 0; i < FR; ++i) {
+      const TA* p = a_row(j, i) + k0;
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] = (k0 + q < K) ? load_elem(p + q) : 0.f;
+      a8[i] = pack(v);
+    }
+    mma_step(a8, S);
+  };
+  zero_acc();
+  __syncthreads();  // W^T resident before any fragment read
+#pragma unroll
+  for (int p = 0; p + 1 < D; ++p)
+    if (p < T) issue();
+  int64_t t = 0;
+  int slot = 0;
+  for (int64_t j = 0; j < my_groups; ++j) {
+    for (int s = 0; s < S; ++s, ++t, slot = slot + 1 == D ? 0 : slot + 1) {
+      const int64_t later = T - 1 - t;
+      vm_wait_stages<PER_STAGE>(static_cast<int>(later < D - 2 ? later : D - 2));
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+      if (t + D - 1 < T) issue();
+      const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * FRAG) + static_cast<uint32_t>(lane) * 16u;
+      f32x4 a4[FR][PA];
+#pragma unroll
+      for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int p = 0; p < PA; ++p) ds_read16_idx(a4[i][p], sa, i * PA + p);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int p = 0; p < PA; ++p) asm volatile("" : "+v"(a4[i][p]));
+      bf16x8 a8[FR];
+#pragma unroll
+      for (int i = 0; i < FR; ++i) {
+        if constexpr (PA == 2) {
+          const float v[8] = {a4[i][0][0], a4[i][0][1], a4[i][0][2], a4[i][0][3],
+                              a4[i][1][0], a4[i][1][1], a4[i][1][2], a4[i][1][3]};
+          a8[i] = pack(v);
+        } else {
+          a8[i] = __builtin_bit_cast(bf16x8, a4[i][0]);
+        }
+      }
+      mma_step(a8, s);
+    }
+    if (K % KS) tail(j);
+    epilogue(j);
+    zero_acc();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
 // out[m, n] = sf(sum_s ws[s][m][n]) in slice order (split-K UPDATE; ws slices are [M, N] dense).
 // Float4 form: four consecutive columns per thread, the slices' loads issued four at a time, the
 // adds in slice order (bitwise equal to the scalar form).
@@ -2447,46 +2706,55 @@ k_tile_nnz(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indic
 struct AggArgs {
   const int64_t* indptr; const int32_t* indices; int64_t n_rows;
   PlanView plan; int use_plan; int64_t chunk; int x_is_row;
-  const float* x; int64_t ldx; int F;
+  const void* x; int64_t ldx; int F;
   const float* w; int64_t ldw; int gsz;
   const float* row_scale; float* y; int64_t ldy; int accumulate; float* partial;
 };
 
-template <int LPE, int VW, int NV, int XM, int WM, bool NT>
+template <int LPE, int VW, int NV, int XM, int WM, typename TX>
 void launch_agg(const AggArgs& a, int64_t n_items_bound, hipStream_t s) {
   const int64_t blocks = (n_items_bound + kWavesPerBlock - 1) / kWavesPerBlock;
-  k_aggregate<LPE, VW, NV, XM, WM, NT><<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
-      a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, a.x_is_row, a.x, a.ldx, a.F, a.w, a.ldw, a.gsz,
-      a.row_scale, a.y, a.ldy, a.accumulate, a.partial);
+  k_aggregate<LPE, VW, NV, XM, WM, TX><<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
+      a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, a.x_is_row, static_cast<const TX*>(a.x), a.ldx, a.F,
+      a.w, a.ldw, a.gsz, a.row_scale, a.y, a.ldy, a.accumulate, a.partial);
 }
 
+// (non-temporal index/weight loads measured +3 %: plain loads throughout)
+// bf16 rows: indexed gathers (x_mode SRC / DST) without or with head weights only
 template <int LPE, int VW, int NV, int XM>
-bool dispatch_w(int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
-  // (non-temporal index/weight loads measured +3 %: plain loads throughout)
+bool dispatch_w(int wm, bool bf, const AggArgs& a, int64_t nb, hipStream_t s) {
+  if (bf) {
+    if constexpr (XM == XM_IDX) {
+      if (wm == WM_NONE) { launch_agg<LPE, VW, NV, XM, WM_NONE, uint16_t>(a, nb, s); return true; }
+      if (wm == WM_HEAD) { launch_agg<LPE, VW, NV, XM, WM_HEAD, uint16_t>(a, nb, s); return true; }
+    }
+    return false;
+  }
   switch (wm) {
-    case WM_NONE: launch_agg<LPE, VW, NV, XM, WM_NONE, false>(a, nb, s); return true;
-    case WM_HEAD: launch_agg<LPE, VW, NV, XM, WM_HEAD, false>(a, nb, s); return true;
-    case WM_FULL: launch_agg<LPE, VW, NV, XM, WM_FULL, false>(a, nb, s); return true;
+    case WM_NONE: launch_agg<LPE, VW, NV, XM, WM_NONE, float>(a, nb, s); return true;
+    case WM_HEAD: launch_agg<LPE, VW, NV, XM, WM_HEAD, float>(a, nb, s); return true;
+    case WM_FULL: launch_agg<LPE, VW, NV, XM, WM_FULL, float>(a, nb, s); return true;
   }
   return false;
 }
 
 template <int LPE, int VW, int NV>
-bool dispatch_x(int xm, int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
-  return xm == XM_EDGE ? dispatch_w<LPE, VW, NV, XM_EDGE>(wm, a, nb, s) : dispatch_w<LPE, VW, NV, XM_IDX>(wm, a, nb, s);
+bool dispatch_x(int xm, int wm, bool bf, const AggArgs& a, int64_t nb, hipStream_t s) {
+  return xm == XM_EDGE ? dispatch_w<LPE, VW, NV, XM_EDGE>(wm, bf, a, nb, s)
+                       : dispatch_w<LPE, VW, NV, XM_IDX>(wm, bf, a, nb, s);
 }
 
 template <int VW>
-bool dispatch_lpe(int lpe, int nv, int xm, int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
+bool dispatch_lpe(int lpe, int nv, int xm, int wm, bool bf, const AggArgs& a, int64_t nb, hipStream_t s) {
   switch (lpe) {
     case 64:
-      if (nv == 1) return dispatch_x<64, VW, 1>(xm, wm, a, nb, s);
-      if (nv == 2) return dispatch_x<64, VW, 2>(xm, wm, a, nb, s);
-      return dispatch_x<64, VW, 4>(xm, wm, a, nb, s);
-    case 32: return dispatch_x<32, VW, 1>(xm, wm, a, nb, s);
-    case 16: return dispatch_x<16, VW, 1>(xm, wm, a, nb, s);
-    case 8: return dispatch_x<8, VW, 1>(xm, wm, a, nb, s);
-    default: return dispatch_x<4, VW, 1>(xm, wm, a, nb, s);
+      if (nv == 1) return dispatch_x<64, VW, 1>(xm, wm, bf, a, nb, s);
+      if (nv == 2) return dispatch_x<64, VW, 2>(xm, wm, bf, a, nb, s);
+      return dispatch_x<64, VW, 4>(xm, wm, bf, a, nb, s);
+    case 32: return dispatch_x<32, VW, 1>(xm, wm, bf, a, nb, s);
+    case 16: return dispatch_x<16, VW, 1>(xm, wm, bf, a, nb, s);
+    case 8: return dispatch_x<8, VW, 1>(xm, wm, bf, a, nb, s);
+    default: return dispatch_x<4, VW, 1>(xm, wm, bf, a, nb, s);
   }
 }
 
@@ -2510,6 +2778,7 @@ struct Tuning {
   int esm_lane = 1;        // edge-per-lane edge-softmax when H in {4,8,16} and rows are 16-B aligned
   int mm_ring = 1;         // fp32 UPDATE on k_mm_ring (LDS-DMA ring) instead of k_mm_rows
   int mm_ring_fr = 0;      // k_mm_ring A fragments per wave: 2 = 128-row groups, 1 = 64-row groups, 0 = auto
+  int mm_ring_depth = 0;   // k_mm_ring stages: 0 = auto (by blocks per CU), else 3, 4 or 8
   int mm_prefetch = 1;     // k_mm_rows A prefetch: 1 auto, 2 always, 0 never
   int64_t mm_split = -1;   // UPDATE K slices: -1 auto, 0 = never split, n = n slices
 };
@@ -2567,6 +2836,7 @@ const Knob* find_knob(const char* key) {
       {"esm_lane", &Tuning::esm_lane, nullptr},
       {"mm_ring", &Tuning::mm_ring, nullptr},
       {"mm_ring_fr", &Tuning::mm_ring_fr, nullptr},
+      {"mm_ring_depth", &Tuning::mm_ring_depth, nullptr},
       {"mm_prefetch", &Tuning::mm_prefetch, nullptr},
       {"mm_split", nullptr, &Tuning::mm_split},
   };
@@ -2664,13 +2934,18 @@ int gta_aggregate_plan_build(const int64_t* indptr, int64_t n_rows, int64_t nnz,
 }
 
 int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int x_mode,
-                     const float* x, int64_t ldx, int64_t F, const float* w, int64_t ldw, int64_t heads,
+                  const void* x, int64_t ldx, int64_t F, int x_dtype, const float* w, int64_t ldw, int64_t heads,
                   const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
                   int64_t plan_chunk, void* workspace, void* stream) {
   const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n_rows < 0 || nnz < 0 || F <= 0) return fail(GTA_ERR_ARG, "aggregate: bad sizes");
   if (x_mode != GTA_IDX_EDGE && x_mode != GTA_IDX_SRC && x_mode != GTA_IDX_DST)
     return fail(GTA_ERR_ARG, "aggregate: bad x_mode");
+  if (x_dtype != GTA_F32 && x_dtype != GTA_BF16) return fail(GTA_ERR_ARG, "aggregate: x_dtype must be F32 or BF16");
+  const bool bf = x_dtype == GTA_BF16;
+  const int xe = bf ? 2 : 4;  // bytes per x element
+  if (bf && (x_mode == GTA_IDX_EDGE || (w && heads == F)))
+    return fail(GTA_ERR_UNSUPPORTED, "aggregate: bf16 rows are gathered by index (SRC / DST) with head weights or none");
   if (F > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "aggregate: F too large");
   if (n_rows == 0) return GTA_OK;
   // with no edges, indices / edge operands are never read (may be NULL); every row gets 0
@@ -2689,7 +2964,7 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
   const int xm = (x_mode == GTA_IDX_EDGE) ? XM_EDGE : XM_IDX;
   // widest vector that keeps every access aligned
   auto ok_vw = [&](int vw) {
-    if (F % vw || ldx % vw || ldy % vw || !aligned(x, 4 * vw) || !aligned(y, 4 * vw)) return false;
+    if (F % vw || ldx % vw || ldy % vw || !aligned(x, xe * vw) || !aligned(y, 4 * vw)) return false;
     if (wm == WM_HEAD && gsz % vw) return false;
     if (wm == WM_FULL && (ldw % vw || !aligned(w, 4 * vw))) return false;
     return true;
@@ -2699,7 +2974,7 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
   // one edge per wave instruction (LPE = 64, wave-uniform row base) whenever the
   // row fills 64 lanes at >= 8 B/lane: measured 3 % faster than two edges per
   // instruction at float4 for F = 128 (profiles/r01_agg_sweep_1.json)
-  if (vw == 4 && F < 4 * kWave && F >= 2 * kWave && ok_vw(2)) vw = 2;
+  if (!bf && vw == 4 && F < 4 * kWave && F >= 2 * kWave && ok_vw(2)) vw = 2;
   const int64_t lanes = (F + vw - 1) / vw;
   int lpe, nv = 1;
   if (lanes >= kWave) {
@@ -2709,8 +2984,8 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
     lpe = 4;
     while (lpe < lanes) lpe <<= 1;
   }
-  if (tuning().force_lpe == 32 && F == 128 && ok_vw(4)) { lpe = 32; vw = 4; nv = 1; }
-  if (tuning().force_lpe == 64 && F == 128 && ok_vw(2)) { lpe = 64; vw = 2; nv = 1; }
+  if (!bf && tuning().force_lpe == 32 && F == 128 && ok_vw(4)) { lpe = 32; vw = 4; nv = 1; }
+  if (!bf && tuning().force_lpe == 64 && F == 128 && ok_vw(2)) { lpe = 64; vw = 2; nv = 1; }
 
   AggArgs a{};
   a.indptr = indptr; a.indices = indices; a.n_rows = n_rows;
@@ -2728,15 +3003,15 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
   bool ok = false;
   // lean path: one edge per instruction exactly filling the wave, SpMM form
   int gl = (wm == WM_HEAD) ? gsz / vw : 0;
-  const bool lean_shape = tuning().agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
+  const bool lean_shape = !bf && tuning().agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
                           !a.x_is_row && wm != WM_FULL && (wm == WM_NONE || gl == 4 || gl == 8 || gl == 16);
   if (lean_shape) {
     const int64_t blocks = (bound + kWavesPerBlock - 1) / kWavesPerBlock;
     const dim3 grid(static_cast<unsigned>(blocks)), blk(kBlock);
 #define GTA_LEAN(VW_, GL_)                                                                                   \
   k_agg_lean<VW_, GL_><<<grid, blk, 0, s>>>(a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, \
-                                            a.x, a.ldx, a.F, a.w, a.ldw, a.row_scale, a.y, a.ldy, a.accumulate, \
-                                            a.partial)
+                                            static_cast<const float*>(a.x), a.ldx, a.F, a.w, a.ldw, a.row_scale, \
+                                            a.y, a.ldy, a.accumulate, a.partial)
     if (vw == 2) {
       if (gl == 0) GTA_LEAN(2, 0); else if (gl == 4) GTA_LEAN(2, 4); else if (gl == 8) GTA_LEAN(2, 8); else GTA_LEAN(2, 16);
     } else if (vw == 4) {
@@ -2748,9 +3023,9 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
     ok = true;
   }
   if (!ok) switch (vw) {
-    case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, a, bound, s); break;
-    case 2: ok = dispatch_lpe<2>(lpe, nv, xm, wm, a, bound, s); break;
-    default: ok = dispatch_lpe<1>(lpe, nv, xm, wm, a, bound, s); break;
+    case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, bf, a, bound, s); break;
+    case 2: ok = dispatch_lpe<2>(lpe, nv, xm, wm, bf, a, bound, s); break;
+    default: ok = dispatch_lpe<1>(lpe, nv, xm, wm, bf, a, bound, s); break;
   }
   if (!ok) return fail(GTA_ERR_UNSUPPORTED, "aggregate: no kernel variant");
   GTA_LAUNCHED("k_aggregate");
@@ -3005,8 +3280,8 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
 int gta_gather_add(const int64_t* indptr, int64_t n_rows, int64_t nnz, const float* xe, int64_t ldxe, int64_t F,
                    float* y, int64_t ldy, int accumulate, void* stream) {
   const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
-  return gta_aggregate(indptr, nullptr, n_rows, nnz, GTA_IDX_EDGE, xe, ldxe, F, nullptr, 0, 0, nullptr, y, ldy,
-                          accumulate, nullptr, 0, nullptr, stream);
+  return gta_aggregate(indptr, nullptr, n_rows, nnz, GTA_IDX_EDGE, xe, ldxe, F, GTA_F32, nullptr, 0, 0, nullptr, y,
+                       ldy, accumulate, nullptr, 0, nullptr, stream);
 }
 
 int gta_scatter(int dir, const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, const void* x,
@@ -3095,30 +3370,41 @@ int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indice
   return GTA_OK;
 }
 
-int gta_apply_node(int bin, int sf, int64_t n, const float* a, int64_t lda, int64_t Fa, const float* b, int64_t ldb,
-                   int64_t Fb, float* out, int64_t ldo, void* stream) {
+int gta_apply_node(int bin, int sf, int64_t n, const void* a, int64_t lda, int64_t Fa, int a_dtype, const float* b,
+                   int64_t ldb, int64_t Fb, float* out, int64_t ldo, void* stream) {
   const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n < 0 || Fa <= 0) return fail(GTA_ERR_ARG, "apply_node: bad sizes");
+  if (a_dtype != GTA_F32 && a_dtype != GTA_BF16) return fail(GTA_ERR_ARG, "apply_node: a_dtype must be F32 or BF16");
   if (n == 0) return GTA_OK;
   if (!a || !out) return fail(GTA_ERR_ARG, "apply_node: bad arguments");
+  const bool bf = a_dtype == GTA_BF16;
+  const float* af = static_cast<const float*>(a);
+  const uint16_t* ah = static_cast<const uint16_t*>(a);
   int64_t Fo;
   if (check_bcast(Fa, Fb, b != nullptr, &Fo)) return fail(GTA_ERR_ARG, "apply_node: widths must divide");
   if (n == 0) return GTA_OK;
   const int64_t total = n * Fo;
   const int bm = !b ? 0 : (Fb == Fo ? 1 : (Fb == 1 ? 2 : -1));
   if (tuning().apply_node_vec && bm >= 0 && Fa == Fo && Fo % 4 == 0 && total / 4 < (int64_t(1) << 32) && lda % 4 == 0 &&
-      ldo % 4 == 0 && aligned(a, 16) && aligned(out, 16) && (bm != 1 || (ldb % 4 == 0 && aligned(b, 16)))) {
+      ldo % 4 == 0 && aligned(a, bf ? 8 : 16) && aligned(out, 16) && (bm != 1 || (ldb % 4 == 0 && aligned(b, 16)))) {
     const uint32_t n4 = static_cast<uint32_t>(total / 4), F4 = static_cast<uint32_t>(Fo / 4);
     const dim3 g(static_cast<unsigned>(std::min<int64_t>((n4 + kBlock - 1) / kBlock, 256 * 16))), blk(kBlock);
-    if (bm == 0) k_apply_node4<0><<<g, blk, 0, S(stream)>>>(bin, sf, n4, F4, a, lda, b, ldb, out, ldo);
-    else if (bm == 1) k_apply_node4<1><<<g, blk, 0, S(stream)>>>(bin, sf, n4, F4, a, lda, b, ldb, out, ldo);
-    else k_apply_node4<2><<<g, blk, 0, S(stream)>>>(bin, sf, n4, F4, a, lda, b, ldb, out, ldo);
+#define GTA_AN4(BM_)                                                                                     \
+  if (bf) k_apply_node4<BM_, uint16_t><<<g, blk, 0, S(stream)>>>(bin, sf, n4, F4, ah, lda, b, ldb, out, ldo); \
+  else k_apply_node4<BM_><<<g, blk, 0, S(stream)>>>(bin, sf, n4, F4, af, lda, b, ldb, out, ldo)
+    if (bm == 0) { GTA_AN4(0); } else if (bm == 1) { GTA_AN4(1); } else { GTA_AN4(2); }
+#undef GTA_AN4
     GTA_LAUNCHED("k_apply_node4");
     return GTA_OK;
   }
   const int64_t blocks = std::min<int64_t>((total + kBlock - 1) / kBlock, 256 * 16);
-  k_apply_node<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, S(stream)>>>(
-      bin, sf, n, a, lda, static_cast<int>(Fa), b, ldb, static_cast<int>(Fb), out, ldo, static_cast<int>(Fo));
+  const dim3 g(static_cast<unsigned>(blocks));
+  if (bf)
+    k_apply_node<uint16_t><<<g, dim3(kBlock), 0, S(stream)>>>(bin, sf, n, ah, lda, static_cast<int>(Fa), b, ldb,
+                                                              static_cast<int>(Fb), out, ldo, static_cast<int>(Fo));
+  else
+    k_apply_node<float><<<g, dim3(kBlock), 0, S(stream)>>>(bin, sf, n, af, lda, static_cast<int>(Fa), b, ldb,
+                                                           static_cast<int>(Fb), out, ldo, static_cast<int>(Fo));
   GTA_LAUNCHED("k_apply_node");
   return GTA_OK;
 }
@@ -3270,9 +3556,41 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
       const int64_t per_cu = nt == 8 ? (fr == 1 ? 4 : 3) : 4;  // ring_blocks(NT, 3, FR)
       blocks = std::min(n_grp, std::max<int64_t>(1, 256 * per_cu / ncb)) * ncb;
     }
+    const int dk = tuning().mm_ring_depth;
+    if (dk == 3 || dk == 4 || dk == 8) {  // forced depth: a persistent grid of what that ring's LDS allows
+      const int64_t per_cu = dk == 8 ? 1 : dk == 4 ? (nt == 8 && fr == 2 ? 2 : 3) : (nt == 8 ? (fr == 1 ? 4 : 3) : 4);
+      D = dk;
+      blocks = std::min(n_grp, std::max<int64_t>(1, 256 * per_cu / ncb)) * ncb;
+    }
     launch_ring(nt, D, fr, dim3(static_cast<unsigned>(blocks)), S(stream), static_cast<const float*>(x), ldx, row_idx, M,
                 static_cast<int>(K), static_cast<const float*>(wt), ldwt, static_cast<int>(N), sf, out, ldo, 0, 0);
     GTA_LAUNCHED("k_mm_ring");
+    return GTA_OK;
+  }
+  if (dtype != GTA_F32 && tuning().mm_ring && nt >= 4 && K <= 256 &&
+      (dtype == GTA_F32_BF16 ? aligned(x, 4) : (aligned(x, 16) && ldx % 8 == 0))) {
+    // bf16 MFMA with the x ring (fp32 x: 64-row groups, 6 stages, two blocks per CU; bf16 x: the
+    // same stages hold twice the k) and W^T resident in LDS; mm_ring_fr = 2: 128-row groups, 3 stages
+    const int fr = tuning().mm_ring_fr == 2 ? 2 : 1;
+    const int sb = K <= 128 ? 4 : 8;
+    const int64_t n_grp = fr == 1 ? (M + 63) / 64 : groups;
+    const int64_t per_cu = 2;
+    const int64_t blocks = std::min(n_grp, std::max<int64_t>(1, 256 * per_cu / ncb)) * ncb;
+    const dim3 gr(static_cast<unsigned>(blocks));
+#define GTA_RBF(TA_, NT_, D_, FR_, SB_)                                                                        \
+  k_mm_ring_bf<TA_, NT_, D_, FR_, SB_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const TA_*>(x), ldx, row_idx, M, \
+                                                                          static_cast<int>(K),                       \
+                                                                          static_cast<const uint16_t*>(wt), ldwt,    \
+                                                                          static_cast<int>(N), sf, out, ldo)
+#define GTA_RBF_F(TA_, NT_, SB_) \
+  if (fr == 2) GTA_RBF(TA_, NT_, 3, 2, SB_); else GTA_RBF(TA_, NT_, 6, 1, SB_)
+#define GTA_RBF_S(TA_, NT_) if (sb == 4) { GTA_RBF_F(TA_, NT_, 4); } else { GTA_RBF_F(TA_, NT_, 8); }
+    if (dtype == GTA_F32_BF16) { if (nt == 8) { GTA_RBF_S(float, 8); } else { GTA_RBF_S(float, 4); } }
+    else { if (nt == 8) { GTA_RBF_S(uint16_t, 8); } else { GTA_RBF_S(uint16_t, 4); } }
+#undef GTA_RBF_S
+#undef GTA_RBF_F
+#undef GTA_RBF
+    GTA_LAUNCHED("k_mm_ring_bf");
     return GTA_OK;
   }
   const int64_t per_cu = 8;
@@ -3329,7 +3647,8 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
     // every (128-row group, K slice) on its own block, one per CU with an 8-deep ring (all stages of a
     // slice in flight from the start), then the ordered slice sum.  GCN Cora's [2708 x 1433].[1433 x 128]:
     // 22 groups x 10 slices of 144 k
-    launch_ring(nt, 8, 2, dim3(static_cast<unsigned>(groups * ncb), static_cast<unsigned>(nsl)), s,
+    const int dk = tuning().mm_ring_depth;
+    launch_ring(nt, dk == 3 || dk == 4 ? dk : 8, 2, dim3(static_cast<unsigned>(groups * ncb), static_cast<unsigned>(nsl)), s,
                 static_cast<const float*>(x), ldx, row_idx, M, static_cast<int>(K), static_cast<const float*>(wt), ldwt,
                 static_cast<int>(N), GTA_SF_NONE, ws, N, static_cast<int>(ks), M * N);
     GTA_LAUNCHED("k_mm_ring<split>");

@@ -227,8 +227,8 @@ class Executor:
             v = self._materialize_deferred(v)
         if isinstance(v, EdgeT):
             return v.t, "edge", False
-        if isinstance(v, Scat):
-            return v.t, v.mode, False
+        if isinstance(v, Scat):  # (a bf16 node table is widened: the element-wise kernels are fp32)
+            return (v.t if v.t.dtype == torch.float32 else v.t.float()), v.mode, False
         if isinstance(v, tuple) and v[0] == "row":
             return v[1], "edge", True
         raise TypeError(f"not an edge operand: {type(v).__name__}")
@@ -242,7 +242,8 @@ class Executor:
                 raise MemoryError(f"stream materialises a {nbytes / 2**30:.0f} GiB edge tensor (scatter not fused "
                                   "with its consumer); choose a fusion partition that keeps it virtual")
             self._count(self.graph.nnz * v.t.shape[1] * 4 * 2 + self.graph.nnz * 4)
-            return ops.scatter(self.graph, v.t, "C" if v.mode == "src" else "R")
+            t = v.t if v.t.dtype == torch.float32 else v.t.float()  # edge tensors are fp32 (exact widening)
+            return ops.scatter(self.graph, t, "C" if v.mode == "src" else "R")
         if isinstance(v, Deferred):
             return self._materialize_deferred(v).t
         raise TypeError(type(v).__name__)

@@ -98,13 +98,17 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
     """y[i] (+)= row_scale[i] * sum_{e in row i} w(e) * x[idx(e)]  (K6/K7/K2).
 
     x_mode: "src" (x is [N_src, F], fused scatter C), "dst" (fused scatter R),
-            "edge" (x is an edge tensor [E, F]).
+            "edge" (x is an edge tensor [E, F]).  x float32, or bfloat16 for "src" / "dst" with
+            head weights or none (rows widened exactly, fp32 sums).
     w: None, or [E, H] with H | F (H == F: full-width edge weights).
     plan: None (one wavefront per row), an AggregatePlan, or an int chunk (cached plan).
     """
     _need_gpu(x, w, row_scale, out, graph.indptr)
     F = x.shape[1]
-    ldx = _rows(x, "x")
+    if x.dtype == torch.bfloat16 and x_mode == "edge":
+        raise TypeError("aggregate: bfloat16 rows are gathered by index (src / dst)")
+    ldx = _rows(x, "x", torch.bfloat16 if x.dtype == torch.bfloat16 else torch.float32)
+    x_dt = _lib.GTA_BF16 if x.dtype == torch.bfloat16 else _lib.GTA_F32
     if x_mode == "edge" and x.shape[0] < graph.nnz:
         raise ValueError("edge-mode x must have E rows")
     if x_mode == "src" and x.shape[0] < graph.n_cols:
@@ -140,7 +144,7 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
             raise ValueError("plan built for another graph")
         pbuf, ws, chunk = plan.buf, plan.workspace(F), plan.chunk
     check(_L().gta_aggregate(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz, _MODES[x_mode],
-                             _ptr(x), ldx, F, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy,
+                             _ptr(x), ldx, F, x_dt, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy,
                              int(bool(accumulate)), _ptr(pbuf), chunk, _ptr(ws), _stream(x.device)), "aggregate")
     return out
 
@@ -397,9 +401,10 @@ def edge_softmax(graph, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize=True, out=N
 
 
 def apply_node(bin, sf, a, b=None, out=None, b_broadcast_row=False):
-    """out[i] = sf(a[i] bin b[i]); b_broadcast_row: b is a single row for all i (e.g. (1+eps))."""
+    """out[i] = sf(a[i] bin b[i]); b_broadcast_row: b is a single row for all i (e.g. (1+eps)).
+    a float32 or bfloat16 (widened exactly); b and out float32."""
     _need_gpu(a, b, out)
-    lda = _rows(a, "a")
+    lda = _rows(a, "a", torch.bfloat16 if a.dtype == torch.bfloat16 else torch.float32)
     ldb = _rows(b, "b") if b is not None else 0
     if b is not None and not b_broadcast_row and b.shape[0] < a.shape[0]:
         raise ValueError("apply_node: b has fewer rows than a")
@@ -410,7 +415,8 @@ def apply_node(bin, sf, a, b=None, out=None, b_broadcast_row=False):
     if out is None:
         out = torch.empty(n, Fo, dtype=torch.float32, device=a.device)
     ldo = _rows(out, "out")
-    check(_L().gta_apply_node(_BINS[bin], _sf(sf), n, _ptr(a), lda, a.shape[1], _ptr(b), ldb,
+    a_dt = _lib.GTA_BF16 if a.dtype == torch.bfloat16 else _lib.GTA_F32
+    check(_L().gta_apply_node(_BINS[bin], _sf(sf), n, _ptr(a), lda, a.shape[1], a_dt, _ptr(b), ldb,
                               0 if b is None else b.shape[1], _ptr(out), ldo, _stream(a.device)), "apply_node")
     return out
 

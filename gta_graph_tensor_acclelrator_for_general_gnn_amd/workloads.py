@@ -15,7 +15,10 @@ import torch
 from . import graph as G
 
 
-def make_tensors(opgraph, graph, network=None, seed=0, device=None, dtype_w=torch.float32):
+def make_tensors(opgraph, graph, network=None, seed=0, device=None, dtype_w=torch.float32, dtype_x=torch.float32):
+    """dtype_x: the model input's storage type (bfloat16 for the bf16 GIN configuration: the
+    aggregate then gathers 2-byte rows, BASELINE.md's GIN byte model; every kernel widens them
+    exactly and sums in fp32)."""
     device = device or graph.device
     gen = torch.Generator(device="cpu")
     gen.manual_seed(seed)
@@ -34,7 +37,7 @@ def make_tensors(opgraph, graph, network=None, seed=0, device=None, dtype_w=torc
                 if w and (fin is None):
                     fin = w
     if fin is not None:
-        t["x"] = randn(n, fin)
+        t["x"] = randn(n, fin).to(dtype_x)
     for op in opgraph.ops:
         if op.comp == "MM":
             k = op.in_width(0)

@@ -40,7 +40,8 @@ extern "C" {
 #define GTA_ABI_VERSION 5  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
                               hooks; 4: knob sets attached to streams (gta_tuning_*); 5: every UPDATE
                               on hand-written kernels (no vendor library), gta_update_mm_t_splits,
-                              the blocked workspace is the slab rows alone and required */
+                              the blocked workspace is the slab rows alone and required, bf16
+                              rows in gta_aggregate (x_dtype) and gta_apply_node (a_dtype) */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -116,13 +117,16 @@ int gta_scatter(int dir, const int64_t* indptr, const int32_t* indices, int64_t 
  *       gta_aggregate_plan_build with the same graph and plan_chunk; rows
  *       longer than plan_chunk are split over several wavefronts whose
  *       partials are summed in a fixed order (deterministic; no atomics).
+ * x_dtype: GTA_F32, or GTA_BF16 for x_mode SRC / DST with w NULL or head weights
+ *          (rows widened exactly to fp32, sums in fp32: the 2-byte gathers of BASELINE.md's
+ *          GIN byte model).
  * workspace: >= gta_aggregate_workspace_bytes(...) when plan != NULL.
  * Reference: hardware_info.yaml Inst_fused [applyedge,gather] [MUL,ADD]
  * ("FinalVersion For Paper/hardware_info.yaml":35-38), inst_fusion_x2
  * code/interpreter.py:575-636, fuse_fetch :764-802; gather ISA
  * template/ISA_defination.yaml:46-61. */
 int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz,
-                  int x_mode, const float* x, int64_t ldx, int64_t F,
+                  int x_mode, const void* x, int64_t ldx, int64_t F, int x_dtype,
                   const float* w, int64_t ldw, int64_t heads,
                   const float* row_scale, float* y, int64_t ldy, int accumulate,
                   const void* plan, int64_t plan_chunk, void* workspace, void* stream);
@@ -219,9 +223,10 @@ int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indice
 
 /* ---- K5 APPLYNODE element-wise -----------------------------------------
  * out[i, c] = sf( a[i, c_a] (bin) b[i, c_b] ), same broadcast rules, ldb == 0
- * broadcasts one row (e.g. the (1+eps) scalar of GIN op 3).
+ * broadcasts one row (e.g. the (1+eps) scalar of GIN op 3).  a_dtype GTA_F32 or GTA_BF16
+ * (a widened exactly); b and out fp32.
  * Reference: applynode ops genGraphOP.py:62, 94-95, 103-108. */
-int gta_apply_node(int bin, int sf, int64_t n, const float* a, int64_t lda, int64_t Fa,
+int gta_apply_node(int bin, int sf, int64_t n, const void* a, int64_t lda, int64_t Fa, int a_dtype,
                    const float* b, int64_t ldb, int64_t Fb, float* out, int64_t ldo, void* stream);
 
 /* ---- K4 UPDATE / MVM on MFMA (applynode MM, applyedge MM) -------------

@@ -40,7 +40,7 @@ def test_every_declared_symbol_is_exported(lib):
 def test_abi_version_and_error_path(lib):
     assert lib.gta_abi_version() == _lib.ABI_VERSION
     # argument validation fails before any device work, so this is safe without a GPU
-    rc = lib.gta_aggregate(None, None, 10, 10, 1, None, 0, 0, None, 0, 0, None, None, 0, 0, None, 0, None, None)
+    rc = lib.gta_aggregate(None, None, 10, 10, 1, None, 0, 0, 0, None, 0, 0, None, None, 0, 0, None, 0, None, None)
     assert rc < 0
     assert b"aggregate" in lib.gta_last_error()
     assert lib.gta_aggregate_plan_bytes(100, 1000, 64) > 0

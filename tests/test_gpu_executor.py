@@ -300,11 +300,11 @@ def test_repeated_execute_replays_a_hip_graph(golden_dir, manifest, cora, dev, t
         assert torch.equal(again.outputs[k], fresh[k])
     # a knob change is part of the cache key: the next call runs eagerly under the new knobs
     from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
-    n_entries = len(executor._AUTO)
     try:
         ops.set_debug("mm_ring", 0)
+        ep = ops.knob_epoch()
         later = run()
-        assert len(executor._AUTO) == n_entries + 1
+        assert any(k[5] == ep for k in executor._AUTO)  # a new entry under the new knob state
     finally:
         ops.set_debug("mm_ring", 1)
     for k in fresh:

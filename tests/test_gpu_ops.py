@@ -907,3 +907,81 @@ def test_degenerate_graphs_every_op(dev, n):
     assert ops.update_mm(x, wm).shape == (n, 64)
     assert ops.update_mm(x[:0], wm).shape == (0, 64)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("F,heads", [(100, 1), (100, 0), (100, 4), (128, 8), (64, 0), (3, 1), (602, 1)])
+@pytest.mark.parametrize("plan", [None, 64])
+@pytest.mark.parametrize("mode", ["src", "dst"])
+def test_aggregate_bf16_rows(dev, F, heads, plan, mode):
+    """bf16 node rows gathered by index (the GIN products byte model: 200-B rows at F = 100),
+    widened exactly and summed in fp32: within the fp32 bound of the fp64 oracle on the bf16
+    values, and bitwise equal to the same kernel form on the fp32-widened table (F = 100: both
+    run 32 lanes x 4 values per edge)."""
+    n, e = 400, 7000
+    g, ip, ix = _graph(n, e, seed=F + heads, heavy_row=900, empty_rows=4, dev=dev)
+    rng = np.random.default_rng(F)
+    x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(torch.bfloat16)
+    w = rng.random((g.nnz, heads)).astype(np.float32) if heads else None
+    xd = x.to(dev)
+    wd = None if w is None else torch.from_numpy(w).to(dev)
+    y = ops.aggregate(g, xd, mode, wd, plan=plan)
+    xf = x.float().numpy()
+    _check(y, isa_ref.aggregate(ip, ix, xf, mode, w), isa_ref.aggregate_abs(ip, ix, xf, mode, w), f"bf16 F={F}")
+    if F == 100:
+        assert torch.equal(y, ops.aggregate(g, xd.float(), mode, wd, plan=plan))
+    acc = torch.randn(n, F, device=dev)
+    y2 = ops.aggregate(g, xd, mode, wd, out=acc.clone(), accumulate=True, plan=plan)
+    _check(y2, acc.cpu().numpy() + isa_ref.aggregate(ip, ix, xf, mode, w),
+           isa_ref.aggregate_abs(ip, ix, xf, mode, w) + np.abs(acc.cpu().numpy()), "bf16 accumulate")
+    with pytest.raises(TypeError):
+        ops.aggregate(g, torch.zeros(g.nnz, F, device=dev, dtype=torch.bfloat16), "edge")
+
+
+@pytest.mark.parametrize("bin_kind,sf,Fa,Fb,bcast", [("MUL", None, 100, 1, True), ("ADD", "RELU", 128, 128, False),
+                                                     (None, "ELU", 7, None, False), ("DIV", None, 100, 4, False)])
+def test_apply_node_bf16_operand(dev, bin_kind, sf, Fa, Fb, bcast):
+    """A bf16 `a` (GIN op 3: (1 + eps) x on the bf16 model input) widened exactly: bitwise equal to
+    the fp32 call on the widened tensor, vector and generic forms alike."""
+    rng = np.random.default_rng(Fa)
+    n = 3001
+    a = torch.from_numpy(rng.standard_normal((n, Fa)).astype(np.float32)).to(torch.bfloat16).to(dev)
+    b = None if Fb is None else torch.from_numpy((rng.random((1 if bcast else n, Fb)) + 0.5).astype(np.float32)).to(dev)
+    got = ops.apply_node(bin_kind, sf, a, b, b_broadcast_row=bcast)
+    want = ops.apply_node(bin_kind, sf, a.float(), b, b_broadcast_row=bcast)
+    assert got.dtype == torch.float32 and torch.equal(got, want)
+
+
+@pytest.mark.parametrize("M,K,N,dt,gathered,sf", [(40000, 100, 128, "mixed", False, None), (40000, 128, 128, "mixed", False, "RELU"),
+                                                  (30000, 128, 64, "bf16", False, None), (5000, 37, 200, "mixed", False, None),
+                                                  (777, 256, 128, "mixed", True, "RELU"), (3001, 100, 130, "bf16", True, None),
+                                                  (2449, 200, 128, "bf16", False, "ELU")])
+def test_update_mm_ring_bf_bitwise(dev, M, K, N, dt, gathered, sf):
+    """k_mm_ring_bf (bf16 MFMA with the x ring and W^T resident in LDS; the GIN MLP GEMMs) ==
+    k_mm_rows bitwise (same k order, same RNE rounding of fp32 x, same zero padding) with 64- and
+    128-row groups, and both within the fp32 bound of fp64 on the bf16-rounded operands: K tails,
+    column blocks past N, gathered rows, SF epilogues."""
+    rng = np.random.default_rng(M + K + N)
+    x = torch.from_numpy(rng.standard_normal((M + 5, K)).astype(np.float32))
+    w = torch.from_numpy((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32)).to(torch.bfloat16)
+    if dt == "bf16":
+        x = x.to(torch.bfloat16)
+    idx = torch.from_numpy(rng.integers(0, M + 5, M).astype(np.int32)) if gathered else None
+    xd, wd = x.to(dev), w.to(dev)
+    idd = None if idx is None else idx.to(dev)
+    outs = []
+    try:
+        for ring, fr in ((0, 0), (1, 1), (1, 2)):
+            ops.set_debug("mm_ring", ring)
+            ops.set_debug("mm_ring_fr", fr)
+            outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
+    finally:
+        ops.set_debug("mm_ring", 1)
+        ops.set_debug("mm_ring_fr", 0)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(outs[0], o)
+    xr = x.to(torch.bfloat16).float().numpy()
+    xs = xr[idx.numpy()] if gathered else xr[:M]
+    wf = w.float().numpy()
+    ref = isa_ref.mm(xs, wf, sf_kind=sf)
+    _check(outs[1], ref, np.abs(xs).astype(np.float64) @ np.abs(wf).astype(np.float64), "k_mm_ring_bf")

@@ -122,7 +122,7 @@ def test_default_grids():
     assert [distributed.grid_shape(w, "rows") for w in (2, 4, 8)] == [(2, 1), (4, 1), (8, 1)]
 
 
-def _bench_worker(rank, world, port, mode, q):
+def _bench_worker(rank, world, port, mode, q, n=N, e=E):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -140,7 +140,7 @@ def _bench_worker(rank, world, port, mode, q):
         bench.Aggregate.launch = launch
         bench.ops.BlockedPlan.auto_blocks = staticmethod(lambda g, f: 1)   # single-pass plan, no device plan
         bench.G.Graph.plan = lambda self, chunk=512: None
-        args = types.SimpleNamespace(mode=mode, grid="auto", row_chunks=2, n=N, e=E, blocks=0, impl="plan")
+        args = types.SimpleNamespace(mode=mode, grid="auto", row_chunks=2, n=n, e=e, blocks=0, impl="plan")
         shard, agg, m, pr, pc, chunks = bench.build(args, world, rank, torch.device("cpu"), "gloo", lambda s: None)
         for _ in range(2):
             agg.step()
@@ -151,39 +151,51 @@ def _bench_worker(rank, world, port, mode, q):
             owned = torch.arange(g.chunks * g.mk) + g.r0
             owned = torch.where(owned < g.r1, owned, torch.full_like(owned, -1))
             # the gathered table holds every rank's rows at the padded positions
-            full = torch.zeros(N, metric.F)
+            full = torch.zeros(n, metric.F)
             for q_ in range(world):
                 r0, r1 = shard.rcuts[q_], shard.rcuts[q_ + 1]
                 rows = torch.cat([agg.y_full[c * w_ + q_ * g.mk:c * w_ + (q_ + 1) * g.mk] for c in range(g.chunks)])
                 full[r0:r1] = rows[:r1 - r0]
-            whole = metric.Shard(N, E, 0, 1, 1, 1, "cpu")
+            whole = metric.Shard(n, e, 0, 1, 1, 1, "cpu")
             ip, ix = whole.graph.numpy()
             ref = isa_ref.aggregate(ip, ix, whole.x.numpy(), "src", whole.alpha.numpy())
             gathered_err = float(np.abs(full.numpy() - ref).max())
         else:
             part, owned = agg.y_own, g.owned_rows(rank)
             gathered_err = 0.0
-        ratio, err, n = bench.oracle_parity(shard, part, owned, k=400)
-        q.put((rank, (pr, pc), ratio, n, gathered_err))
+        ratio, err, n_rows = bench.oracle_parity(shard, part, owned, k=400)
+        if mode == "edges":  # every owned row of this rank against the fp64 oracle, not a sample
+            whole = metric.Shard(n, e, 0, 1, 1, 1, "cpu")
+            ip, ix = whole.graph.numpy()
+            ref = isa_ref.aggregate(ip, ix, whole.x.numpy(), "src", whole.alpha.numpy())
+            ok = owned >= 0
+            gathered_err = float(np.abs(part[ok].double().numpy() - ref[owned[ok].numpy()]).max()) if ok.any() else 0.0
+        q.put((rank, (pr, pc), ratio, n_rows, gathered_err, int(shard.graph.nnz)))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode", [(2, "edges"), (4, "edges"), (2, "rows"), (3, "rows")])
-def test_bench_exchange_gloo(world, mode):
+@pytest.mark.parametrize("world,mode,n,e", [(2, "edges", N, E), (4, "edges", N, E), (2, "rows", N, E),
+                                           (3, "rows", N, E), (8, "edges", N, E), (8, "edges", 400, 9)])
+def test_bench_exchange_gloo(world, mode, n, e):
     """bench.py's N-rank step (gloo, oracle kernels): every rank's rows after the exchange match the
-    fp64 oracle; in rows mode the gathered table is the whole Y."""
+    fp64 oracle; in rows mode the gathered table is the whole Y.  World 8 runs the driver's 8-GPU
+    layout, the 4 x 2 grid with one row-group sub-group per pair of ranks (distributed.row_groups),
+    every rank's owned rows checked; the 9-edge graph leaves ranks with empty tiles."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, mode, q)) for r in range(world)]
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, mode, q, n, e)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(240)
+        p.join(300)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     out = [q.get(timeout=10) for _ in range(world)]
-    for rank, grid, ratio, n, gathered in out:
+    for rank, grid, ratio, n_rows, gathered, nnz in out:
         assert grid == distributed.grid_shape(world, mode)
-        assert n > 0 and ratio <= 1.0, (rank, ratio)
+        assert ratio <= 1.0, (rank, ratio)
         assert gathered < 1e-5
+    assert sum(o[5] for o in out) == (e if mode == "edges" else sum(o[5] for o in out))
+    if e < world:
+        assert any(o[5] == 0 for o in out)  # at least one rank held an empty tile
