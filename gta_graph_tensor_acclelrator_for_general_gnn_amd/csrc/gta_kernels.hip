@@ -2427,14 +2427,12 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
 // FR x NT v_mfma_f32_16x16x32_bf16 per wave.  A K tail (K % 32) is one register step with masked
 // loads.  Same k order, the same RNE rounding of x (to_bf16_bits) and the same zero padding as
 // k_mm_rows: results bitwise equal to it.
-template <int NT, int D, int FR, int SB, int PA>
-constexpr int ring_bf_blocks() {
-  return (160 * 1024 / (D * 4 * FR * PA * 1024 + NT * SB * 1024)) > 4 ? 4
-                                                                      : (160 * 1024 / (D * 4 * FR * PA * 1024 + NT * SB * 1024));
+constexpr int ring_bf_blocks(int NT, int D, int FR, int SB, int PA) {  // blocks per CU its LDS allows (<= 4)
+  return (160 / (D * 4 * FR * PA + NT * SB)) > 4 ? 4 : (160 / (D * 4 * FR * PA + NT * SB));
 }
 
 template <typename TA, int NT, int D = 3, int FR = 2, int SB = 4>
-__global__ void __launch_bounds__(kBlock, (ring_bf_blocks<NT, D, FR, SB, sizeof(TA) == 4 ? 2 : 1>()))
+__global__ void __launch_bounds__(kBlock, ring_bf_blocks(NT, D, FR, SB, sizeof(TA) == 4 ? 2 : 1))
 k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
              const uint16_t* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo) {
   static_assert(NT == 4 || NT == 8, "column fragments");
@@ -2500,8 +2498,11 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     for (int i = 0; i < FR; ++i)
 #pragma unroll
       for (int p = 0; p < PA; ++p)
-        __builtin_amdgcn_global_load_lds(const_cast<TA*>(asrc[i] + k + 4 * p),
-                                         GTA_TO_LDS(base + (wv * FR + i) * FRAG + p * 1024), 16, 0, 0);
+      {  // (a non-dependent source pointer: a TA-dependent builtin argument drops the kernel's host stub)
+        const char* src = reinterpret_cast<const char*>(asrc[i] + k + 4 * p);
+        __builtin_amdgcn_global_load_lds(const_cast<char*>(src), GTA_TO_LDS(base + (wv * FR + i) * FRAG + p * 1024), 16,
+                                         0, 0);
+      }
   };
   f32x4 acc[FR][NT];
   auto zero_acc = [&]() __attribute__((always_inline)) {
@@ -2517,8 +2518,9 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     for (int q = 0; q < 8; ++q) r[q] = static_cast<short>(to_bf16_bits(v[q]));
     return r;
   };
+  const uint32_t bbase = GTA_LDS_ADDR(bres) + static_cast<uint32_t>(lane) * 16u;
   auto mma_step = [&](const bf16x8 (&a8)[FR], int s) __attribute__((always_inline)) {
-    const uint32_t sb = GTA_LDS_ADDR(bres + s * 1024) + static_cast<uint32_t>(lane) * 16u;
+    const uint32_t sb = bbase + static_cast<uint32_t>(s) * 1024u;
     f32x4 b4[NT];
 #pragma unroll
     for (int c = 0; c < NT; ++c) ds_read16_kib(b4[c], sb, c * SB);
