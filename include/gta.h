@@ -88,7 +88,9 @@ int gta_debug_get(const char* key, int64_t* value);
  * instead of the calling thread's knobs.  h may be changed or destroyed after attaching (attach
  * again to apply changes); h == NULL detaches.  Streams without an attached set use the calling
  * thread's knobs (gta_debug_set), so concurrent calls on different streams never see each
- * other's settings. */
+ * other's settings.  The set is keyed by the raw hipStream_t value: detach before destroying the
+ * stream (a stream created later may reuse the handle and would inherit the set), and a set
+ * attached to the null stream (NULL) governs every call made on the default stream. */
 typedef struct gta_tuning gta_tuning;
 gta_tuning* gta_tuning_create(void);
 void gta_tuning_destroy(gta_tuning* h);

@@ -83,8 +83,8 @@ def main():
     which = "all"
     if "--shapes" in args:
         which = args[args.index("--shapes") + 1]
-    for a in args:
-        if "=" in a and not a.startswith("--"):
+    for i, a in enumerate(args):
+        if "=" in a and not a.startswith("--") and (i == 0 or args[i - 1] != "--sweep"):
             k, v = a.split("=")
             ops.set_debug(k, int(v))
     names = list(SHAPES) if which == "all" else which.split(",")

@@ -341,3 +341,20 @@ def test_graphed_run_follows_weights_changed_in_place(golden_dir, manifest, cora
         ref = executor.Executor(og, st, gd, tensors, sem).run()
         for k in ref:
             assert torch.equal(out[k], ref[k]), (k, trial)
+
+
+def test_gin_bf16_model_input_on_gpu(golden_dir, manifest, cora, dev):
+    """GIN with the bf16 model input (the gin-products configuration's storage) on the real kernels:
+    the bf16-row aggregate accumulating into (1+eps) x (bf16 apply_node), the bf16 MFMA MLP;
+    every op vs the fp64 oracle on the same bf16 values."""
+    rec = [s for s in _all_streams(manifest) if s["network"] == "GIN" and not s["reorder"] and s["dataset"] == "cora"][0]
+    sem = Semantics.for_network("GIN", False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    ip, ix = cora
+    gd = G.from_numpy(ip, ix, device=dev)
+    tc = workloads.make_tensors(og, G.from_numpy(ip, ix), "GIN", seed=7, dtype_w=torch.bfloat16, dtype_x=torch.bfloat16)
+    res, ex = executor.run_stream(og, st, gd, {k: v.to(dev) for k, v in tc.items()}, sem)
+    # op-local fp64 checks (the bf16 GEMMs' inputs rounded to bf16 in the reference too)
+    from oracle.sampled import SampledChecker
+    assert SampledChecker(ex, ip, ix).check(n_samples=400, seed=3)

@@ -245,3 +245,22 @@ def test_gather_acc_fusion_cpu(golden_dir, manifest, monkeypatch):
             nbytes[on] = ex.alg_bytes
             compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
         assert nbytes[True] < nbytes[False]
+
+
+def test_gin_bf16_model_input_cpu(golden_dir, manifest, monkeypatch):
+    """The bf16 GIN configuration (x stored in bf16: BASELINE.md's 200-B rows, bf16 MLP weights):
+    every op of the stream, the gather-accumulate fusion included, equals the fp64 oracle run on
+    the same bf16 values (the executor widens a bf16 table only where an element-wise edge op
+    materialises it)."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    rec = [s for s in _streams(manifest) if s["network"] == "GIN" and not s["reorder"]][0]
+    sem = Semantics.for_network("GIN", False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    gc, ip, ix = _cora_graph(golden_dir)
+    tensors = workloads.make_tensors(og, gc, "GIN", seed=6, dtype_w=torch.bfloat16, dtype_x=torch.bfloat16)
+    assert tensors["x"].dtype == torch.bfloat16
+    ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
+    ex = executor.Executor(og, st, gc, tensors, sem)
+    ex.run()
+    compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
