@@ -2235,7 +2235,12 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   const int64_t grp0 = blockIdx.x / ncb, gstep = gridDim.x / ncb;
   const int64_t n_groups = (M + GR - 1) / GR;
   const int64_t my_groups = grp0 < n_groups ? (n_groups - grp0 + gstep - 1) / gstep : 0;
-  const int S = K / KS;  // whole stages per group (a K tail: register steps of 16 k)
+  // stages per group: with K % 4 == 0 a K tail is one more ring stage whose 16-B pieces lie wholly
+  // inside or wholly past K (those read the row start instead and are zeroed after the LDS read);
+  // otherwise the tail is a register step of 16 k with masked loads, paid synchronously per group
+  const bool ring_tail = (K % KS) != 0 && (K % 4) == 0;
+  const int S = ring_tail ? (K + KS - 1) / KS : K / KS;
+  const bool dead = ring_tail && (S - 1) * KS + 4 * g >= K;  // this lane's pieces of the last stage
   const int64_t T = my_groups * S;
   const float* bsrc[NT / 4];
 #pragma unroll
@@ -2264,17 +2269,18 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     }
     char* base = lds + iss_slot * STAGE;
     iss_slot = iss_slot + 1 == D ? 0 : iss_slot + 1;
+    const int ko = (dead && iss_s == S - 1) ? -4 * g : k;  // a piece past K reads its row's start
     if (++iss_s == S) {
       iss_s = 0;
       ++iss_j;
     }
 #pragma unroll
     for (int i = 0; i < FR; ++i)
-      __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[i] + k), GTA_TO_LDS(base + (wv * FR + i) * 1024), 16, 0,
+      __builtin_amdgcn_global_load_lds(const_cast<float*>(asrc[i] + ko), GTA_TO_LDS(base + (wv * FR + i) * 1024), 16, 0,
                                        0);
 #pragma unroll
     for (int q = 0; q < NT / 4; ++q)
-      __builtin_amdgcn_global_load_lds(const_cast<float*>(bsrc[q] + k),  // (a const source fails the host pass)
+      __builtin_amdgcn_global_load_lds(const_cast<float*>(bsrc[q] + ko),  // (a const source fails the host pass)
                                        GTA_TO_LDS(base + A_BYTES + (wv * (NT / 4) + q) * 1024), 16, 0, 0);
   };
   f32x4 acc[FR][NT];
@@ -2395,6 +2401,12 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     for (int i = 0; i < FR; ++i) asm volatile("" : "+v"(a4[i]));
 #pragma unroll
     for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(b4[c]));
+    if (dead && s == S - 1) {  // pieces past K: zeros, as k_mm_rows' masked loads and staging give
+#pragma unroll
+      for (int i = 0; i < FR; ++i) a4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < NT; ++c) b4[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
     // j outermost: the FR x NT accumulators are each touched once per FR*NT MFMAs; per
     // accumulator the k order is k_mm_rows' (bitwise equal)
 #pragma unroll
@@ -2406,7 +2418,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
           acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i][jj], b4[c][jj], acc[i][c], 0, 0, 0);
   }
   // the group's last stage is done: its K tail, its rows out, the next group's sums
-  if (K % KS) tail(j);
+  if (!ring_tail && (K % KS)) tail(j);
   epilogue(j);
   zero_acc();
   // the counted waits above assume only ring DMA is outstanding; stores may retire out of order
@@ -2452,7 +2464,11 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   const int64_t grp0 = blockIdx.x / ncb, gstep = gridDim.x / ncb;
   const int64_t n_groups = (M + GR - 1) / GR;
   const int64_t my_groups = grp0 < n_groups ? (n_groups - grp0 + gstep - 1) / gstep : 0;
-  const int S = K / KS;
+  // a K tail is one more ring stage when its pieces (4 fp32 / 8 bf16) lie wholly inside or wholly past
+  // K (those read the row start and are zeroed after the LDS read); else a masked register step
+  const bool ring_tail = (K % KS) != 0 && (K % (PA == 2 ? 4 : 8)) == 0;
+  const int S = ring_tail ? (K + KS - 1) / KS : K / KS;
+  const int kdead = ring_tail ? K - (S - 1) * KS : KS;  // pieces of the last stage from this k (lane-relative) are past K
   const int64_t T = my_groups * S;
   // W^T resident: fragment (c, s) at bres + (c * SB + s) KiB, lane L's 8 bf16 of row n0 + 16c + r16,
   // k = 32s + 8g .. +7 (zeros past K and N)
@@ -2490,6 +2506,7 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     }
     char* base = lds + iss_slot * STAGE;
     iss_slot = iss_slot + 1 == D ? 0 : iss_slot + 1;
+    const bool last = ring_tail && iss_s == S - 1;
     if (++iss_s == S) {
       iss_s = 0;
       ++iss_j;
@@ -2499,7 +2516,8 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
 #pragma unroll
       for (int p = 0; p < PA; ++p)
       {  // (a non-dependent source pointer: a TA-dependent builtin argument drops the kernel's host stub)
-        const char* src = reinterpret_cast<const char*>(asrc[i] + k + 4 * p);
+        const int ko = (last && 8 * g + 4 * p >= kdead) ? -8 * g : k + 4 * p;  // a piece past K reads its row's start
+        const char* src = reinterpret_cast<const char*>(asrc[i] + ko);
         __builtin_amdgcn_global_load_lds(const_cast<char*>(src), GTA_TO_LDS(base + (wv * FR + i) * FRAG + p * 1024), 16,
                                          0, 0);
       }
@@ -2622,6 +2640,13 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
       for (int i = 0; i < FR; ++i)
 #pragma unroll
         for (int p = 0; p < PA; ++p) asm volatile("" : "+v"(a4[i][p]));
+      if (ring_tail && s == S - 1) {  // pieces past K: zeros, as k_mm_rows' masked loads give
+#pragma unroll
+        for (int i = 0; i < FR; ++i)
+#pragma unroll
+          for (int p = 0; p < PA; ++p)
+            if (8 * g + 4 * p >= kdead) a4[i][p] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
       bf16x8 a8[FR];
 #pragma unroll
       for (int i = 0; i < FR; ++i) {
@@ -2635,7 +2660,7 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
       }
       mma_step(a8, s);
     }
-    if (K % KS) tail(j);
+    if (!ring_tail && (K % KS)) tail(j);
     epilogue(j);
     zero_acc();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -3542,22 +3567,12 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
     const bool uneven = per_cu2 / std::ceil(per_cu2) < 0.95;
     const int fr = (frk == 1 || (frk == 0 && ((K <= 256 && uneven) || groups < 512))) ? 1 : 2;
     const int64_t n_grp = fr == 1 ? (M + 63) / 64 : groups;
-    const int64_t units = n_grp * ncb;
-    // ring depth by the blocks each CU runs: up to one -> 8 stages (7 in flight), two -> 4, more ->
-    // the persistent 3-deep form with every CU slot filled (each CU the same number of row groups
-    // +-1; profiles/r02_mm_ring_probe.json)
+    // the persistent 3-deep ring with every CU slot its LDS allows filled (each CU the same number of
+    // row groups +-1; profiles/r02_mm_ring_probe.json); 4 or 8 stages at fewer blocks per CU were
+    // measured slower on every shape from 16,384 to 232,965 rows (profiles/r03_mm_depth_sweep.log)
     int D = 3;
-    int64_t blocks;
-    if (units <= 256) {
-      D = 8;
-      blocks = units;
-    } else if (units <= 512) {
-      D = 4;
-      blocks = units;
-    } else {
-      const int64_t per_cu = nt == 8 ? (fr == 1 ? 4 : 3) : 4;  // ring_blocks(NT, 3, FR)
-      blocks = std::min(n_grp, std::max<int64_t>(1, 256 * per_cu / ncb)) * ncb;
-    }
+    const int64_t per_cu3 = nt == 8 ? (fr == 1 ? 4 : 3) : 4;  // ring_blocks(NT, 3, FR)
+    int64_t blocks = std::min(n_grp, std::max<int64_t>(1, 256 * per_cu3 / ncb)) * ncb;
     const int dk = tuning().mm_ring_depth;
     if (dk == 3 || dk == 4 || dk == 8) {  // forced depth: a persistent grid of what that ring's LDS allows
       const int64_t per_cu = dk == 8 ? 1 : dk == 4 ? (nt == 8 && fr == 2 ? 2 : 3) : (nt == 8 ? (fr == 1 ? 4 : 3) : 4);
@@ -3650,7 +3665,9 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
     // slice in flight from the start), then the ordered slice sum.  GCN Cora's [2708 x 1433].[1433 x 128]:
     // 22 groups x 10 slices of 144 k
     const int dk = tuning().mm_ring_depth;
-    launch_ring(nt, dk == 3 || dk == 4 ? dk : 8, 2, dim3(static_cast<unsigned>(groups * ncb), static_cast<unsigned>(nsl)), s,
+    const int fr = tuning().mm_ring_fr == 1 ? 1 : 2;
+    const int64_t n_grp = fr == 1 ? (M + 63) / 64 : groups;
+    launch_ring(nt, dk == 3 || dk == 4 ? dk : 8, fr, dim3(static_cast<unsigned>(n_grp * ncb), static_cast<unsigned>(nsl)), s,
                 static_cast<const float*>(x), ldx, row_idx, M, static_cast<int>(K), static_cast<const float*>(wt), ldwt,
                 static_cast<int>(N), GTA_SF_NONE, ws, N, static_cast<int>(ks), M * N);
     GTA_LAUNCHED("k_mm_ring<split>");

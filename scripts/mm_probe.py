@@ -17,6 +17,7 @@ from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops  # noqa: E402
 
 SHAPES = {
     "cora": [(2708, 1433, 128, "f32"), (2708, 128, 64, "f32")],
+    "cora_x": [(2708, 1433, 128, "f32"), (2708, 1432, 128, "f32")],
     "mid": [(16384, 128, 128, "f32"), (29000, 602, 128, "f32"), (44625, 500, 128, "f32"), (29000, 602, 256, "f32"),
             (16384, 1433, 128, "f32"), (5000, 602, 128, "f32")],
     "big": [(232965, 602, 128, "f32"), (232965, 602, 256, "f32"), (89250, 500, 128, "f32"), (232965, 128, 128, "f32"),
