@@ -1752,6 +1752,27 @@ k_edge_softmax_v(const int64_t* __restrict__ indptr, const int32_t* __restrict__
 // ---------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// SF epilogue of the MFMA GEMMs applied to the whole accumulator tile in place, the switch on sf
+// OUTSIDE the element loops.  With sf_apply per element each of the FR x NT x 4 store sites held
+// its own switch over every SF body: k_mm_ring<8, 8, 2> compiled to 147 KB, and an epilogue run
+// walked ~100 KB of cold instruction cache (each new lane of code an L2 round trip), a fixed
+// ~10 us per launch that a 9-stage split-K block could not hide.  Here the no-SF path is one branch.
+template <int FR, int NT>
+__device__ __forceinline__ void sf_tile(int sf, f32x4 (&acc)[FR][NT]) {
+  switch (sf) {
+#define GTA_SFT(K_)                                                                  \
+  case K_:                                                                           \
+    _Pragma("unroll") for (int i = 0; i < FR; ++i)                                    \
+      _Pragma("unroll") for (int c = 0; c < NT; ++c)                                  \
+        _Pragma("unroll") for (int r = 0; r < 4; ++r) acc[i][c][r] = sf_apply(K_, acc[i][c][r]); \
+    return;
+    GTA_SFT(GTA_SF_RELU) GTA_SFT(GTA_SF_EXP_LEAKY_RELU) GTA_SFT(GTA_SF_ELU) GTA_SFT(GTA_SF_EXP)
+    GTA_SFT(GTA_SF_LEAKY_RELU) GTA_SFT(GTA_SF_SIGMOID) GTA_SFT(GTA_SF_TANH) GTA_SFT(GTA_SF_RECIP)
+#undef GTA_SFT
+    default: return;  // GTA_SF_NONE
+  }
+}
+
 __global__ void __launch_bounds__(kBlock)
 k_mm_f32(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
          const float* __restrict__ w, int64_t ldw, int N, int sf, float* __restrict__ out, int64_t ldo) {
@@ -2082,6 +2103,7 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
       }
       if (!one_chunk) __syncthreads();
     }
+    sf_tile(sf, acc);
     if (vstore) {
       // lane (g, r16 = 4q + p) holds C[4g + r][4q + p], r = 0..3; a 4x4 transpose inside each
       // lane quad (DPP swaps of lane bit 0, then bit 1) leaves C[4g + p][4q + r] -- four
@@ -2093,7 +2115,7 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
         for (int c = 0; c < NT; ++c) {
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = sf_apply(sf, acc[i][c][r]);
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][c][r];
 #pragma unroll
           for (int m2 = 0; m2 < 2; ++m2) {  // bit 0: registers (2m2, 2m2+1) across lanes (p, p^1)
             const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
@@ -2127,7 +2149,7 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
           for (int r = 0; r < 4; ++r) {
             const int64_t m = mw + 16 * i + 4 * g + r;
             const int n = n0 + 16 * c + r16;
-            if (m < M && n < N) out[m * ldo + n] = sf_apply(sf, acc[i][c][r]);
+            if (m < M && n < N) out[m * ldo + n] = acc[i][c][r];
           }
     }
   }
@@ -2208,7 +2230,7 @@ template <int NT, int D = 3, int FR = 2>
 __global__ void __launch_bounds__(kBlock, ring_blocks(NT, D, FR))
 k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const float* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
-          int kslice = 0, int64_t slice_stride = 0) {
+          int kslice = 0, int64_t slice_stride = 0, int lr = 1) {
   static_assert(NT == 4 || NT == 8, "B fragments split evenly over the 4 waves");
   static_assert(FR == 1 || FR == 2, "one or two A fragments per wave");
   static_assert(D >= 3 && D <= 8, "ring depth");
@@ -2240,13 +2262,25 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   // otherwise the tail is a register step of 16 k with masked loads, paid synchronously per group
   const bool ring_tail = (K % KS) != 0 && (K % 4) == 0;
   const int S = ring_tail ? (K + KS - 1) / KS : K / KS;
-  const bool dead = ring_tail && (S - 1) * KS + 4 * g >= K;  // this lane's pieces of the last stage
+  // DMA lane map.  lr = 1 (row-contiguous): lane L fills row rr = L / 4 of a fragment with its
+  // 16-B piece cp = L % 4, so 4 consecutive lanes read one row's 64 contiguous bytes (a fragment
+  // instruction touches 16 row segments in 16 lane quads); the piece it carries is the logical
+  // k piece c = cp ^ ((rr >> 2) & 2), an XOR swizzle that keeps the fragment reads below
+  // conflict-free in every ds_read_b128 lane group.  lr = 0: lane (g, r) fills its own MFMA
+  // fragment (row r, piece g): 16 rows per 16 consecutive lanes.  Either way lane (g, r) reads
+  // logical piece g of row r: the values and the k order are the same (bitwise equal).
+  const int rr = lr ? lane >> 2 : r16;
+  const int cdma = lr ? (lane & 3) ^ ((rr >> 2) & 2) : g;  // logical 16-B k piece this lane DMAs
+  const uint32_t rdoff = lr ? static_cast<uint32_t>(r16 * 64 + ((g ^ ((r16 >> 2) & 2)) * 16))
+                            : static_cast<uint32_t>(lane) * 16u;
+  const bool dead = ring_tail && (S - 1) * KS + 4 * cdma >= K;  // this lane's DMA piece of the last stage
+  const bool dead_rd = ring_tail && (S - 1) * KS + 4 * g >= K;  // the piece this lane reads
   const int64_t T = my_groups * S;
   const float* bsrc[NT / 4];
 #pragma unroll
   for (int t = 0; t < NT / 4; ++t) {
-    const int n = min(n0 + 16 * (wv * (NT / 4) + t) + r16, N - 1);
-    bsrc[t] = wt + static_cast<int64_t>(n) * ldwt + 4 * g;
+    const int n = min(n0 + 16 * (wv * (NT / 4) + t) + rr, N - 1);
+    bsrc[t] = wt + static_cast<int64_t>(n) * ldwt + 4 * cdma;
   }
   // A source row of group j, fragment i, fragment row sub
   auto a_row = [&](int64_t j, int i, int sub) __attribute__((always_inline)) -> const float* {
@@ -2264,12 +2298,12 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     const int k = iss_s * KS;
     if (j != asrc_j) {
 #pragma unroll
-      for (int i = 0; i < FR; ++i) asrc[i] = a_row(j, i, r16) + 4 * g;
+      for (int i = 0; i < FR; ++i) asrc[i] = a_row(j, i, rr) + 4 * cdma;
       asrc_j = j;
     }
     char* base = lds + iss_slot * STAGE;
     iss_slot = iss_slot + 1 == D ? 0 : iss_slot + 1;
-    const int ko = (dead && iss_s == S - 1) ? -4 * g : k;  // a piece past K reads its row's start
+    const int ko = (dead && iss_s == S - 1) ? -4 * cdma : k;  // a piece past K reads its row's start
     if (++iss_s == S) {
       iss_s = 0;
       ++iss_j;
@@ -2300,6 +2334,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   const bool vstore = ldo % 4 == 0 && aligned(out, 16);
   auto epilogue = [&](int64_t j) __attribute__((always_inline)) {
     const int64_t mw = (grp0 + j * gstep) * GR + wv * (16 * FR);
+    sf_tile(sf, acc);
     if (vstore) {  // quad-transposed 16-B row stores (k_mm_rows' epilogue)
       const int p = r16 & 3, q = r16 >> 2;
 #pragma unroll
@@ -2308,7 +2343,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
         for (int c = 0; c < NT; ++c) {
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = sf_apply(sf, acc[i][c][r]);
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][c][r];
 #pragma unroll
           for (int m2 = 0; m2 < 2; ++m2) {
             const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
@@ -2342,7 +2377,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
           for (int r = 0; r < 4; ++r) {
             const int64_t m = mw + 16 * i + 4 * g + r;
             const int n = n0 + 16 * c + r16;
-            if (m < M && n < N) out[m * ldo + n] = sf_apply(sf, acc[i][c][r]);
+            if (m < M && n < N) out[m * ldo + n] = acc[i][c][r];
           }
     }
   };
@@ -2389,8 +2424,8 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     // fragment reads in inline asm: hipcc cannot tell them apart from the DMA in flight into
     // another slot and would wait vmcnt(0) before a plain LDS read (draining the ring every step).
     // The asm wait names every loaded register, so no MFMA is scheduled above it.
-    const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * 1024) + static_cast<uint32_t>(lane) * 16u;
-    const uint32_t sb = GTA_LDS_ADDR(lds + slot * STAGE + A_BYTES) + static_cast<uint32_t>(lane) * 16u;
+    const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * 1024) + rdoff;
+    const uint32_t sb = GTA_LDS_ADDR(lds + slot * STAGE + A_BYTES) + rdoff;
     f32x4 a4[FR], b4[NT];
 #pragma unroll
     for (int i = 0; i < FR; ++i) ds_read16_idx(a4[i], sa, i);
@@ -2401,7 +2436,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     for (int i = 0; i < FR; ++i) asm volatile("" : "+v"(a4[i]));
 #pragma unroll
     for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(b4[c]));
-    if (dead && s == S - 1) {  // pieces past K: zeros, as k_mm_rows' masked loads and staging give
+    if (dead_rd && s == S - 1) {  // pieces past K: zeros, as k_mm_rows' masked loads and staging give
 #pragma unroll
       for (int i = 0; i < FR; ++i) a4[i] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -2446,7 +2481,8 @@ constexpr int ring_bf_blocks(int NT, int D, int FR, int SB, int PA) {  // blocks
 template <typename TA, int NT, int D = 3, int FR = 2, int SB = 4>
 __global__ void __launch_bounds__(kBlock, ring_bf_blocks(NT, D, FR, SB, sizeof(TA) == 4 ? 2 : 1))
 k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
-             const uint16_t* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo) {
+             const uint16_t* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
+             int lr = 1) {
   static_assert(NT == 4 || NT == 8, "column fragments");
   static_assert(FR == 1 || FR == 2, "one or two A fragments per wave");
   static_assert(D >= 3 && D <= 8, "ring depth");
@@ -2489,11 +2525,34 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     }
     *reinterpret_cast<uint4*>(bres + f * 1024 + L * 16) = v;
   }
-  auto a_row = [&](int64_t j, int i) __attribute__((always_inline)) -> const TA* {
-    const int64_t m = min<int64_t>((grp0 + j * gstep) * GR + wv * (16 * FR) + 16 * i + r16, M - 1);
+  auto a_row = [&](int64_t j, int i, int sub) __attribute__((always_inline)) -> const TA* {
+    const int64_t m = min<int64_t>((grp0 + j * gstep) * GR + wv * (16 * FR) + 16 * i + sub, M - 1);
     return x + (row_idx ? static_cast<int64_t>(row_idx[m]) : m) * ldx;
   };
-  const TA* asrc[FR];
+  // DMA lane map (k_mm_ring's): lr = 1 (row-contiguous): DMA instruction p of a fragment holds
+  // rows RPI p .. RPI p + RPI - 1 (RPI = 8 fp32 / 16 bf16), LPR consecutive lanes reading one row's
+  // 32-k stage slice (128 / 64 contiguous bytes); lane L carries logical piece c = (L % LPR) ^
+  // swz(row), the XOR swizzle that keeps the fragment reads conflict-free in every ds_read_b128
+  // lane group.  lr = 0: lane (g, r) fills its own fragment (row r, k 8g + 4p).  The image holds
+  // a fragment's rows in order ([16][RB] bytes) under lr = 1, and lane (g, r) reads logical piece
+  // 2g + p (fp32) / g (bf16) of row r either way: same values, same k order.
+  constexpr int RB = 32 * static_cast<int>(sizeof(TA)), LPR = RB / 16, RPI = 64 / LPR;
+  auto swz = [](int r) __attribute__((always_inline)) { return PA == 2 ? (r >> 1) & 5 : (r >> 2) & 2; };
+  int drow[PA], doff[PA];  // per DMA instruction p: fragment row, element offset of the lane's piece
+  uint32_t rdoff[PA];      // per read p: byte offset of logical piece (2g + p | g) of row r16
+#pragma unroll
+  for (int p = 0; p < PA; ++p) {
+    if (lr) {
+      drow[p] = RPI * p + lane / LPR;
+      doff[p] = ((lane % LPR) ^ swz(drow[p])) * (16 / static_cast<int>(sizeof(TA)));
+      rdoff[p] = static_cast<uint32_t>(r16 * RB + (((PA == 2 ? 2 * g + p : g)) ^ swz(r16)) * 16);
+    } else {
+      drow[p] = r16;
+      doff[p] = 8 * g + 4 * p;
+      rdoff[p] = static_cast<uint32_t>(lane * 16 + p * 1024);
+    }
+  }
+  const TA* asrc[FR][PA];
   int64_t asrc_j = -1, iss_j = 0;
   int iss_s = 0, iss_slot = 0;
   auto issue = [&]() __attribute__((always_inline)) {
@@ -2501,7 +2560,9 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     const int k = iss_s * KS;
     if (j != asrc_j) {
 #pragma unroll
-      for (int i = 0; i < FR; ++i) asrc[i] = a_row(j, i) + 8 * g;
+      for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int p = 0; p < PA; ++p) asrc[i][p] = a_row(j, i, drow[p]) + doff[p];
       asrc_j = j;
     }
     char* base = lds + iss_slot * STAGE;
@@ -2516,8 +2577,8 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
 #pragma unroll
       for (int p = 0; p < PA; ++p)
       {  // (a non-dependent source pointer: a TA-dependent builtin argument drops the kernel's host stub)
-        const int ko = (last && 8 * g + 4 * p >= kdead) ? -8 * g : k + 4 * p;  // a piece past K reads its row's start
-        const char* src = reinterpret_cast<const char*>(asrc[i] + ko);
+        const int ko = (last && doff[p] >= kdead) ? -doff[p] : k;  // a piece past K reads its row's start
+        const char* src = reinterpret_cast<const char*>(asrc[i][p] + ko);
         __builtin_amdgcn_global_load_lds(const_cast<char*>(src), GTA_TO_LDS(base + (wv * FR + i) * FRAG + p * 1024), 16,
                                          0, 0);
       }
@@ -2555,6 +2616,7 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   const bool vstore = ldo % 4 == 0 && aligned(out, 16);
   auto epilogue = [&](int64_t j) __attribute__((always_inline)) {
     const int64_t mw = (grp0 + j * gstep) * GR + wv * (16 * FR);
+    sf_tile(sf, acc);
     if (vstore) {
       const int p = r16 & 3, q = r16 >> 2;
 #pragma unroll
@@ -2563,7 +2625,7 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
         for (int c = 0; c < NT; ++c) {
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = sf_apply(sf, acc[i][c][r]);
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][c][r];
 #pragma unroll
           for (int m2 = 0; m2 < 2; ++m2) {
             const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
@@ -2597,7 +2659,7 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
           for (int r = 0; r < 4; ++r) {
             const int64_t m = mw + 16 * i + 4 * g + r;
             const int n = n0 + 16 * c + r16;
-            if (m < M && n < N) out[m * ldo + n] = sf_apply(sf, acc[i][c][r]);
+            if (m < M && n < N) out[m * ldo + n] = acc[i][c][r];
           }
     }
   };
@@ -2606,7 +2668,7 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     bf16x8 a8[FR];
 #pragma unroll
     for (int i = 0; i < FR; ++i) {
-      const TA* p = a_row(j, i) + k0;
+      const TA* p = a_row(j, i, r16) + k0;
       float v[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) v[q] = (k0 + q < K) ? load_elem(p + q) : 0.f;
@@ -2629,12 +2691,12 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
       __builtin_amdgcn_s_barrier();
       asm volatile("" ::: "memory");
       if (t + D - 1 < T) issue();
-      const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * FRAG) + static_cast<uint32_t>(lane) * 16u;
+      const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * FRAG);
       f32x4 a4[FR][PA];
 #pragma unroll
       for (int i = 0; i < FR; ++i)
 #pragma unroll
-        for (int p = 0; p < PA; ++p) ds_read16_idx(a4[i][p], sa, i * PA + p);
+        for (int p = 0; p < PA; ++p) ds_read16_idx(a4[i][p], sa + rdoff[p], i * PA);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int i = 0; i < FR; ++i)
@@ -2807,6 +2869,7 @@ struct Tuning {
   int mm_ring_fr = 0;      // k_mm_ring A fragments per wave: 2 = 128-row groups, 1 = 64-row groups, 0 = auto
   int mm_ring_depth = 0;   // k_mm_ring stages: 0 = auto (by blocks per CU), else 3, 4 or 8
   int mm_prefetch = 1;     // k_mm_rows A prefetch: 1 auto, 2 always, 0 never
+  int mm_dma_rows = 1;     // ring DMA lane map: 1 = row-contiguous lane quads/octets (swizzled image), 0 = lane = fragment
   int64_t mm_split = -1;   // UPDATE K slices: -1 auto, 0 = never split, n = n slices
 };
 
@@ -2865,6 +2928,7 @@ const Knob* find_knob(const char* key) {
       {"mm_ring_fr", &Tuning::mm_ring_fr, nullptr},
       {"mm_ring_depth", &Tuning::mm_ring_depth, nullptr},
       {"mm_prefetch", &Tuning::mm_prefetch, nullptr},
+      {"mm_dma_rows", &Tuning::mm_dma_rows, nullptr},
       {"mm_split", nullptr, &Tuning::mm_split},
   };
   const std::string k(key ? key : "");
@@ -3509,7 +3573,7 @@ void launch_ring(int nt, int D, int fr, dim3 gr, hipStream_t s, const float* x, 
                  int64_t slice_stride) {
 #define GTA_RING(NT_, D_, FR_)                                                                              \
   k_mm_ring<NT_, D_, FR_><<<gr, dim3(kBlock), 0, s>>>(x, ldx, row_idx, M, K, wt, ldwt, N, sf, out, ldo, kslice, \
-                                                      slice_stride)
+                                                      slice_stride, tuning().mm_dma_rows)
 #define GTA_RING_D(NT_, FR_) \
   if (D == 8) GTA_RING(NT_, 8, FR_); else if (D == 4) GTA_RING(NT_, 4, FR_); else GTA_RING(NT_, 3, FR_)
   if (nt == 8) { if (fr == 1) { GTA_RING_D(8, 1); } else { GTA_RING_D(8, 2); } }
@@ -3598,7 +3662,8 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   k_mm_ring_bf<TA_, NT_, D_, FR_, SB_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const TA_*>(x), ldx, row_idx, M, \
                                                                           static_cast<int>(K),                       \
                                                                           static_cast<const uint16_t*>(wt), ldwt,    \
-                                                                          static_cast<int>(N), sf, out, ldo)
+                                                                          static_cast<int>(N), sf, out, ldo,         \
+                                                                          tuning().mm_dma_rows)
 #define GTA_RBF_F(TA_, NT_, SB_) \
   if (fr == 2) GTA_RBF(TA_, NT_, 3, 2, SB_); else GTA_RBF(TA_, NT_, 6, 1, SB_)
 #define GTA_RBF_S(TA_, NT_) if (sb == 4) { GTA_RBF_F(TA_, NT_, 4); } else { GTA_RBF_F(TA_, NT_, 8); }

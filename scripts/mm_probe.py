@@ -18,6 +18,8 @@ from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops  # noqa: E402
 SHAPES = {
     "cora": [(2708, 1433, 128, "f32"), (2708, 128, 64, "f32")],
     "cora_x": [(2708, 1433, 128, "f32"), (2708, 1432, 128, "f32")],
+    "short_k": [(16384, 144, 128, "f32"), (16384, 137, 128, "f32"), (2816, 144, 128, "f32"), (2816, 1433, 128, "f32")],
+    "k144": [(16384, 144, 128, "f32")],
     "mid": [(16384, 128, 128, "f32"), (29000, 602, 128, "f32"), (44625, 500, 128, "f32"), (29000, 602, 256, "f32"),
             (16384, 1433, 128, "f32"), (5000, 602, 128, "f32")],
     "big": [(232965, 602, 128, "f32"), (232965, 602, 256, "f32"), (89250, 500, 128, "f32"), (232965, 128, 128, "f32"),
@@ -27,9 +29,12 @@ SHAPES = {
 }
 
 
+LDX = 0  # --ldx L: x is the first K columns of an [M, L] table (rows L * 4 B apart)
+
+
 def one(M, K, N, dt, dev, reps=20):
     g = torch.Generator(device="cpu").manual_seed(M + K + N)
-    x = torch.randn(M, K, generator=g).to(dev)
+    x = torch.randn(M, max(K, LDX), generator=g).to(dev)[:, :K]
     w = (torch.randn(K, N, generator=g) / K ** 0.5).to(dev)
     if dt == "bf16":
         x, w = x.to(torch.bfloat16), w.to(torch.bfloat16)
@@ -82,10 +87,13 @@ def main():
     dev = torch.device("cuda", 0)
     args = sys.argv[1:]
     which = "all"
+    if "--ldx" in args:
+        global LDX
+        LDX = int(args[args.index("--ldx") + 1])
     if "--shapes" in args:
         which = args[args.index("--shapes") + 1]
     for i, a in enumerate(args):
-        if "=" in a and not a.startswith("--") and (i == 0 or args[i - 1] != "--sweep"):
+        if "=" in a and not a.startswith("--") and (i == 0 or args[i - 1] not in ("--sweep", "--ldx")):
             k, v = a.split("=")
             ops.set_debug(k, int(v))
     names = list(SHAPES) if which == "all" else which.split(",")
