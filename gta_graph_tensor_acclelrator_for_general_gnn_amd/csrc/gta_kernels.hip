@@ -3726,13 +3726,14 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
   const int64_t ks = mm_kslice(K, splits), nsl = (K + ks - 1) / ks;
   if (nsl > 65535) return fail(GTA_ERR_UNSUPPORTED, "update_mm_t_split: too many slices");
   if (ring) {
-    // every (128-row group, K slice) on its own block, one per CU with an 8-deep ring (all stages of a
-    // slice in flight from the start), then the ordered slice sum.  GCN Cora's [2708 x 1433].[1433 x 128]:
-    // 22 groups x 10 slices of 144 k
+    // every (64-row group, K slice) on its own block, a 4-deep ring at three blocks per CU, then the
+    // ordered slice sum.  GCN Cora's [2708 x 1433].[1433 x 128]: 43 groups x 10 slices of 144 k,
+    // 28.8 us against 31.5 for 128-row groups on an 8-deep ring at one block per CU
+    // (profiles/r03/mm_cora_epilogue.log); mm_ring_fr = 2 / mm_ring_depth = 3 or 8 select those
     const int dk = tuning().mm_ring_depth;
-    const int fr = tuning().mm_ring_fr == 1 ? 1 : 2;
+    const int fr = tuning().mm_ring_fr == 2 ? 2 : 1;
     const int64_t n_grp = fr == 1 ? (M + 63) / 64 : groups;
-    launch_ring(nt, dk == 3 || dk == 4 ? dk : 8, fr, dim3(static_cast<unsigned>(n_grp * ncb), static_cast<unsigned>(nsl)), s,
+    launch_ring(nt, dk == 3 || dk == 8 ? dk : 4, fr, dim3(static_cast<unsigned>(n_grp * ncb), static_cast<unsigned>(nsl)), s,
                 static_cast<const float*>(x), ldx, row_idx, M, static_cast<int>(K), static_cast<const float*>(wt), ldwt,
                 static_cast<int>(N), GTA_SF_NONE, ws, N, static_cast<int>(ks), M * N);
     GTA_LAUNCHED("k_mm_ring<split>");

@@ -992,3 +992,34 @@ def test_update_mm_ring_bf_bitwise(dev, M, K, N, dt, gathered, sf):
     wf = w.float().numpy()
     ref = isa_ref.mm(xs, wf, sf_kind=sf)
     _check(outs[1], ref, np.abs(xs).astype(np.float64) @ np.abs(wf).astype(np.float64), "k_mm_ring_bf")
+
+
+@pytest.mark.parametrize("dt", ["f32", "mixed"])
+@pytest.mark.parametrize("K,N", [(1433, 128), (602, 128), (500, 128), (602, 256), (128, 64), (100, 128)])
+@pytest.mark.parametrize("M", [2708, 16384, 29000, 44625])
+def test_update_mm_hand_written_every_m(dev, M, K, N, dt):
+    """every UPDATE row count runs a hand-written kernel (hipBLASLt is gone):
+    GCN Cora's 2,708 rows (split-K ring slices + ordered slice sum), 16,384 / 29,000 / 44,625 rows
+    (an 8-way row shard of Reddit / Flickr-scale tables: the persistent ring), fp32 and fp32 x with
+    bf16 W (the bf16 ring), against the fp64 oracle on sampled rows (first, last, every 61st),
+    with RELU on one shape per dtype; two calls bitwise equal."""
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(M + K + N)
+    x = torch.randn(M, K, device=dev, generator=gen)
+    w = torch.randn(K, N, device=dev, generator=gen) / K ** 0.5
+    if dt == "mixed":
+        w = w.to(torch.bfloat16)
+    sf = "RELU" if (K, N) == (602, 128) else None
+    y = ops.update_mm(x, w, sf=sf)
+    y2 = ops.update_mm(x, w, sf=sf)
+    torch.cuda.synchronize()
+    assert torch.equal(y, y2)
+    rows = np.unique(np.concatenate([np.arange(0, M, 61), [M - 1]]))
+    xs = x[torch.from_numpy(rows).to(dev)].cpu()
+    if dt == "mixed":
+        xs = xs.to(torch.bfloat16).float()
+    xs = xs.numpy()
+    wf = w.float().cpu().numpy()
+    ref = isa_ref.mm(xs, wf, sf_kind=sf)
+    _check(y[torch.from_numpy(rows).to(dev)], ref, np.abs(xs).astype(np.float64) @ np.abs(wf).astype(np.float64),
+           f"UPDATE M={M} K={K} N={N} {dt}")
