@@ -2230,7 +2230,7 @@ template <int NT, int D = 3, int FR = 2>
 __global__ void __launch_bounds__(kBlock, ring_blocks(NT, D, FR))
 k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const float* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
-          int kslice = 0, int64_t slice_stride = 0, int lr = 1) {
+          int kslice = 0, int64_t slice_stride = 0) {
   static_assert(NT == 4 || NT == 8, "B fragments split evenly over the 4 waves");
   static_assert(FR == 1 || FR == 2, "one or two A fragments per wave");
   static_assert(D >= 3 && D <= 8, "ring depth");
@@ -2262,17 +2262,16 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   // otherwise the tail is a register step of 16 k with masked loads, paid synchronously per group
   const bool ring_tail = (K % KS) != 0 && (K % 4) == 0;
   const int S = ring_tail ? (K + KS - 1) / KS : K / KS;
-  // DMA lane map.  lr = 1 (row-contiguous): lane L fills row rr = L / 4 of a fragment with its
-  // 16-B piece cp = L % 4, so 4 consecutive lanes read one row's 64 contiguous bytes (a fragment
-  // instruction touches 16 row segments in 16 lane quads); the piece it carries is the logical
-  // k piece c = cp ^ ((rr >> 2) & 2), an XOR swizzle that keeps the fragment reads below
-  // conflict-free in every ds_read_b128 lane group.  lr = 0: lane (g, r) fills its own MFMA
-  // fragment (row r, piece g): 16 rows per 16 consecutive lanes.  Either way lane (g, r) reads
-  // logical piece g of row r: the values and the k order are the same (bitwise equal).
-  const int rr = lr ? lane >> 2 : r16;
-  const int cdma = lr ? (lane & 3) ^ ((rr >> 2) & 2) : g;  // logical 16-B k piece this lane DMAs
-  const uint32_t rdoff = lr ? static_cast<uint32_t>(r16 * 64 + ((g ^ ((r16 >> 2) & 2)) * 16))
-                            : static_cast<uint32_t>(lane) * 16u;
+  // DMA lane map (row-contiguous): lane L fills row rr = L / 4 of a fragment with its 16-B piece
+  // cp = L % 4, so 4 consecutive lanes read one row's 64 contiguous bytes; the piece it carries is
+  // the logical k piece c = cp ^ ((rr >> 2) & 2), an XOR swizzle that keeps the fragment reads
+  // below conflict-free in every ds_read_b128 lane group.  Lane (g, r) then reads logical piece g
+  // of row r: the values and k order of the former lane = fragment map (lane (g, r) DMAing its own
+  // piece: 16 rows per 16 consecutive lanes), bitwise equal and 1-4 % faster on every shape
+  // measured (profiles/r03/mm_dma_rows_ab.log).
+  const int rr = lane >> 2;
+  const int cdma = (lane & 3) ^ ((rr >> 2) & 2);  // logical 16-B k piece this lane DMAs
+  const uint32_t rdoff = static_cast<uint32_t>(r16 * 64 + ((g ^ ((r16 >> 2) & 2)) * 16));
   const bool dead = ring_tail && (S - 1) * KS + 4 * cdma >= K;  // this lane's DMA piece of the last stage
   const bool dead_rd = ring_tail && (S - 1) * KS + 4 * g >= K;  // the piece this lane reads
   const int64_t T = my_groups * S;
@@ -2481,8 +2480,7 @@ constexpr int ring_bf_blocks(int NT, int D, int FR, int SB, int PA) {  // blocks
 template <typename TA, int NT, int D = 3, int FR = 2, int SB = 4>
 __global__ void __launch_bounds__(kBlock, ring_bf_blocks(NT, D, FR, SB, sizeof(TA) == 4 ? 2 : 1))
 k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
-             const uint16_t* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
-             int lr = 1) {
+             const uint16_t* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo) {
   static_assert(NT == 4 || NT == 8, "column fragments");
   static_assert(FR == 1 || FR == 2, "one or two A fragments per wave");
   static_assert(D >= 3 && D <= 8, "ring depth");
@@ -2529,28 +2527,21 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     const int64_t m = min<int64_t>((grp0 + j * gstep) * GR + wv * (16 * FR) + 16 * i + sub, M - 1);
     return x + (row_idx ? static_cast<int64_t>(row_idx[m]) : m) * ldx;
   };
-  // DMA lane map (k_mm_ring's): lr = 1 (row-contiguous): DMA instruction p of a fragment holds
-  // rows RPI p .. RPI p + RPI - 1 (RPI = 8 fp32 / 16 bf16), LPR consecutive lanes reading one row's
-  // 32-k stage slice (128 / 64 contiguous bytes); lane L carries logical piece c = (L % LPR) ^
-  // swz(row), the XOR swizzle that keeps the fragment reads conflict-free in every ds_read_b128
-  // lane group.  lr = 0: lane (g, r) fills its own fragment (row r, k 8g + 4p).  The image holds
-  // a fragment's rows in order ([16][RB] bytes) under lr = 1, and lane (g, r) reads logical piece
-  // 2g + p (fp32) / g (bf16) of row r either way: same values, same k order.
+  // DMA lane map (row-contiguous, as k_mm_ring's): DMA instruction p of a fragment holds rows
+  // RPI p .. RPI p + RPI - 1 (RPI = 8 fp32 / 16 bf16), LPR consecutive lanes reading one row's 32-k
+  // stage slice (128 / 64 contiguous bytes); lane L carries logical piece c = (L % LPR) ^ swz(row),
+  // the XOR swizzle that keeps the fragment reads conflict-free in every ds_read_b128 lane group.
+  // The image holds a fragment's rows in order ([16][RB] bytes) and lane (g, r) reads logical piece
+  // 2g + p (fp32) / g (bf16) of row r: the values and k order of the lane = fragment map.
   constexpr int RB = 32 * static_cast<int>(sizeof(TA)), LPR = RB / 16, RPI = 64 / LPR;
   auto swz = [](int r) __attribute__((always_inline)) { return PA == 2 ? (r >> 1) & 5 : (r >> 2) & 2; };
   int drow[PA], doff[PA];  // per DMA instruction p: fragment row, element offset of the lane's piece
   uint32_t rdoff[PA];      // per read p: byte offset of logical piece (2g + p | g) of row r16
 #pragma unroll
   for (int p = 0; p < PA; ++p) {
-    if (lr) {
-      drow[p] = RPI * p + lane / LPR;
-      doff[p] = ((lane % LPR) ^ swz(drow[p])) * (16 / static_cast<int>(sizeof(TA)));
-      rdoff[p] = static_cast<uint32_t>(r16 * RB + (((PA == 2 ? 2 * g + p : g)) ^ swz(r16)) * 16);
-    } else {
-      drow[p] = r16;
-      doff[p] = 8 * g + 4 * p;
-      rdoff[p] = static_cast<uint32_t>(lane * 16 + p * 1024);
-    }
+    drow[p] = RPI * p + lane / LPR;
+    doff[p] = ((lane % LPR) ^ swz(drow[p])) * (16 / static_cast<int>(sizeof(TA)));
+    rdoff[p] = static_cast<uint32_t>(r16 * RB + (((PA == 2 ? 2 * g + p : g)) ^ swz(r16)) * 16);
   }
   const TA* asrc[FR][PA];
   int64_t asrc_j = -1, iss_j = 0;
@@ -2869,7 +2860,6 @@ struct Tuning {
   int mm_ring_fr = 0;      // k_mm_ring A fragments per wave: 2 = 128-row groups, 1 = 64-row groups, 0 = auto
   int mm_ring_depth = 0;   // k_mm_ring stages: 0 = auto (by blocks per CU), else 3, 4 or 8
   int mm_prefetch = 1;     // k_mm_rows A prefetch: 1 auto, 2 always, 0 never
-  int mm_dma_rows = 1;     // ring DMA lane map: 1 = row-contiguous lane quads/octets (swizzled image), 0 = lane = fragment
   int64_t mm_split = -1;   // UPDATE K slices: -1 auto, 0 = never split, n = n slices
 };
 
@@ -2928,7 +2918,6 @@ const Knob* find_knob(const char* key) {
       {"mm_ring_fr", &Tuning::mm_ring_fr, nullptr},
       {"mm_ring_depth", &Tuning::mm_ring_depth, nullptr},
       {"mm_prefetch", &Tuning::mm_prefetch, nullptr},
-      {"mm_dma_rows", &Tuning::mm_dma_rows, nullptr},
       {"mm_split", nullptr, &Tuning::mm_split},
   };
   const std::string k(key ? key : "");
@@ -3573,7 +3562,7 @@ void launch_ring(int nt, int D, int fr, dim3 gr, hipStream_t s, const float* x, 
                  int64_t slice_stride) {
 #define GTA_RING(NT_, D_, FR_)                                                                              \
   k_mm_ring<NT_, D_, FR_><<<gr, dim3(kBlock), 0, s>>>(x, ldx, row_idx, M, K, wt, ldwt, N, sf, out, ldo, kslice, \
-                                                      slice_stride, tuning().mm_dma_rows)
+                                                      slice_stride)
 #define GTA_RING_D(NT_, FR_) \
   if (D == 8) GTA_RING(NT_, 8, FR_); else if (D == 4) GTA_RING(NT_, 4, FR_); else GTA_RING(NT_, 3, FR_)
   if (nt == 8) { if (fr == 1) { GTA_RING_D(8, 1); } else { GTA_RING_D(8, 2); } }
@@ -3662,8 +3651,7 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   k_mm_ring_bf<TA_, NT_, D_, FR_, SB_><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const TA_*>(x), ldx, row_idx, M, \
                                                                           static_cast<int>(K),                       \
                                                                           static_cast<const uint16_t*>(wt), ldwt,    \
-                                                                          static_cast<int>(N), sf, out, ldo,         \
-                                                                          tuning().mm_dma_rows)
+                                                                          static_cast<int>(N), sf, out, ldo)
 #define GTA_RBF_F(TA_, NT_, SB_) \
   if (fr == 2) GTA_RBF(TA_, NT_, 3, 2, SB_); else GTA_RBF(TA_, NT_, 6, 1, SB_)
 #define GTA_RBF_S(TA_, NT_) if (sb == 4) { GTA_RBF_F(TA_, NT_, 4); } else { GTA_RBF_F(TA_, NT_, 8); }

@@ -513,7 +513,7 @@ def tile_nnz(graph, T):
 
 
 _KNOB_EPOCH = [0]  # bumped by every knob change: part of the executor's HIP-graph cache key
-_ATTACHED = set()  # raw stream handles with an attached knob set (the executor stays eager on them)
+_ATTACHED = {}  # raw stream handle -> id of the Tuning whose values it carries (the executor stays eager on them)
 
 
 def knob_epoch():
@@ -541,6 +541,8 @@ class Tuning:
     detach(stream) drops the stream's set.  Unknown keys raise GTAError.
     The set is keyed by the raw stream handle: detach before the stream is destroyed (a new stream
     may reuse the handle), and attaching to the null stream (0) governs every default-stream call.
+    A Tuning that is garbage-collected detaches the streams still carrying its values (not those
+    another Tuning attached to since).
     The executor's automatic HIP-graph replay stays eager on a stream with an attached set."""
 
     def __init__(self, **knobs):
@@ -568,13 +570,13 @@ class Tuning:
 
     def attach(self, stream):
         check(self._lib.gta_tuning_attach(self._ptr(stream), self._h), "tuning_attach")
-        _ATTACHED.add(self._ptr(stream))
+        _ATTACHED[self._ptr(stream)] = id(self)
         _KNOB_EPOCH[0] += 1
 
     @classmethod
     def detach(cls, stream):
         check(_L().gta_tuning_attach(cls._ptr(stream), None), "tuning_attach")
-        _ATTACHED.discard(cls._ptr(stream))
+        _ATTACHED.pop(cls._ptr(stream), None)
         _KNOB_EPOCH[0] += 1
 
     @staticmethod
@@ -584,5 +586,9 @@ class Tuning:
 
     def __del__(self):
         h, self._h = getattr(self, "_h", None), None
+        for sp in [sp for sp, owner in list(_ATTACHED.items()) if owner == id(self)]:
+            self._lib.gta_tuning_attach(sp, None)  # the stream no longer carries a dead set's values
+            _ATTACHED.pop(sp, None)
+            _KNOB_EPOCH[0] += 1
         if h:
             self._lib.gta_tuning_destroy(h)

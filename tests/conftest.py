@@ -32,3 +32,16 @@ def dev():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda:0")
+
+
+# Full-size GPU checks first: the metric kernel at Reddit size, the BASELINE-config
+# layers and the multi-rank bench run before the many small kernel-form tests, so an early `-x`
+# stop in a small test cannot hide them.  Order inside each group is kept.
+_FIRST = ("test_gpu_metric.py", "test_gpu_configs.py", "test_gpu_distributed.py")
+
+
+def pytest_collection_modifyitems(config, items):
+    def rank(item):
+        name = os.path.basename(str(item.fspath))
+        return _FIRST.index(name) if name in _FIRST else len(_FIRST)
+    items[:] = sorted(items, key=rank)  # stable: the rest keep their collection order

@@ -98,3 +98,23 @@ def test_tuning_handles(lib):
     del t                                                # the stream holds a copy: safe to destroy
     ops.Tuning.detach(fake_stream)
     ops.Tuning.detach(fake_stream)                       # detaching twice is harmless
+
+
+def test_tuning_detaches_its_streams_when_collected(lib):
+    """a garbage-collected Tuning detaches the streams still carrying its values,
+    but not a stream that another Tuning attached to since (stream pointers are only keys here)."""
+    import gc
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
+    s1, s2 = 0x7700010, 0x7700020
+    a = ops.Tuning(seg_lean=0)
+    a.attach(s1)
+    a.attach(s2)
+    b = ops.Tuning(seg_lean=1)
+    b.attach(s2)                                         # s2 now carries b's values
+    epoch = ops.knob_epoch()
+    del a
+    gc.collect()
+    assert not ops.Tuning.attached(s1) and ops.Tuning.attached(s2)
+    assert ops.knob_epoch() > epoch                      # cached HIP graphs keyed on knobs see the change
+    ops.Tuning.detach(s2)
+    del b

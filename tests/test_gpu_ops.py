@@ -697,17 +697,14 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     old_min = ops.MM_ROWS_MIN_M
     try:
         ops.MM_ROWS_MIN_M = 0
-        # k_mm_rows, then the ring with 128-row groups, 64-row groups, and the automatic choice, with
-        # the row-contiguous DMA lane map (default) and the lane = fragment map
-        for ring, fr, dma in ((0, 0, 1), (1, 2, 1), (1, 1, 1), (1, 0, 1), (1, 2, 0), (1, 1, 0)):
+        # k_mm_rows, then the ring with 128-row groups, 64-row groups, and the automatic choice
+        for ring, fr in ((0, 0), (1, 2), (1, 1), (1, 0)):
             ops.set_debug("mm_ring", ring)
             ops.set_debug("mm_ring_fr", fr)
-            ops.set_debug("mm_dma_rows", dma)
             outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
     finally:
         ops.set_debug("mm_ring", 1)
         ops.set_debug("mm_ring_fr", 0)
-        ops.set_debug("mm_dma_rows", 1)
         ops.MM_ROWS_MIN_M = old_min
     torch.cuda.synchronize()
     for o in outs[1:]:
@@ -828,13 +825,13 @@ def test_update_mm_split_ring_bitwise(dev, M, K, N, gathered, sf):
     idd = None if idx is None else idx.to(dev)
     outs = []
     try:
-        for ring, dma in ((0, 1), (1, 1), (1, 0)):
+        for ring, fr in ((0, 0), (1, 1), (1, 2)):
             ops.set_debug("mm_ring", ring)
-            ops.set_debug("mm_dma_rows", dma)
+            ops.set_debug("mm_ring_fr", fr)
             outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
     finally:
         ops.set_debug("mm_ring", 1)
-        ops.set_debug("mm_dma_rows", 1)
+        ops.set_debug("mm_ring_fr", 0)
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
     xs = x.numpy()[idx.numpy()] if gathered else x.numpy()[:M]
@@ -975,15 +972,13 @@ def test_update_mm_ring_bf_bitwise(dev, M, K, N, dt, gathered, sf):
     idd = None if idx is None else idx.to(dev)
     outs = []
     try:
-        for ring, fr, dma in ((0, 0, 1), (1, 1, 1), (1, 2, 1), (1, 1, 0), (1, 2, 0)):
+        for ring, fr in ((0, 0), (1, 1), (1, 2)):
             ops.set_debug("mm_ring", ring)
             ops.set_debug("mm_ring_fr", fr)
-            ops.set_debug("mm_dma_rows", dma)
             outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
     finally:
         ops.set_debug("mm_ring", 1)
         ops.set_debug("mm_ring_fr", 0)
-        ops.set_debug("mm_dma_rows", 1)
     torch.cuda.synchronize()
     for o in outs[1:]:
         assert torch.equal(outs[0], o)
