@@ -1018,3 +1018,49 @@ def test_update_mm_hand_written_every_m(dev, M, K, N, dt):
     ref = isa_ref.mm(xs, wf, sf_kind=sf)
     _check(y[torch.from_numpy(rows).to(dev)], ref, np.abs(xs).astype(np.float64) @ np.abs(wf).astype(np.float64),
            f"UPDATE M={M} K={K} N={N} {dt}")
+
+
+def _ring_vs_rows(dev, x, w, what):
+    """(ring output, k_mm_rows output): the default ring form and k_mm_rows on the same call."""
+    y_ring = ops.update_mm(x, w)
+    try:
+        ops.set_debug("mm_ring", 0)
+        y_rows = ops.update_mm(x, w)
+    finally:
+        ops.set_debug("mm_ring", 1)
+    torch.cuda.synchronize()
+    assert torch.equal(y_ring, y_rows), f"{what}: ring != k_mm_rows"
+    return y_ring
+
+
+@pytest.mark.parametrize("K", list(range(32, 65)))
+def test_update_mm_ring_every_k_tail(dev, K):
+    """Every K tail class of the fp32 ring (K % 16 = 0..15; K % 4 = 0 runs the tail as one more
+    ring stage whose pieces past K read the row start and are zeroed, other K a register step) with
+    the row-contiguous swizzled DMA lane map: bitwise equal to k_mm_rows, within the fp64 bound.
+    N = 72: a partial second column fragment."""
+    M, N = 3000, 72
+    rng = np.random.default_rng(K)
+    x = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32))
+    w = torch.from_numpy((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32))
+    y = _ring_vs_rows(dev, x.to(dev), w.to(dev), f"fp32 K={K}")
+    ref = isa_ref.mm(x.numpy(), w.numpy())
+    _check(y, ref, np.abs(x.numpy()).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), f"ring K={K}")
+
+
+@pytest.mark.parametrize("dt,K", [("mixed", k) for k in range(1, 97, 3)] + [("bf16", k) for k in range(8, 97, 8)])
+def test_update_mm_ring_bf_every_k_tail(dev, dt, K):
+    """The bf16 ring's K tails (32-k stages; a tail whose 16-B pieces lie wholly inside or past K
+    is one more ring stage, otherwise a masked register step) for fp32 x rounded to bf16 (K = 1,
+    4, ..., 94) and bf16 x (K = 8, ..., 96): bitwise equal to k_mm_rows, within the fp32 bound of
+    fp64 on the bf16-rounded operands."""
+    M, N = 2500, 128
+    rng = np.random.default_rng(K + 7)
+    x = torch.from_numpy(rng.standard_normal((M, K)).astype(np.float32))
+    w = torch.from_numpy((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32)).to(torch.bfloat16)
+    if dt == "bf16":
+        x = x.to(torch.bfloat16)
+    y = _ring_vs_rows(dev, x.to(dev), w.to(dev), f"{dt} K={K}")
+    xr = x.to(torch.bfloat16).float().numpy()
+    wf = w.float().numpy()
+    _check(y, isa_ref.mm(xr, wf), np.abs(xr).astype(np.float64) @ np.abs(wf).astype(np.float64), f"ring_bf {dt} K={K}")
