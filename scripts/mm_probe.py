@@ -20,6 +20,8 @@ SHAPES = {
     "cora_x": [(2708, 1433, 128, "f32"), (2708, 1432, 128, "f32")],
     "short_k": [(16384, 144, 128, "f32"), (16384, 137, 128, "f32"), (2816, 144, 128, "f32"), (2816, 1433, 128, "f32")],
     "k144": [(16384, 144, 128, "f32")],
+    "big_one": [(232965, 602, 128, "f32")],
+    "mid_one": [(16384, 1433, 128, "f32")],
     "mid": [(16384, 128, 128, "f32"), (29000, 602, 128, "f32"), (44625, 500, 128, "f32"), (29000, 602, 256, "f32"),
             (16384, 1433, 128, "f32"), (5000, 602, 128, "f32")],
     "big": [(232965, 602, 128, "f32"), (232965, 602, 256, "f32"), (89250, 500, 128, "f32"), (232965, 128, 128, "f32"),
