@@ -127,13 +127,14 @@ class Aggregate:
             self.launch(c)
             a, b, _ = self.parts[c]
             if self.mode == "edges" and self.pc > 1:
-                own = self.y_own[c * g.mk:(c + 1) * g.mk]
+                p0, p1 = g.part(c)
+                own = self.y_own[p0:p1]
                 if nccl:  # RCCL reduce-scatter among the pc ranks of this row group
                     works.append(dist.reduce_scatter_tensor(own, self.y[a:b], group=self.group, async_op=True))
                 else:     # gloo (CPU / one-GPU rehearsal): no reduce-scatter
                     part = self.y[a:b].clone()
                     dist.all_reduce(part, group=self.group)
-                    own.copy_(part[g.j * g.mk:(g.j + 1) * g.mk])
+                    own.copy_(part[g.j * (p1 - p0):(g.j + 1) * (p1 - p0)])
             elif self.mode == "rows" and self.world > 1:
                 w = self.world * g.mk
                 out = self.y_full[c * w:(c + 1) * w]
@@ -158,6 +159,16 @@ def build(args, world, rank, dev, backend, note):
     if mode == "rows" and pc != 1:
         raise SystemExit("--mode rows uses a PRx1 grid")
     chunks = args.row_chunks or (1 if world == 1 else 2)
+    # edges mode: the last chunk's reduce-scatter is the exchange left exposed after the last launch,
+    # so the chunks shrink toward the end (default 70 / 30 for two: the first chunk's exchange still
+    # hides under the second's compute at up to ~2x the modelled xGMI time)
+    fracs = None
+    if mode == "edges" and pc > 1 and chunks > 1:
+        cf = getattr(args, "chunk_fracs", "auto")
+        if cf == "auto":
+            fracs = [0.7, 0.3] if chunks == 2 else None
+        elif cf != "equal":
+            fracs = [float(v) for v in cf.split(",")]
     count_reduce = None
     if world > 1:
         def count_reduce(t):
@@ -174,7 +185,8 @@ def build(args, world, rank, dev, backend, note):
             ip2[:ip.numel()] = ip
             shard.graph = shard.grid.graph = G.Graph(ip2, shard.graph.indices, n_cols=shard.graph.n_cols)
     else:
-        shard = metric.Shard(args.n, args.e, rank, pr, pc, chunks, dev, count_reduce=count_reduce, note=note)
+        shard = metric.Shard(args.n, args.e, rank, pr, pc, chunks, dev, count_reduce=count_reduce, note=note,
+                             fracs=fracs)
     groups = None
     if mode == "edges" and pc > 1:
         groups = distributed.row_groups(pr, pc) if pr > 1 else [None]
@@ -405,6 +417,8 @@ def main():
                          "rows = destination-row tiles + RCCL all-gather of Y")
     ap.add_argument("--grid", default="auto", help="PRxPC rank grid (auto: 1x2, 2x2, 4x2; rows: Nx1)")
     ap.add_argument("--row-chunks", type=int, default=0, help="row chunks per tile for comm overlap (0 = auto)")
+    ap.add_argument("--chunk-fracs", default="auto",
+                    help="edges mode: relative row-chunk sizes, e.g. 0.7,0.3 ('equal'; 'auto' = 0.7,0.3 for two)")
     ap.add_argument("--impl", choices=["blocked", "plan"], default="blocked")
     ap.add_argument("--blocks", type=int, default=0, help="column blocks (0 = auto, ~6 MB X slices)")
     ap.add_argument("--n", "--graph-nodes", dest="n", type=int, default=N_REDDIT)
@@ -578,6 +592,7 @@ def main():
         "config": {"workload": "GAT layer-1 aggregate block [3,11,12] (scatter C -> applyedge MUL -> gather ADD)",
                    "graph": "reddit-shaped", "N": args.n, "E": args.e, "F": F, "heads": HEADS,
                    "parallelism": par, "mode": mode, "grid": f"{pr}x{pc}", "row_chunks": chunks,
+                   "chunk_rows": shard.grid.mks if mode == "edges" else None,
                    "impl": agg.impl, "blocks": agg.blocks if agg.impl == "blocked" else None,
                    "world_size_seen": dist.get_world_size() if world > 1 else 1,
                    "backend": (dist.get_backend() if world > 1 else None)},

@@ -357,16 +357,19 @@ class GridShard:
     partial aggregates with one reduce-scatter: rank (i, j) ends with rows
     R_i + j*m .. R_i + (j+1)*m of the block (m = ceil(n_i / pc); the CSR is padded to pc*m rows).
 
-    chunks = C > 1 lays the padded rows out chunk-major so the exchange can overlap the compute:
-    row R_i + j*m + c*mk + v (mk = ceil(m / C)) sits at padded row c*pc*mk + j*mk + v, so chunk c
-    is the contiguous [pc*mk] range holding one mk-row part per rank of the group -- one
-    reduce-scatter per chunk, issued while chunk c+1 aggregates.  Rank j's output is then
-    [C*mk] rows, part c at c*mk (owned_rows gives their global ids).
+    chunks = C > 1 lays the padded rows out chunk-major so the exchange can overlap the compute.
+    Chunk c covers rows [off_c, off_c+1) of each rank's block (mk_c = off_c+1 - off_c): row
+    R_i + j*m + off_c + v sits at padded row pc*off_c + j*mk_c + v, so chunk c is the contiguous
+    [pc*mk_c] range holding one mk_c-row part per rank of the group -- one reduce-scatter per
+    chunk, issued while chunk c+1 aggregates.  Rank j's output is then [off_C] rows, part c at
+    off_c (owned_rows gives their global ids).  Equal chunks (fracs None): off_c = c*mk with
+    mk = ceil(m / C) (the last part padded).  fracs (C weights): chunk sizes in that proportion, so
+    a smaller last chunk leaves less exchange exposed after the last launch.
 
     Built from a whole graph (GridShard(graph, ...)) or from the rank's row group alone
     (GridShard.from_rows: the multi-GPU bench, where no rank holds the whole graph)."""
 
-    def __init__(self, graph, rank, pr, pc, chunks=1):
+    def __init__(self, graph, rank, pr, pc, chunks=1, fracs=None):
         ip = graph.indptr
         rcuts = row_cuts_ip(ip, pr)
         ccuts = [int(c) for c in partition.column_cuts(graph, pc)]
@@ -374,18 +377,36 @@ class GridShard:
         r0, r1 = rcuts[i], rcuts[i + 1]
         e0, e1 = int(ip[r0]), int(ip[r1])
         self._build(rcuts, ccuts, rank, pr, pc, chunks, (ip[r0:r1 + 1] - e0).contiguous(),
-                    graph.indices[e0:e1].long(), e0)
+                    graph.indices[e0:e1].long(), e0, fracs)
 
     @classmethod
-    def from_rows(cls, rcuts, ccuts, rank, pr, pc, row_indptr, row_src, chunks=1, e0=0):
+    def from_rows(cls, rcuts, ccuts, rank, pr, pc, row_indptr, row_src, chunks=1, e0=0, fracs=None):
         """The shard from its row group only: row_indptr [n_i + 1] (local, from 0) and row_src (int64
         source column of each of the group's edges, columns sorted within rows); e0 = the group's
         first global edge id (edge_ids are global CSR ids, local_edge_ids index the group's edges)."""
         self = cls.__new__(cls)
-        self._build(list(rcuts), list(ccuts), rank, pr, pc, chunks, row_indptr, row_src, e0)
+        self._build(list(rcuts), list(ccuts), rank, pr, pc, chunks, row_indptr, row_src, e0, fracs)
         return self
 
-    def _build(self, rcuts, ccuts, rank, pr, pc, chunks, lip, src, e0):
+    @staticmethod
+    def chunk_offsets(m, chunks, fracs=None):
+        """[off_0 = 0, ..., off_C] of a block of m rows: equal chunks of ceil(m / C) (the last
+        padded past m), or sizes in proportion to fracs (sum = m, every chunk >= 1 row when m >= C)."""
+        if chunks <= 1:
+            return [0, m]
+        if fracs is None:
+            mk = -(-m // chunks)
+            return [c * mk for c in range(chunks + 1)]
+        if len(fracs) != chunks or min(fracs) <= 0:
+            raise ValueError(f"fracs must be {chunks} positive weights")
+        tot, acc, offs = float(sum(fracs)), 0.0, [0]
+        for c in range(chunks - 1):
+            acc += fracs[c]
+            offs.append(min(max(offs[-1] + (1 if m >= chunks else 0), int(round(m * acc / tot))),
+                            m - (chunks - 1 - c if m >= chunks else 0)))
+        return offs + [m]
+
+    def _build(self, rcuts, ccuts, rank, pr, pc, chunks, lip, src, e0, fracs=None):
         self.pr, self.pc, self.rank = pr, pc, rank
         self.i, self.j = divmod(rank, pc)
         self.rcuts, self.ccuts = rcuts, ccuts
@@ -395,7 +416,10 @@ class GridShard:
         self.r0, self.r1, self.c0, self.c1 = r0, r1, c0, c1
         self.m = max(1, -(-(r1 - r0) // pc))
         self.chunks = max(1, int(chunks))
-        self.mk = -(-self.m // self.chunks)
+        self.fracs = None if fracs is None or self.chunks == 1 else list(fracs)
+        self.offs = self.chunk_offsets(self.m, self.chunks, self.fracs)
+        self.mks = [b - a for a, b in zip(self.offs[:-1], self.offs[1:])]
+        self.mk = -(-self.m // self.chunks)  # the equal-chunk size (rows mode pads every rank's chunks to it)
         keep = (src >= c0) & (src < c1)
         deg = lip[1:] - lip[:-1]
         rows = torch.repeat_interleave(torch.arange(r1 - r0, device=dev), deg)[keep]
@@ -403,11 +427,13 @@ class GridShard:
         self.local_edge_ids = torch.nonzero(keep, as_tuple=False).flatten()
         if self.chunks > 1:  # chunk-major padded rows; a stable sort keeps each row's edge order
             jj, u = rows // self.m, rows % self.m
-            rows = (u // self.mk) * (pc * self.mk) + jj * self.mk + u % self.mk
+            offs = torch.tensor(self.offs, device=dev)
+            c = torch.searchsorted(offs, u, right=True) - 1
+            rows = pc * offs[c] + jj * (offs[c + 1] - offs[c]) + (u - offs[c])
             order = torch.sort(rows, stable=True).indices
             rows, local_src, self.local_edge_ids = rows[order], local_src[order], self.local_edge_ids[order]
         self.edge_ids = self.local_edge_ids + e0
-        n_pad = self.chunks * pc * self.mk
+        n_pad = pc * self.offs[-1]
         counts = torch.bincount(rows, minlength=n_pad)
         indptr = torch.zeros(n_pad + 1, dtype=torch.int64, device=dev)
         indptr[1:] = torch.cumsum(counts, 0)
@@ -415,23 +441,22 @@ class GridShard:
 
     def chunk_rows(self, c):
         """Padded row range [a, b) of chunk c: the input of its reduce-scatter."""
-        w = self.pc * self.mk
-        return c * w, (c + 1) * w
+        return self.pc * self.offs[c], self.pc * self.offs[c + 1]
+
+    def part(self, c):
+        """Row range [a, b) of chunk c inside this rank's reduce-scatter output."""
+        return self.offs[c], self.offs[c + 1]
 
     def out_rows(self):
-        """Rows of this rank's reduce-scatter output (chunks * mk; = m when chunks == 1)."""
-        return self.m if self.chunks == 1 else self.chunks * self.mk
+        """Rows of this rank's reduce-scatter output (off_C: = m when chunks == 1)."""
+        return self.offs[-1]
 
     def owned_rows(self, rank):
         """Global row ids of `rank`'s reduce-scatter output ([out_rows] rows; -1 = padding)."""
         i, j = divmod(rank, self.pc)
         r0, r1 = self.rcuts[i], self.rcuts[i + 1]
         m = max(1, -(-(r1 - r0) // self.pc))
-        if self.chunks == 1:
-            t = torch.arange(m) + r0 + j * m
-            return torch.where(t < r1, t, torch.full_like(t, -1))
-        mk = -(-m // self.chunks)
-        u = torch.arange(self.chunks * mk)  # c*mk + v
+        u = torch.arange(self.chunk_offsets(m, self.chunks, self.fracs)[-1])
         t = r0 + j * m + u
         return torch.where((u < m) & (t < r1), t, torch.full_like(t, -1))
 

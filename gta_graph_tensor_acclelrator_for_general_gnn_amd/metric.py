@@ -67,7 +67,7 @@ class Shard:
     although each rank generated only its rows."""
 
     def __init__(self, n, e, rank, pr, pc, chunks, device, seed=SEED, count_reduce=None, keep_rows=True,
-                 note=None):
+                 note=None, fracs=None):
         note = note or (lambda msg: None)
         self.n, self.e, self.seed, self.device = n, e, seed, device
         self.csr = G.CounterCSR(n, e, seed)
@@ -87,7 +87,8 @@ class Shard:
             del counts
         else:
             ccuts = [0, n]
-        self.grid = distributed.GridShard.from_rows(self.rcuts, ccuts, rank, pr, pc, lip, src, chunks, self.e0)
+        self.grid = distributed.GridShard.from_rows(self.rcuts, ccuts, rank, pr, pc, lip, src, chunks, self.e0,
+                                                    fracs=fracs)
         g = self.grid
         self.graph = g.graph
         self.alpha = alpha[g.local_edge_ids].contiguous()

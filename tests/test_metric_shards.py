@@ -83,13 +83,19 @@ def _global_counts(pr, pc):
     return lambda c: tot.clone()
 
 
-@pytest.mark.parametrize("pr,pc,chunks", [(1, 2, 1), (2, 2, 2), (4, 2, 2), (3, 1, 2), (1, 4, 3)])
-def test_grid_tiles_reassemble_to_the_whole_aggregate(pr, pc, chunks):
+@pytest.mark.parametrize("pr,pc,chunks,fracs", [(1, 2, 1, None), (2, 2, 2, None), (4, 2, 2, None), (3, 1, 2, None),
+                                                (1, 4, 3, None), (4, 2, 2, (0.7, 0.3)), (2, 2, 3, (0.5, 0.3, 0.2)),
+                                                (1, 2, 2, (0.9, 0.1))])
+def test_grid_tiles_reassemble_to_the_whole_aggregate(pr, pc, chunks, fracs):
+    """Every rank's tile aggregate, reduce-scattered chunk by chunk inside its row group, covers
+    each row exactly once and equals the whole-graph oracle; equal and weighted chunk sizes
+    (bench's default in edges mode: 70 / 30, the smaller chunk last)."""
     whole = metric.Shard(N, E, 0, 1, 1, 1, "cpu")
     ip, ix = whole.graph.numpy()
     ref = isa_ref.aggregate(ip, ix, whole.x.numpy(), "src", whole.alpha.numpy())
     world = pr * pc
-    shards = [metric.Shard(N, E, r, pr, pc, chunks, "cpu", count_reduce=_global_counts(pr, pc)) for r in range(world)]
+    shards = [metric.Shard(N, E, r, pr, pc, chunks, "cpu", count_reduce=_global_counts(pr, pc), fracs=fracs)
+              for r in range(world)]
     assert sum(s.graph.nnz for s in shards) == E
     partial = {}
     for r, s in enumerate(shards):
@@ -106,7 +112,9 @@ def test_grid_tiles_reassemble_to_the_whole_aggregate(pr, pc, chunks):
         for c in range(g.chunks):  # the reduce-scatter of chunk c inside row group i
             a, b = g.chunk_rows(c)
             tot = sum(partial[g.i * pc + jj][a:b] for jj in range(pc))
-            own.append(tot[g.j * g.mk:(g.j + 1) * g.mk])
+            p0, p1 = g.part(c)
+            assert (b - a) == pc * (p1 - p0)  # one equal part per rank of the group
+            own.append(tot[g.j * (p1 - p0):(g.j + 1) * (p1 - p0)])
         own = np.concatenate(own)
         rows = g.owned_rows(r).numpy()
         ok = rows >= 0
@@ -140,7 +148,8 @@ def _bench_worker(rank, world, port, mode, q, n=N, e=E):
         bench.Aggregate.launch = launch
         bench.ops.BlockedPlan.auto_blocks = staticmethod(lambda g, f: 1)   # single-pass plan, no device plan
         bench.G.Graph.plan = lambda self, chunk=512: None
-        args = types.SimpleNamespace(mode=mode, grid="auto", row_chunks=2, n=n, e=e, blocks=0, impl="plan")
+        args = types.SimpleNamespace(mode=mode, grid="auto", row_chunks=2, chunk_fracs="auto", n=n, e=e, blocks=0,
+                                     impl="plan")
         shard, agg, m, pr, pc, chunks = bench.build(args, world, rank, torch.device("cpu"), "gloo", lambda s: None)
         for _ in range(2):
             agg.step()
