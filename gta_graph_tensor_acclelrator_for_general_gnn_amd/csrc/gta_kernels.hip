@@ -844,7 +844,7 @@ k_att_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
           uint32_t row_bytes, const float* __restrict__ a, int64_t lda, const float* __restrict__ b,
           uint32_t brow_bytes, float* __restrict__ slabs, const SegItem* __restrict__ items,
           const int64_t* __restrict__ row_ptr = nullptr, int normalize = 1, float* __restrict__ y = nullptr,
-          int64_t ldy = 0, float* __restrict__ sums = nullptr) {
+          int64_t ldy = 0, float* __restrict__ sums = nullptr, int sf_out = GTA_SF_NONE) {
   constexpr int G = 32, U = 8, F = 128, LDS = F + 8;
   const int lane = threadIdx.x & (kWave - 1);
   const int l32 = lane & (G - 1);
@@ -931,6 +931,9 @@ k_att_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
       if (normalize) {
         v.x /= sh; v.y /= sh; v.z /= sh; v.w /= sh;
       }
+      if (sf_out != GTA_SF_NONE) {  // the layer's SF on y (GAT op 13), as the reduce applies it
+        v.x = sf_apply(sf_out, v.x); v.y = sf_apply(sf_out, v.y); v.z = sf_apply(sf_out, v.z); v.w = sf_apply(sf_out, v.w);
+      }
       *reinterpret_cast<float4*>(y + static_cast<int64_t>(it.row) * ldy + l32 * 4) = v;
       if (sums != nullptr && q == 0) sums[static_cast<int64_t>(it.row) * 8 + h] = sh;
       return;
@@ -1010,14 +1013,15 @@ k_seg_reduce(int64_t n_rows, const float* __restrict__ slabs, const float* __res
   o.store(yp);
 }
 
-// Ordered reduce of the attention form: y[row, c] = sum_k acc_k / sum_k s_k[head(c)]
-// (normalize; rows without edges get 0), or the numerator alone; sums[row, h] =
+// Ordered reduce of the attention form: y[row, c] = sf_out(sum_k acc_k / sum_k s_k[head(c)])
+// (normalize; rows without edges get sf_out(0)), or of the numerator alone; sums[row, h] =
 // sum_k s_k[h] when requested.  Slab rows hold F partials then H sums (stride F + H rounded up to 4);
-// same item order as k_seg_reduce.
+// same item order as k_seg_reduce.  sf_out: an SF applied to y (GTA_SF_NONE: none) -- the SF that
+// follows GAT's aggregate (op 13), fused so y is written once instead of twice.
 template <int VW>
 __global__ void __launch_bounds__(kBlock)
 k_seg_reduce_att(int64_t n_rows, const float* __restrict__ slabs, int H, int normalize, float* __restrict__ y,
-                 int64_t ldy, float* __restrict__ sums, RowItems ri, int skip_single = 0) {
+                 int64_t ldy, float* __restrict__ sums, RowItems ri, int skip_single = 0, int sf_out = GTA_SF_NONE) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
   if (row >= n_rows) return;
@@ -1046,6 +1050,10 @@ k_seg_reduce_att(int64_t n_rows, const float* __restrict__ slabs, int H, int nor
   Vec<VW> o;
 #pragma unroll
   for (int q = 0; q < VW; ++q) o.v[q] = normalize ? (any ? acc[q] / sh : 0.f) : acc[q];
+  if (sf_out != GTA_SF_NONE) {
+#pragma unroll
+    for (int q = 0; q < VW; ++q) o.v[q] = sf_apply(sf_out, o.v[q]);
+  }
   o.store(y + row * ldy + col);
   if (sums != nullptr && lane < H) sums[row * H + lane] = sl;
 }
@@ -3289,12 +3297,12 @@ int64_t gta_gat_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t nnz, i
 
 int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
                               int64_t nnz, const float* x, int64_t ldx, int64_t F, const float* a_dst, int64_t lda,
-                              const float* b_src, int64_t ldb, int64_t heads, int sf, int normalize, float* y,
-                              int64_t ldy, float* sums, const void* plan, int64_t blocks, int64_t item_edges,
+                              const float* b_src, int64_t ldb, int64_t heads, int sf, int normalize, int sf_out,
+                              float* y, int64_t ldy, float* sums, const void* plan, int64_t blocks, int64_t item_edges,
                               void* workspace, void* stream) {
   const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n_rows < 0 || nnz < 0 || blocks < 1 || blocks > 63 || heads <= 0 || lda < heads || ldb < heads ||
-      item_edges < 1)
+      item_edges < 1 || sf_out < GTA_SF_NONE || sf_out > GTA_SF_RECIP)
     return fail(GTA_ERR_ARG, "gat_aggregate_blocked: bad sizes");
   if (n_rows == 0) return GTA_OK;
   if (!indptr || !x || !a_dst || !b_src || !y || !plan || (!workspace && nnz > 0))
@@ -3337,7 +3345,7 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
     skip_single = direct;
     const int64_t* rp = direct ? v.row_ptr : nullptr;
     k_att_h32<2><<<g2h, blk, 0, s>>>(indices, nit, x, rb, a_dst, lda, b_src, bbytes, slabs, it, rp, normalize, y,
-                                     ldy, sums);  // NT bit 2: non-temporal slab stores
+                                     ldy, sums, sf_out);  // NT bit 2: non-temporal slab stores
   } else if (F == 128 && (F / heads) % 4 == 0 && lph32 >= 1 && 32 % lph32 == 0) {
     const dim3 g2h(static_cast<unsigned>((items + 2 * kWavesPerBlock - 1) / (2 * kWavesPerBlock)));
     if (elr) k_agg_seg4<4, 8, false, 0, true, GTA_SF_EXP_LEAKY_RELU, 32><<<g2h, blk, 0, s>>>(
@@ -3350,9 +3358,10 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
   }
   const dim3 g3(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
   const int H = static_cast<int>(heads);
-  if (F == 64) k_seg_reduce_att<1><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri);
-  else if (F == 128) k_seg_reduce_att<2><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri, skip_single);
-  else k_seg_reduce_att<4><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri);
+  if (F == 64) k_seg_reduce_att<1><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri, 0, sf_out);
+  else if (F == 128)
+    k_seg_reduce_att<2><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri, skip_single, sf_out);
+  else k_seg_reduce_att<4><<<g3, blk, 0, s>>>(n_rows, slabs, H, normalize, y, ldy, sums, ri, 0, sf_out);
   GTA_LAUNCHED("k_seg_reduce_att");
   return GTA_OK;
 }

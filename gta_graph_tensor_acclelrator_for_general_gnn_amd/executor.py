@@ -533,8 +533,9 @@ class Executor:
             found[M] = (pat, cons[M][0], S)
         return found
 
-    def _eval_attention(self, G2, M):
-        """G2 = gather(scatter_C(x) * alpha|v) as one fused launch; None if the shapes do not allow it."""
+    def _eval_attention(self, G2, M, sf_out=None):
+        """G2 = gather(scatter_C(x) * alpha|v) as one fused launch; None if the shapes do not allow it.
+        sf_out: the SF of G2's only consumer, applied as y is written (the caller owns that op's value)."""
         pat, _, S = self.attn[M]
         st = self._att_state.get(pat["A"])
         sv = self.values.get(S)
@@ -555,7 +556,8 @@ class Executor:
         G = pat["G"]
         gv = self.values.get(G)
         want = not norm and isinstance(gv, Lazy) and gv.v is None
-        y, sums = ops.gat_aggregate_blocked(self.graph, x, a, b, sf, normalize=norm, want_sums=want, blocks=B)
+        y, sums = ops.gat_aggregate_blocked(self.graph, x, a, b, sf, normalize=norm, want_sums=want, blocks=B,
+                                            sf_out=sf_out)
         E, n = self.graph.nnz, self.graph.n_rows
         self._count(E * (4 + 4 * F + 4 * H) + n * (8 + 4 * F + 4 * H))
         if want:
@@ -846,10 +848,34 @@ class Executor:
                 v = self._eval_mm_first(op, self.g.ops[self.reorder[op.idx]])
                 if v is not None:
                     return v
+            v = self._attention_with_sf(op, block)
+            if v is not None:
+                return v
             return self._gather_value(op)
         if op.type == "applynode":
             return self._eval_applynode(op)
         raise ValueError(op.type)
+
+    def _attention_with_sf(self, op, block):
+        """An attention gather whose only consumer is an applynode SF of the same block (GAT op 12 ->
+        op 13): one fused launch writes the SF's value (the reduce applies it as y is stored, bitwise
+        what apply_node computes); the gather's own value stays available, recomputed unfused if read."""
+        if not (self.fuse_sf and self.fuse_attention) or self.dist is not None or op.order != "R":
+            return None
+        src = self.g.inputs[op.idx][0]
+        if src.kind != "op" or src.op not in self.attn or not isinstance(self.values.get(src.op), (Deferred, Lazy)):
+            return None
+        cons = self.consumers[op.idx]
+        if len(cons) != 1:
+            return None
+        c = self.g.ops[cons[0]]
+        if c.comp != "SF" or c.type != "applynode" or c.idx not in block.ops or len(self.g.inputs[c.idx]) != 1:
+            return None
+        y = self._eval_attention(op, src.op, sf_out=self.sem.sf_of(c))
+        if y is None:
+            return None
+        self.values[c.idx] = y
+        return Lazy(lambda: self._gather_value(op))
 
     def _sf_child(self, op, block):
         """The SF op this op's output feeds exclusively (same kind, same block), if fusable."""

@@ -273,10 +273,11 @@ def blocked_ready(graph, blocks):
 
 
 def gat_aggregate_blocked(graph, x, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize=True, out=None, sums=None,
-                          want_sums=False, plan=None, blocks=16):
+                          want_sums=False, plan=None, blocks=16, sf_out=None):
     """Fused GAT attention aggregate (gta_gat_aggregate_blocked): with v = sf(a_dst[dst] + b_src[src]),
-    normalize: out[i] = sum_e v x[src] / sum_e v per head (GAT ops 6-12 without the SF); else the
-    numerator alone.  sums[i, h] = sum_e v (want_sums / sums given).  Returns (out, sums)."""
+    normalize: out[i] = sum_e v x[src] / sum_e v per head (GAT ops 6-12); else the numerator alone.
+    sf_out: an SF applied to out as it is written (GAT op 13; None = none), bitwise equal to
+    apply_node(None, sf_out, out).  sums[i, h] = sum_e v (want_sums / sums given).  Returns (out, sums)."""
     _need_gpu(x, a_dst, b_src, out, sums, graph.indptr)
     F, H = x.shape[1], a_dst.shape[1]
     if b_src.shape[1] != H:
@@ -298,7 +299,7 @@ def gat_aggregate_blocked(graph, x, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize
     ws = plan.workspace_att(F, H)
     check(_L().gta_gat_aggregate_blocked(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols,
                                          graph.nnz, _ptr(x), _rows(x, "x"), F, _ptr(a_dst), _rows(a_dst, "a_dst"), _ptr(b_src),
-                                         _rows(b_src, "b_src"), H, _sf(sf), 1 if normalize else 0, _ptr(out),
+                                         _rows(b_src, "b_src"), H, _sf(sf), 1 if normalize else 0, _sf(sf_out), _ptr(out),
                                          _rows(out, "out"), _ptr(sums), _ptr(plan.buf), plan.blocks, plan.item_edges,
                                          _ptr(ws),
                                          _stream(x.device)), "gat_aggregate_blocked")

@@ -37,11 +37,12 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 5  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+#define GTA_ABI_VERSION 6  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
                               hooks; 4: knob sets attached to streams (gta_tuning_*); 5: every UPDATE
                               on hand-written kernels (no vendor library), gta_update_mm_t_splits,
                               the blocked workspace is the slab rows alone and required, bf16
-                              rows in gta_aggregate (x_dtype) and gta_apply_node (a_dtype) */
+                              rows in gta_aggregate (x_dtype) and gta_apply_node (a_dtype);
+                              6: gta_gat_aggregate_blocked's sf_out (an SF applied to y) */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -179,6 +180,9 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
  *            = the GAT-original chain alpha = v / sum (ops 6-10), alpha * x (op 11), gather (op 12)
  * else:      y[i, c] = sum_e v(e, h(c)) x[src(e), c]     (GAT-trans numerator, op 10)
  * sums[i, h] = sum_e v(e, h) if sums != NULL (GAT-trans denominator, op 9).  h(c) = c / (F/heads).
+ * sf_out (ABI 6): GTA_SF_NONE, or an SF applied to every y element as it is written -- the
+ * applynode SF that follows the aggregate (GAT op 13, genGraphOP.py:64); rows without edges get
+ * sf_out(0).  Same function as gta_apply_node's SF: bitwise equal to y then gta_apply_node. 
  * Column-blocked like gta_aggregate_blocked (same plan; rows' columns sorted): the score
  * table b is gathered beside x from the same L2-resident slice and no [E, heads] tensor is
  * ever written.  workspace >= gta_gat_aggregate_blocked_workspace_bytes.  F in {64, 128,
@@ -188,8 +192,8 @@ int64_t gta_gat_aggregate_blocked_workspace_bytes(int64_t n_rows, int64_t nnz, i
                                                   int64_t heads, int64_t item_edges);
 int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
                               int64_t nnz, const float* x, int64_t ldx, int64_t F, const float* a_dst, int64_t lda,
-                              const float* b_src, int64_t ldb, int64_t heads, int sf, int normalize, float* y,
-                              int64_t ldy, float* sums, const void* plan, int64_t blocks, int64_t item_edges,
+                              const float* b_src, int64_t ldb, int64_t heads, int sf, int normalize, int sf_out,
+                              float* y, int64_t ldy, float* sums, const void* plan, int64_t blocks, int64_t item_edges,
                               void* workspace, void* stream);
 
 /* ---- K2 GATHER ADD (edge -> node) ---------------------------------------

@@ -48,9 +48,11 @@ def edge_softmax(graph, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize=True, out=N
 
 
 def gat_aggregate_blocked(graph, x, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize=True, out=None, sums=None,
-                          want_sums=False, plan=None, blocks=16):
+                          want_sums=False, plan=None, blocks=16, sf_out=None):
     ip, ix = graph.numpy()
     y, su = isa_ref.gat_aggregate(ip, ix, _np(x), _np(a_dst), _np(b_src), sf, normalize)
+    if sf_out is not None:
+        y = isa_ref.sf(sf_out, y)
     return _t(y), (_t(su) if (want_sums or sums is not None) else None)
 
 

@@ -1064,3 +1064,30 @@ def test_update_mm_ring_bf_every_k_tail(dev, dt, K):
     xr = x.to(torch.bfloat16).float().numpy()
     wf = w.float().numpy()
     _check(y, isa_ref.mm(xr, wf), np.abs(xr).astype(np.float64) @ np.abs(wf).astype(np.float64), f"ring_bf {dt} K={K}")
+
+
+@pytest.mark.parametrize("F,H", [(128, 8), (64, 4), (256, 8)])
+@pytest.mark.parametrize("blocks", [1, 2, 4])
+@pytest.mark.parametrize("sf_out", ["ELU", "RELU", "EXP", "SIGMOID"])
+@pytest.mark.parametrize("normalize", [True, False])
+def test_gat_aggregate_fused_output_sf(dev, F, H, blocks, sf_out, normalize):
+    """ABI 6 sf_out: the SF that follows GAT's aggregate (op 13) applied as y is written, by the
+    ordered reduce and by k_att_h32's direct epilogue (a row's only item, B <= 2): bitwise equal
+    to the aggregate followed by apply_node's SF, rows without edges included (sf(0)); per-head
+    sums untouched.  Lean (F = 128, 8 heads) and generic forms."""
+    n, e = 2000, 30000
+    rng = np.random.default_rng(F + blocks)
+    deg = np.diff(G.synthetic(n, e, seed=9).numpy()[0]).copy()
+    deg[3], deg[4], deg[5] = 0, 1, 2500
+    ip = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    ix = np.concatenate([np.sort(rng.integers(0, n, d)) for d in deg]).astype(np.int32)
+    g = G.from_numpy(ip, ix, device=dev)
+    x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(dev)
+    a = torch.from_numpy(rng.standard_normal((n, H)).astype(np.float32)).to(dev)
+    b = torch.from_numpy(rng.standard_normal((n, H)).astype(np.float32)).to(dev)
+    y0, s0 = ops.gat_aggregate_blocked(g, x, a, b, normalize=normalize, want_sums=True, blocks=blocks)
+    y1, s1 = ops.gat_aggregate_blocked(g, x, a, b, normalize=normalize, want_sums=True, blocks=blocks, sf_out=sf_out)
+    want = ops.apply_node(None, sf_out, y0)
+    torch.cuda.synchronize()
+    assert torch.equal(y1, want)
+    assert torch.equal(s0, s1)
