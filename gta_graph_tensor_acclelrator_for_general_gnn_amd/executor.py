@@ -857,9 +857,11 @@ class Executor:
         raise ValueError(op.type)
 
     def _attention_with_sf(self, op, block):
-        """An attention gather whose only consumer is an applynode SF of the same block (GAT op 12 ->
-        op 13): one fused launch writes the SF's value (the reduce applies it as y is stored, bitwise
-        what apply_node computes); the gather's own value stays available, recomputed unfused if read."""
+        """An attention gather whose only consumer is an applynode SF (GAT op 12 -> op 13): one fused
+        launch writes the SF's value (the reduce applies it as y is stored, bitwise what apply_node
+        computes); the gather's own value stays available, recomputed unfused if read.  The SF may sit
+        in a later block (GAT Reddit's stream puts op 13 in a block of its own): its block then finds
+        the value present, as for any fused post-op."""
         if not (self.fuse_sf and self.fuse_attention) or self.dist is not None or op.order != "R":
             return None
         src = self.g.inputs[op.idx][0]
@@ -869,7 +871,7 @@ class Executor:
         if len(cons) != 1:
             return None
         c = self.g.ops[cons[0]]
-        if c.comp != "SF" or c.type != "applynode" or c.idx not in block.ops or len(self.g.inputs[c.idx]) != 1:
+        if c.comp != "SF" or c.type != "applynode" or len(self.g.inputs[c.idx]) != 1:
             return None
         y = self._eval_attention(op, src.op, sf_out=self.sem.sf_of(c))
         if y is None:
