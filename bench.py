@@ -98,7 +98,9 @@ class Aggregate:
         self.blocks = blocks or ops.BlockedPlan.auto_blocks(self.parts[0][2], F)
         if impl == "blocked" and (self.blocks < 4 or not ops.BlockedPlan.supports(F, HEADS)):
             self.impl = "plan"
-        for _, _, gg in self.parts:
+        for a_, b_, gg in self.parts:
+            if b_ <= a_:
+                continue  # an empty chunk (a row block smaller than the chunk count): nothing to launch
             if self.impl == "blocked" and not gg.blocked_plan(self.blocks).sorted:
                 raise SystemExit("blocked aggregate needs sorted rows")
             if self.impl == "plan":
@@ -115,6 +117,8 @@ class Aggregate:
 
     def launch(self, c):
         a, b, gg = self.parts[c]
+        if b <= a:
+            return
         if self.impl == "blocked":
             ops.aggregate_blocked(gg, self.x, self.alpha, out=self.y[a:b], blocks=self.blocks)
         else:
@@ -126,6 +130,8 @@ class Aggregate:
         for c in range(len(self.parts)):
             self.launch(c)
             a, b, _ = self.parts[c]
+            if b <= a:
+                continue  # every rank of the row group has the same chunk offsets: all skip it
             if self.mode == "edges" and self.pc > 1:
                 p0, p1 = g.part(c)
                 own = self.y_own[p0:p1]

@@ -185,12 +185,14 @@ def _bench_worker(rank, world, port, mode, q, n=N, e=E):
 
 
 @pytest.mark.parametrize("world,mode,n,e", [(2, "edges", N, E), (4, "edges", N, E), (2, "rows", N, E),
-                                           (3, "rows", N, E), (8, "edges", N, E), (8, "edges", 400, 9)])
+                                           (3, "rows", N, E), (8, "edges", N, E), (8, "edges", 400, 9),
+                                           (8, "edges", 8, 20)])
 def test_bench_exchange_gloo(world, mode, n, e):
     """bench.py's N-rank step (gloo, oracle kernels): every rank's rows after the exchange match the
     fp64 oracle; in rows mode the gathered table is the whole Y.  World 8 runs the driver's 8-GPU
     layout, the 4 x 2 grid with one row-group sub-group per pair of ranks (distributed.row_groups),
-    every rank's owned rows checked; the 9-edge graph leaves ranks with empty tiles."""
+    every rank's owned rows checked; the 9-edge graph leaves ranks with empty tiles; the 8-row graph
+    gives row blocks of one row per rank, so the 70 / 30 chunking leaves an empty last chunk."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
