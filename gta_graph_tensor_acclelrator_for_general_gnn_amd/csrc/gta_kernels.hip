@@ -238,7 +238,10 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
             const TX* __restrict__ x, int64_t ldx, int F,
             const float* __restrict__ w, int64_t ldw, int gsz,
             const float* __restrict__ row_scale, float* __restrict__ y, int64_t ldy, int accumulate,
-            float* __restrict__ partial) {
+            float* __restrict__ partial, const TX* __restrict__ xs = nullptr, int64_t ldxs = 0,
+            const float* __restrict__ self_scale = nullptr) {
+  // xs (gta_aggregate_self): y[row] = self_scale * xs[row] + row_scale[row] * sum, the self term
+  // formed exactly as an applynode MUL by a broadcast scalar would (GIN op 3 + op 4)
   constexpr int EPI = kWave / LPE;                 // edges per wave instruction
   // row loads in flight per lane: ~64 B of each lane's rows per unrolled step
   constexpr int XB = NV * VW * static_cast<int>(sizeof(TX));
@@ -365,6 +368,12 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
             old.load(yp);
 #pragma unroll
             for (int k = 0; k < VW; ++k) o.v[k] = old.v[k] + scale * acc[v][k];
+          } else if (xs != nullptr) {
+            Vec<VW> sv;
+            load_row(sv, xs + row * ldxs + col[v]);
+            const float ss = self_scale ? *self_scale : 1.f;
+#pragma unroll
+            for (int k = 0; k < VW; ++k) o.v[k] = sv.v[k] * ss + scale * acc[v][k];
           } else {
 #pragma unroll
             for (int k = 0; k < VW; ++k) o.v[k] = scale * acc[v][k];
@@ -1380,7 +1389,8 @@ __global__ void k_items_permute(BlockedView v, int64_t n_rows, int B) {
 // sum the chunk partials of split rows, in chunk order
 __global__ void __launch_bounds__(kBlock)
 k_aggregate_combine(PlanView plan, int F, const float* __restrict__ row_scale, float* __restrict__ y, int64_t ldy,
-                    int accumulate, const float* __restrict__ partial) {
+                    int accumulate, const float* __restrict__ partial, const void* __restrict__ xs = nullptr,
+                    int64_t ldxs = 0, int xs_bf16 = 0, const float* __restrict__ self_scale = nullptr) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t s = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
   if (s >= plan.hdr[1]) return;
@@ -1392,7 +1402,13 @@ k_aggregate_combine(PlanView plan, int F, const float* __restrict__ row_scale, f
     float a = 0.f;
     for (int j = 0; j < cnt; ++j) a += partial[(first + j) * F + c];
     float* yp = y + row * ldy + c;
-    *yp = accumulate ? (*yp + scale * a) : scale * a;
+    if (xs != nullptr) {  // the self term, as k_aggregate forms it
+      const float xv = xs_bf16 ? load_elem(static_cast<const uint16_t*>(xs) + row * ldxs + c)
+                               : static_cast<const float*>(xs)[row * ldxs + c];
+      *yp = xv * (self_scale ? *self_scale : 1.f) + scale * a;
+    } else {
+      *yp = accumulate ? (*yp + scale * a) : scale * a;
+    }
   }
 }
 
@@ -2797,6 +2813,7 @@ struct AggArgs {
   const void* x; int64_t ldx; int F;
   const float* w; int64_t ldw; int gsz;
   const float* row_scale; float* y; int64_t ldy; int accumulate; float* partial;
+  const void* xs; int64_t ldxs; const float* self_scale;  // gta_aggregate_self's term (xs: x's dtype)
 };
 
 template <int LPE, int VW, int NV, int XM, int WM, typename TX>
@@ -2804,7 +2821,8 @@ void launch_agg(const AggArgs& a, int64_t n_items_bound, hipStream_t s) {
   const int64_t blocks = (n_items_bound + kWavesPerBlock - 1) / kWavesPerBlock;
   k_aggregate<LPE, VW, NV, XM, WM, TX><<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
       a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, a.x_is_row, static_cast<const TX*>(a.x), a.ldx, a.F,
-      a.w, a.ldw, a.gsz, a.row_scale, a.y, a.ldy, a.accumulate, a.partial);
+      a.w, a.ldw, a.gsz, a.row_scale, a.y, a.ldy, a.accumulate, a.partial, static_cast<const TX*>(a.xs), a.ldxs,
+      a.self_scale);
 }
 
 // (non-temporal index/weight loads measured +3 %: plain loads throughout)
@@ -3021,12 +3039,16 @@ int gta_aggregate_plan_build(const int64_t* indptr, int64_t n_rows, int64_t nnz,
   return GTA_OK;
 }
 
-int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int x_mode,
-                  const void* x, int64_t ldx, int64_t F, int x_dtype, const float* w, int64_t ldw, int64_t heads,
-                  const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
-                  int64_t plan_chunk, void* workspace, void* stream) {
+}  // extern "C"
+namespace {
+int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int x_mode,
+                   const void* x, int64_t ldx, int64_t F, int x_dtype, const float* w, int64_t ldw, int64_t heads,
+                   const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
+                   int64_t plan_chunk, void* workspace, void* stream, const void* xs, int64_t ldxs,
+                   const float* self_scale) {
   const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n_rows < 0 || nnz < 0 || F <= 0) return fail(GTA_ERR_ARG, "aggregate: bad sizes");
+  if (xs && (accumulate || ldxs < F)) return fail(GTA_ERR_ARG, "aggregate_self: no accumulate; ld_self >= F");
   if (x_mode != GTA_IDX_EDGE && x_mode != GTA_IDX_SRC && x_mode != GTA_IDX_DST)
     return fail(GTA_ERR_ARG, "aggregate: bad x_mode");
   if (x_dtype != GTA_F32 && x_dtype != GTA_BF16) return fail(GTA_ERR_ARG, "aggregate: x_dtype must be F32 or BF16");
@@ -3053,6 +3075,7 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
   // widest vector that keeps every access aligned
   auto ok_vw = [&](int vw) {
     if (F % vw || ldx % vw || ldy % vw || !aligned(x, xe * vw) || !aligned(y, 4 * vw)) return false;
+    if (xs && (ldxs % vw || !aligned(xs, xe * vw))) return false;
     if (wm == WM_HEAD && gsz % vw) return false;
     if (wm == WM_FULL && (ldw % vw || !aligned(w, 4 * vw))) return false;
     return true;
@@ -3081,6 +3104,7 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
   a.x = x; a.ldx = ldx; a.F = static_cast<int>(F); a.w = w; a.ldw = ldw; a.gsz = gsz;
   a.row_scale = row_scale; a.y = y; a.ldy = ldy; a.accumulate = accumulate;
   a.partial = static_cast<float*>(workspace);
+  a.xs = xs; a.ldxs = ldxs; a.self_scale = self_scale;
   int64_t bound = n_rows;
   if (plan) {
     if (plan_chunk <= 0 || !workspace) return fail(GTA_ERR_ARG, "aggregate: plan needs chunk and workspace");
@@ -3091,7 +3115,7 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
   bool ok = false;
   // lean path: one edge per instruction exactly filling the wave, SpMM form
   int gl = (wm == WM_HEAD) ? gsz / vw : 0;
-  const bool lean_shape = !bf && tuning().agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
+  const bool lean_shape = !bf && !xs && tuning().agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
                           !a.x_is_row && wm != WM_FULL && (wm == WM_NONE || gl == 4 || gl == 8 || gl == 16);
   if (lean_shape) {
     const int64_t blocks = (bound + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -3122,11 +3146,30 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
     if (sb > 0) {
       const int64_t blocks = (sb + kWavesPerBlock - 1) / kWavesPerBlock;
       k_aggregate_combine<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
-          a.plan, a.F, row_scale, y, ldy, accumulate, a.partial);
+          a.plan, a.F, row_scale, y, ldy, accumulate, a.partial, xs, ldxs, bf ? 1 : 0, self_scale);
       GTA_LAUNCHED("k_aggregate_combine");
     }
   }
   return GTA_OK;
+}
+}  // namespace
+extern "C" {
+
+int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int x_mode,
+                  const void* x, int64_t ldx, int64_t F, int x_dtype, const float* w, int64_t ldw, int64_t heads,
+                  const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
+                  int64_t plan_chunk, void* workspace, void* stream) {
+  return aggregate_impl(indptr, indices, n_rows, nnz, x_mode, x, ldx, F, x_dtype, w, ldw, heads, row_scale, y, ldy,
+                        accumulate, plan, plan_chunk, workspace, stream, nullptr, 0, nullptr);
+}
+
+int gta_aggregate_self(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int x_mode,
+                       const void* x, int64_t ldx, int64_t F, int x_dtype, const float* w, int64_t ldw, int64_t heads,
+                       const float* row_scale, const void* x_self, int64_t ld_self, const float* self_scale, float* y,
+                       int64_t ldy, const void* plan, int64_t plan_chunk, void* workspace, void* stream) {
+  if (!x_self) return fail(GTA_ERR_ARG, "aggregate_self: x_self is NULL");
+  return aggregate_impl(indptr, indices, n_rows, nnz, x_mode, x, ldx, F, x_dtype, w, ldw, heads, row_scale, y, ldy, 0,
+                        plan, plan_chunk, workspace, stream, x_self, ld_self, self_scale);
 }
 
 int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t item_edges) {

@@ -177,6 +177,7 @@ class Executor:
         #   available (recomputed on demand).
         self.gather_acc = dist is None or dist.local_rows or dist.s.world == 1
         self.gacc = self._match_gather_acc()
+        self.gacc_t = {T: A for A, (_, _, T) in self.gacc.items()}  # node op T -> its ADD consumer
 
     # ---------------------------------------------------------------- inputs
     def _ext(self, op, slot):
@@ -367,13 +368,37 @@ class Executor:
             found[A.idx] = (G.idx, 1 - gs, T.idx)
         return found
 
+    def _self_term(self, top):
+        """(x, s) when node op T = applynode MUL(x, s) of a node tensor x by a one-element scalar s
+        (GIN op 3: (1 + eps) x): the aggregate can form T itself (gta_aggregate_self).  Else None."""
+        if top.type != "applynode" or top.comp != "MUL" or self._binary(top) != "MUL":
+            return None
+        ins = self._inputs(top)
+        if len(ins) == 1:
+            extra = self._ext(top, 1)
+            ins = ins + ([self._wrap_ext(extra)] if extra is not None else [])
+        if len(ins) != 2:
+            return None
+        xs = [z for z in ins if isinstance(z, NodeT)]
+        rows = [z for z in ins if isinstance(z, tuple) and z[0] == "row"]
+        if len(xs) != 1 or len(rows) != 1 or rows[0][1].numel() != 1 or rows[0][1].dtype != torch.float32:
+            return None
+        return xs[0].t, rows[0][1]
+
     def _eval_gather_acc(self, A):
         """A = ADD(G, T) as G's aggregate accumulated into T's buffer; None if G's form cannot
-        accumulate (then A runs unfused)."""
+        accumulate (then A runs unfused).  When T = x * s (a scalar) and T was left unformed, the
+        aggregate forms it in its epilogue instead (no [N, F] T written and read back)."""
         G, slot_t, T = self.gacc[A.idx]
         raw = self.values.get(G)
         if not (isinstance(raw, Lazy) and raw.v is None):
             return None
+        tv = self.values.get(T)
+        if isinstance(tv, Lazy) and tv.v is None:
+            st = self._self_term(self.g.ops[T])
+            y = self._eval_gather(self.g.ops[G], self_term=st) if st is not None else None
+            if y is not None:
+                return y  # T stays unformed: recomputed by its own kernel if something reads it
         t = self._source(A, slot_t)
         if not isinstance(t, NodeT) or t.t.dtype != torch.float32 or not t.t.is_contiguous():
             return None
@@ -664,10 +689,32 @@ class Executor:
             x = x.float()
         return x, W
 
-    def _eval_gather(self, op, acc=None):
+    def _eval_gather(self, op, acc=None, self_term=None):
+        """self_term (x, s): y = x * s + the aggregate, or None if this gather's form cannot take it."""
         if op.order != "R":
             raise NotImplementedError("gather ORDER C (to source) is not emitted by genGraphOP")
         src = self.g.inputs[op.idx][0]
+        if self_term is not None:
+            v = self._source(op, 0) if not (self.fuse_attention and src.kind == "op" and src.op in self.attn) else None
+            if isinstance(v, Deferred):
+                p = self.g.ops[v.op]
+                pins = self._inputs(p)
+                if p.comp == "MM" or self._binary(p) != "MUL":
+                    return None
+                if len(pins) == 1:
+                    extra = self._ext(p, 1)
+                    pins = pins + ([self._wrap_ext(extra)] if extra is not None else [])
+                if len(pins) != 2:
+                    return None
+                y = self._weighted_aggregate(pins[0], pins[1], self_term=self_term)
+                return None if y is None else NodeT(y)
+            if isinstance(v, Scat):
+                y = self._spmm(v.t, v.mode, None, self_term=self_term)
+                if y is not None:
+                    n, E = self.graph.n_rows, self.graph.nnz
+                    self._count(E * (4 + v.t.shape[1] * v.t.element_size()) + n * (8 + v.t.shape[1] * 4))
+                    return NodeT(y)
+            return None
         if self.fuse_attention and src.kind == "op" and src.op in self.attn:
             raw = self.values.get(src.op)
             if isinstance(raw, (Deferred, Lazy)):
@@ -711,8 +758,9 @@ class Executor:
     def _plan(self):
         return self.plan_chunk if self.plan_chunk else None
 
-    def _weighted_aggregate(self, u, v, acc=None):
-        """sum_e u(e) (.) v(e): the wider operand is the feature row, the narrower the (head) weight."""
+    def _weighted_aggregate(self, u, v, acc=None, self_term=None):
+        """sum_e u(e) (.) v(e): the wider operand is the feature row, the narrower the (head) weight.
+        self_term: see _eval_gather (None back if this form cannot take it)."""
         n, E = self.graph.n_rows, self.graph.nnz
 
         def width(z):
@@ -722,6 +770,8 @@ class Executor:
 
         x, w = (u, v) if width(u) >= width(v) else (v, u)
         if isinstance(w, tuple) and w[0] == "row":  # constant row weight: aggregate then scale (linear)
+            if self_term is not None:
+                return None
             y = self._unweighted(x)
             return ops.apply_node("MUL", None, y, w[1], b_broadcast_row=True)
         wt = self._to_edge_tensor(w)
@@ -731,12 +781,21 @@ class Executor:
             xt, mode = self._to_edge_tensor(x), "edge"
         if xt.shape[1] % wt.shape[1]:
             raise ValueError(f"weighted aggregate: weight width {wt.shape[1]} does not divide {xt.shape[1]}")
-        y = self._spmm(xt, mode, wt, acc)
-        self._count(E * (4 + 4 * wt.shape[1] + 4 * xt.shape[1]) + n * (8 + 4 * xt.shape[1]))
+        y = self._spmm(xt, mode, wt, acc, self_term)
+        if y is None:
+            return None
+        self._count(E * (4 + 4 * wt.shape[1] + xt.element_size() * xt.shape[1]) + n * (8 + 4 * xt.shape[1]))
         return y
 
-    def _spmm(self, xt, mode, wt, acc=None):
-        """SpMM-form aggregate: column-blocked when the gathered table outgrows L2, else row-chunked."""
+    def _spmm(self, xt, mode, wt, acc=None, self_term=None):
+        """SpMM-form aggregate: column-blocked when the gathered table outgrows L2, else row-chunked.
+        self_term (x, s): y = x * s + the aggregate in one launch (row-chunked form; None back when
+        x's dtype is not the gathered table's)."""
+        if self_term is not None:
+            xs, sc = self_term
+            if xs.dtype != xt.dtype or xs.shape[1] != xt.shape[1] or xs.shape[0] < self.graph.n_rows:
+                return None
+            return ops.aggregate(self.graph, xt, mode, wt, plan=self._plan(), self_term=(xs, sc))
         heads = 0 if wt is None else wt.shape[1]
         if (mode == "src" and self.blocked_blocks and xt.shape[0] * xt.shape[1] * 4 >= self.blocked_min_table_bytes
                 and ops.BlockedPlan.supports(xt.shape[1], heads)):
@@ -853,6 +912,8 @@ class Executor:
                 return v
             return self._gather_value(op)
         if op.type == "applynode":
+            if self.gather_acc and op.idx in self.gacc_t and self._self_term(op) is not None:
+                return Lazy(lambda: self._eval_applynode(op))  # its ADD consumer's aggregate may form it
             return self._eval_applynode(op)
         raise ValueError(op.type)
 

@@ -94,8 +94,12 @@ class AggregatePlan:
         return int(self.buf[8:16].view(torch.int64).item())
 
 
-def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumulate=False, plan=None):
+def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumulate=False, plan=None, self_term=None):
     """y[i] (+)= row_scale[i] * sum_{e in row i} w(e) * x[idx(e)]  (K6/K7/K2).
+
+    self_term: None, or (x_self, s): y[i] = x_self[i] * s + row_scale[i] * sum (gta_aggregate_self,
+    no accumulate; x_self [>= N, F] of x's dtype, s a one-element float32 device tensor) -- bitwise
+    apply_node("MUL", x_self, s) followed by the accumulating aggregate (GIN ops 3-4).
 
     x_mode: "src" (x is [N_src, F], fused scatter C), "dst" (fused scatter R),
             "edge" (x is an edge tensor [E, F]).  x float32, or bfloat16 for "src" / "dst" with
@@ -143,6 +147,19 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
         if plan.graph is not graph:
             raise ValueError("plan built for another graph")
         pbuf, ws, chunk = plan.buf, plan.workspace(F), plan.chunk
+    if self_term is not None:
+        xs, sc = self_term
+        if accumulate or xs.dtype != x.dtype or xs.shape[0] < graph.n_rows or xs.shape[1] != F:
+            raise ValueError("aggregate self_term: x_self [N, F] of x's dtype, no accumulate")
+        if sc.dtype != torch.float32 or sc.numel() != 1:
+            raise ValueError("aggregate self_term: s must be a one-element float32 tensor")
+        _need_gpu(xs, sc)
+        ldxs = _rows(xs, "x_self", xs.dtype)
+        check(_L().gta_aggregate_self(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz, _MODES[x_mode],
+                                      _ptr(x), ldx, F, x_dt, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(xs), ldxs,
+                                      _ptr(sc.contiguous()), _ptr(out), ldy, _ptr(pbuf), chunk, _ptr(ws),
+                                      _stream(x.device)), "aggregate_self")
+        return out
     check(_L().gta_aggregate(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz, _MODES[x_mode],
                              _ptr(x), ldx, F, x_dt, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy,
                              int(bool(accumulate)), _ptr(pbuf), chunk, _ptr(ws), _stream(x.device)), "aggregate")

@@ -37,12 +37,13 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 6  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+#define GTA_ABI_VERSION 7  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
                               hooks; 4: knob sets attached to streams (gta_tuning_*); 5: every UPDATE
                               on hand-written kernels (no vendor library), gta_update_mm_t_splits,
                               the blocked workspace is the slab rows alone and required, bf16
                               rows in gta_aggregate (x_dtype) and gta_apply_node (a_dtype);
-                              6: gta_gat_aggregate_blocked's sf_out (an SF applied to y) */
+                              6: gta_gat_aggregate_blocked's sf_out (an SF applied to y); 7:
+                              gta_aggregate_self (the aggregate with a scaled self term) */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -133,6 +134,17 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
                   const float* w, int64_t ldw, int64_t heads,
                   const float* row_scale, float* y, int64_t ldy, int accumulate,
                   const void* plan, int64_t plan_chunk, void* workspace, void* stream);
+
+/* ABI 7: the aggregate with a self term, y[i, :] = self_scale[0] * x_self[i, :] + row_scale[i] *
+ * sum_{e in row i} w(e) x[idx(e), :] (no accumulate).  x_self has x's dtype and F columns (ld_self
+ * >= F); self_scale is a DEVICE pointer to one float (NULL = 1), so a captured graph follows it.
+ * The self term is formed as an applynode MUL by a broadcast scalar forms it: bitwise equal to
+ * gta_apply_node(MUL, x_self, s) into y, then gta_aggregate accumulating into y.  GIN ops 3-4
+ * (genGraphOP.py:99-103): agg + (1 + eps) x with no [N, F] intermediate. */
+int gta_aggregate_self(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int x_mode,
+                       const void* x, int64_t ldx, int64_t F, int x_dtype, const float* w, int64_t ldw, int64_t heads,
+                       const float* row_scale, const void* x_self, int64_t ld_self, const float* self_scale, float* y,
+                       int64_t ldy, const void* plan, int64_t plan_chunk, void* workspace, void* stream);
 
 /* plan/workspace sizing: chunk must be a positive multiple of 64 */
 int64_t gta_aggregate_plan_bytes(int64_t n_rows, int64_t nnz, int64_t chunk);

@@ -17,9 +17,16 @@ def _t(a):
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32))
 
 
-def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumulate=False, plan=None):
+SELF_TERM_CALLS = [0]  # aggregates that formed a self term (the executor's GIN ops 3-4 fusion)
+
+
+def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumulate=False, plan=None, self_term=None):
     ip, ix = graph.numpy()
     y = isa_ref.aggregate(ip, ix, _np(x), x_mode, _np(w), _np(row_scale))
+    if self_term is not None:
+        SELF_TERM_CALLS[0] += 1
+        xs, sc = self_term
+        y = _np(xs)[:graph.n_rows] * float(_np(sc).reshape(-1)[0]) + y
     if out is not None:
         y = y + (_np(out) if accumulate else 0)
         out.copy_(_t(y))

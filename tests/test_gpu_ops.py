@@ -1091,3 +1091,24 @@ def test_gat_aggregate_fused_output_sf(dev, F, H, blocks, sf_out, normalize):
     torch.cuda.synchronize()
     assert torch.equal(y1, want)
     assert torch.equal(s0, s1)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("F,heads", [(100, 1), (100, 0), (128, 8), (64, 0)])
+@pytest.mark.parametrize("plan", [None, 64])
+def test_aggregate_self_term(dev, dt, F, heads, plan):
+    """ABI 7 gta_aggregate_self: y = x_self * s + sum (GIN ops 3-4 in one launch) is bitwise equal to
+    apply_node("MUL", x_self, s) followed by the aggregate accumulating into it -- split rows
+    (plan 64: a 900-edge row across chunks, summed by the combine kernel) and empty rows included."""
+    n, e = 500, 9000
+    g, ip, ix = _graph(n, e, seed=F + heads, heavy_row=900, empty_rows=5, dev=dev)
+    rng = np.random.default_rng(F)
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(tdt).to(dev)
+    w = torch.from_numpy(rng.random((g.nnz, heads)).astype(np.float32)).to(dev) if heads else None
+    s = torch.tensor([[1.1]], device=dev)
+    t = ops.apply_node("MUL", None, x, s, b_broadcast_row=True)
+    want = ops.aggregate(g, x, "src", w, out=t, accumulate=True, plan=plan)
+    got = ops.aggregate(g, x, "src", w, plan=plan, self_term=(x, s))
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)

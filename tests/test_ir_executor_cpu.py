@@ -241,7 +241,11 @@ def test_gather_acc_fusion_cpu(golden_dir, manifest, monkeypatch):
             ex.gather_acc = on
             if on:
                 assert ex.gacc, "GIN's ADD(gather, MUL) not matched"
+            calls = fake_ops.SELF_TERM_CALLS[0]
             ex.run()
+            if on and len(st.blocks) < len(og):  # op 3 = (1 + eps) x formed by the aggregate's epilogue
+                assert fake_ops.SELF_TERM_CALLS[0] == calls + 1  # (gta_aggregate_self; a stream of one-op
+                # blocks materialises op 1's edge tensor, and the gather then accumulates into op 3)
             nbytes[on] = ex.alg_bytes
             compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
         assert nbytes[True] < nbytes[False]
