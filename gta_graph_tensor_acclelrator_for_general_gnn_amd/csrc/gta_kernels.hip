@@ -369,6 +369,8 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
 #pragma unroll
             for (int k = 0; k < VW; ++k) o.v[k] = old.v[k] + scale * acc[v][k];
           } else if (xs != nullptr) {
+#pragma clang fp contract(off)
+            // no fma contraction: each product rounded, as the unfused MUL and aggregate store them
             Vec<VW> sv;
             load_row(sv, xs + row * ldxs + col[v]);
             const float ss = self_scale ? *self_scale : 1.f;
@@ -429,7 +431,8 @@ __global__ void __launch_bounds__(kBlock)
 k_agg_lean(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows, PlanView plan,
            int use_plan, int64_t chunk, const float* __restrict__ x, int64_t ldx, int F,
            const float* __restrict__ w, int64_t ldw, const float* __restrict__ row_scale,
-           float* __restrict__ y, int64_t ldy, int accumulate, float* __restrict__ partial) {
+           float* __restrict__ y, int64_t ldy, int accumulate, float* __restrict__ partial,
+           const float* __restrict__ xs = nullptr, int64_t ldxs = 0, const float* __restrict__ self_scale = nullptr) {
   constexpr int U = (GL > 8) ? GL : 8;               // edges per unrolled step
   constexpr int NWL = (GL > 0) ? U / GL : 0;         // weight loads per step
   const int lane = threadIdx.x & (kWave - 1);
@@ -508,6 +511,13 @@ k_agg_lean(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indic
       old.load(yp);
 #pragma unroll
       for (int k = 0; k < VW; ++k) o.v[k] = old.v[k] + scale * acc[k];
+    } else if (xs != nullptr) {  // gta_aggregate_self's term, as k_aggregate forms it
+#pragma clang fp contract(off)
+      Vec<VW> sv;
+      sv.load(xs + row * ldxs + col);
+      const float ss = self_scale ? *self_scale : 1.f;
+#pragma unroll
+      for (int k = 0; k < VW; ++k) o.v[k] = sv.v[k] * ss + scale * acc[k];
     } else {
 #pragma unroll
       for (int k = 0; k < VW; ++k) o.v[k] = scale * acc[k];
@@ -1403,6 +1413,7 @@ k_aggregate_combine(PlanView plan, int F, const float* __restrict__ row_scale, f
     for (int j = 0; j < cnt; ++j) a += partial[(first + j) * F + c];
     float* yp = y + row * ldy + c;
     if (xs != nullptr) {  // the self term, as k_aggregate forms it
+#pragma clang fp contract(off)
       const float xv = xs_bf16 ? load_elem(static_cast<const uint16_t*>(xs) + row * ldxs + c)
                                : static_cast<const float*>(xs)[row * ldxs + c];
       *yp = xv * (self_scale ? *self_scale : 1.f) + scale * a;
@@ -3115,7 +3126,7 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
   bool ok = false;
   // lean path: one edge per instruction exactly filling the wave, SpMM form
   int gl = (wm == WM_HEAD) ? gsz / vw : 0;
-  const bool lean_shape = !bf && !xs && tuning().agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
+  const bool lean_shape = !bf && tuning().agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
                           !a.x_is_row && wm != WM_FULL && (wm == WM_NONE || gl == 4 || gl == 8 || gl == 16);
   if (lean_shape) {
     const int64_t blocks = (bound + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -3123,7 +3134,8 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
 #define GTA_LEAN(VW_, GL_)                                                                                   \
   k_agg_lean<VW_, GL_><<<grid, blk, 0, s>>>(a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, \
                                             static_cast<const float*>(a.x), a.ldx, a.F, a.w, a.ldw, a.row_scale, \
-                                            a.y, a.ldy, a.accumulate, a.partial)
+                                            a.y, a.ldy, a.accumulate, a.partial, static_cast<const float*>(a.xs), \
+                                            a.ldxs, a.self_scale)
     if (vw == 2) {
       if (gl == 0) GTA_LEAN(2, 0); else if (gl == 4) GTA_LEAN(2, 4); else if (gl == 8) GTA_LEAN(2, 8); else GTA_LEAN(2, 16);
     } else if (vw == 4) {
