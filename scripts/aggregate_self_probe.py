@@ -1,3 +1,5 @@
+"""gta_aggregate_self (GIN ops 3-4 in one launch) against apply_node MUL then the aggregate then ADD,
+bitwise, for widths that take each aggregate kernel form (lean F = 128, generic LPE = 64 with NV 2/4)."""
 import os, sys
 import numpy as np
 import torch
@@ -16,7 +18,6 @@ for F in (602, 128, 600, 604, 300):
     Gv = ops.aggregate(g, x, "src", w)
     A1 = ops.apply_node("ADD", None, Gv, T)
     A2 = ops.aggregate(g, x, "src", w, self_term=(x, s))
-    T2 = ops.aggregate(G.from_numpy(np.zeros(g.n_rows + 1, np.int64), np.zeros(0, np.int32), device=dev), x, "src", None, self_term=(x, s)) if False else None
     torch.cuda.synchronize()
     print(F, "T==x*s", torch.equal(T, x * torch.tensor(1.1, device=dev)), "A1==A2", torch.equal(A1, A2),
           "A1==G+T", torch.equal(A1, Gv + T), "A2==G+T", torch.equal(A2, Gv + T), flush=True)
