@@ -98,8 +98,9 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
     """y[i] (+)= row_scale[i] * sum_{e in row i} w(e) * x[idx(e)]  (K6/K7/K2).
 
     self_term: None, or (x_self, s): y[i] = x_self[i] * s + row_scale[i] * sum (gta_aggregate_self,
-    no accumulate; x_self [>= N, F] of x's dtype, s a one-element float32 device tensor) -- bitwise
-    apply_node("MUL", x_self, s) followed by the accumulating aggregate (GIN ops 3-4).
+    no accumulate; x_self [>= N, F] of x's dtype, s a one-element float32 device tensor) -- without
+    row_scale bitwise apply_node("MUL", x_self, s) followed by the accumulating aggregate (GIN ops
+    3-4); with row_scale the scaled sum is rounded before the add.
 
     x_mode: "src" (x is [N_src, F], fused scatter C), "dst" (fused scatter R),
             "edge" (x is an edge tensor [E, F]).  x float32, or bfloat16 for "src" / "dst" with

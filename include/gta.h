@@ -138,8 +138,10 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
 /* ABI 7: the aggregate with a self term, y[i, :] = self_scale[0] * x_self[i, :] + row_scale[i] *
  * sum_{e in row i} w(e) x[idx(e), :] (no accumulate).  x_self has x's dtype and F columns (ld_self
  * >= F); self_scale is a DEVICE pointer to one float (NULL = 1), so a captured graph follows it.
- * The self term is formed as an applynode MUL by a broadcast scalar forms it: bitwise equal to
- * gta_apply_node(MUL, x_self, s) into y, then gta_aggregate accumulating into y.  GIN ops 3-4
+ * The self term is formed as an applynode MUL by a broadcast scalar forms it, each product rounded
+ * (no fma contraction): with row_scale NULL, bitwise equal to gta_apply_node(MUL, x_self, s) into y
+ * then gta_aggregate accumulating into y; with row_scale, the scaled sum is rounded before the add
+ * (the unfused scaled aggregate, then ADD).  GIN ops 3-4
  * (genGraphOP.py:99-103): agg + (1 + eps) x with no [N, F] intermediate. */
 int gta_aggregate_self(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int x_mode,
                        const void* x, int64_t ldx, int64_t F, int x_dtype, const float* w, int64_t ldw, int64_t heads,
