@@ -22,11 +22,38 @@ Returns ExecResult(values per op, outputs of sink ops, elapsed_s, alg_bytes).
 """
 import os
 import time
+import weakref
 
 import torch
 
 from . import ir, ops
 from .semantics import Semantics
+
+
+# [W | W_s1 | ...] column concatenations of sibling weights, cached per source-weight objects and
+# versions (weak references: an address alone is never the key), so a forward reuses one tensor --
+# and ops._transposed its W^T -- instead of a cat + W^T per call.  Entries are only made outside a
+# HIP graph capture; a capture that reads one records (sources, concatenation) in _CAPTURED_WCAT,
+# and GraphedRun re-concatenates it when a source weight changes in place.
+_WCAT = {}
+_CAPTURED_WCAT = []
+
+
+def _sibling_cat(srcs):
+    key = tuple(id(w) for w in srcs)
+    vers = tuple(w._version for w in srcs)
+    capturing = srcs[0].is_cuda and torch.cuda.is_current_stream_capturing()
+    ent = _WCAT.get(key)
+    if ent is not None and ent[1] == vers and all(r() is w for r, w in zip(ent[0], srcs)):
+        if capturing:
+            _CAPTURED_WCAT.append((list(srcs), ent[2]))
+        return ent[2]
+    Wc = torch.cat(srcs, dim=1).contiguous()
+    if not capturing:  # a tensor from the capture's private pool is never handed to eager runs
+        if len(_WCAT) >= 64:
+            _WCAT.clear()
+        _WCAT[key] = (tuple(weakref.ref(w) for w in srcs), vers, Wc)
+    return Wc
 
 
 class NodeT:
@@ -169,7 +196,6 @@ class Executor:
         #   sibling_mm: applynode MMs that multiply the same node tensor run as ONE GEMM over the
         #   concatenated weights (x read once; e.g. GraphSAGE's x W3 and x W4, GAT's scores W1, W2)
         self.sibling_mm = True
-        self._wcat = {}
         self.pushdown = self._match_pushdown()
         #   gather_acc: applynode ADD(gather G, node op T), each the other's only reader (GIN op 4:
         #   agg + (1+eps) x), runs as the aggregate accumulating into T's fresh output buffer:
@@ -474,11 +500,7 @@ class Executor:
             out = ops.update_mm(x2, W2, sf=post_sf)
             self._count(x.shape[0] * (x.shape[1] * x.element_size() + W.shape[1] * 4) + W.numel() * W.element_size())
             return out
-        key = (main_idx,) + tuple(o.idx for o in sibs)
-        Wc = self._wcat.get(key)
-        if Wc is None:
-            Wc = torch.cat([W] + [self.tensors[f"w:{o.idx}"] for o in sibs], dim=1).contiguous()
-            self._wcat[key] = Wc
+        Wc = _sibling_cat([W] + [self.tensors[f"w:{o.idx}"] for o in sibs])
         x2, Wc2 = self._mm_dtypes(x, Wc)
         out = ops.update_mm(x2, Wc2)
         self._count(x.shape[0] * (x.shape[1] * x.element_size() + Wc.shape[1] * 4) + Wc.numel() * Wc.element_size())
@@ -1283,8 +1305,8 @@ class GraphedRun:
     Flickr) are where it matters.  Inputs are the tensors given here (static addresses: update
     them in place between replays); outputs are the same tensors after every replay.  The
     warm-up run builds every plan, workspace and W^T cache outside the capture.  The graph keeps
-    the W^T tensors it reads alive, and a weight changed in place (its version moved) is
-    re-transposed into them before the next replay."""
+    the W^T tensors (and sibling-weight concatenations) it reads alive, and a weight changed in
+    place (its version moved) is re-concatenated / re-transposed into them before the next replay."""
 
     def __init__(self, opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, warmup=2):
         if graph.device.type != "cuda":
@@ -1299,16 +1321,28 @@ class GraphedRun:
         torch.cuda.synchronize(graph.device)
         self.cuda_graph = torch.cuda.CUDAGraph()
         del ops._CAPTURED_WT[:]
+        del _CAPTURED_WCAT[:]
         try:
             with torch.cuda.graph(self.cuda_graph):
                 self.executor = Executor(opgraph, stream, graph, tensors, semantics, plan_chunk)
                 self.outputs = self.executor.run()
         finally:
             taken, ops._CAPTURED_WT[:] = list(ops._CAPTURED_WT), []
+            cats, _CAPTURED_WCAT[:] = list(_CAPTURED_WCAT), []
+        # (sibling weights, their concatenation read by the graph, the versions it holds); refreshed
+        # before the W^T below, so a re-concatenation moves Wc's version and re-transposes it too
+        self._wcats = [[srcs, wc, tuple(w._version for w in srcs)]
+                       for srcs, wc in {id(wc): (srcs, wc) for srcs, wc in cats}.values()]
         # (weight, its W^T read by the graph, the weight version that W^T holds)
         self._wts = [[w, wt, w._version] for w, wt in {id(wt): (w, wt) for w, wt in taken}.values()]
 
     def replay(self):
+        for ent in self._wcats:
+            srcs, wc, vers = ent
+            now = tuple(w._version for w in srcs)
+            if now != vers:  # a sibling weight changed in place: re-concatenate into the graph's copy
+                wc.copy_(torch.cat(srcs, dim=1))
+                ent[2] = now
         for ent in self._wts:
             w, wt, ver = ent
             if w._version != ver:  # changed in place since the capture: refresh the graph's W^T

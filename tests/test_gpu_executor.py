@@ -343,6 +343,35 @@ def test_graphed_run_follows_weights_changed_in_place(golden_dir, manifest, cora
             assert torch.equal(out[k], ref[k]), (k, trial)
 
 
+def test_graphed_run_follows_sibling_weights_changed_in_place(golden_dir, manifest, cora, dev):
+    """GAT's sibling MMs read one cached [W | W_s] concatenation (and its cached W^T) inside the
+    captured graph; a sibling weight changed in place between replays is re-concatenated and
+    re-transposed before the next replay, which then equals a fresh eager run bitwise."""
+    rec = [s for s in _all_streams(manifest) if s["network"] == "GAT" and not s["reorder"]
+           and s["dataset"] == "cora"][0]
+    sem = Semantics.for_network("GAT", False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    ip, ix = cora
+    gd = G.from_numpy(ip, ix, device=dev)
+    tensors = {k: v.to(dev) for k, v in workloads.make_tensors(og, G.from_numpy(ip, ix), "GAT", seed=4).items()}
+    gr = executor.GraphedRun(og, st, gd, tensors, sem)
+    assert gr._wcats, "the captured graph reads a cached sibling concatenation"
+    srcs, wc, _ = gr._wcats[0]
+    assert any(wt is not None for w, wt, _ in gr._wts if w is wc), "and its cached W^T"
+    first = {k: v.clone() for k, v in gr.replay().items()}
+    ref = executor.Executor(og, st, gd, tensors, sem).run()
+    for k in ref:
+        assert torch.equal(first[k], ref[k]), k
+    for trial, w in enumerate([srcs[-1], srcs[0], srcs[-1]]):  # a sibling, the main weight, a sibling
+        w.mul_(-0.5 - 0.25 * trial)
+        out = {k: v.clone() for k, v in gr.replay().items()}
+        ref = executor.Executor(og, st, gd, tensors, sem).run()
+        for k in ref:
+            assert torch.equal(out[k], ref[k]), (k, trial)
+        assert not all(torch.equal(out[k], first[k]) for k in ref), trial
+
+
 def test_gin_bf16_model_input_on_gpu(golden_dir, manifest, cora, dev):
     """GIN with the bf16 model input (the gin-products configuration's storage) on the real kernels:
     the bf16-row aggregate accumulating into (1+eps) x (bf16 apply_node), the bf16 MFMA MLP;

@@ -268,3 +268,30 @@ def test_gin_bf16_model_input_cpu(golden_dir, manifest, monkeypatch):
     ex = executor.Executor(og, st, gc, tensors, sem)
     ex.run()
     compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
+
+
+def test_sibling_weight_concat_is_cached_and_follows_in_place_updates(golden_dir, manifest, monkeypatch):
+    """GAT's sibling MMs of x (W and the attention projections) share one [W | W_s] concatenation:
+    a second forward reuses the cached tensor (no cat, and so no new W^T), and a sibling weight
+    changed in place makes the next forward re-concatenate (results follow the oracle)."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    executor._WCAT.clear()
+    rec = [s for s in _streams(manifest) if s["network"] == "GAT" and not s["reorder"]][0]
+    sem = Semantics.for_network("GAT", False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    g, ip, ix = _cora_graph(golden_dir)
+    tensors = workloads.make_tensors(og, g, "GAT", seed=5)
+    executor.Executor(og, st, g, tensors, sem, plan_chunk=0).run()
+    assert len(executor._WCAT) == 1
+    (refs, vers, wc), = executor._WCAT.values()
+    executor.Executor(og, st, g, tensors, sem, plan_chunk=0).run()
+    assert next(iter(executor._WCAT.values()))[2] is wc  # reused, not rebuilt
+    sib = refs[-1]()
+    sib.mul_(-0.75)  # in place: the version moves, the cached concatenation is stale
+    ex = executor.Executor(og, st, g, tensors, sem, plan_chunk=0)
+    ex.run()
+    wc2 = [e[2] for e in executor._WCAT.values() if e[0][-1]() is sib][0]
+    assert wc2 is not wc and torch.equal(wc2[:, -sib.shape[1]:], sib)
+    ref = execute_ref(og, sem, ip, ix, {k: v.numpy() for k, v in tensors.items()})
+    compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
