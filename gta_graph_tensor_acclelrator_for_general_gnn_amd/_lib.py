@@ -10,7 +10,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgta.so")
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 # enum mirrors of include/gta.h
 GTA_F32, GTA_BF16, GTA_F32_BF16 = 0, 1, 2
@@ -49,7 +49,7 @@ SIGNATURES = {
     "gta_apply_node": (_i32, [_i32, _i32, _i64, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _vp, _i64, _vp]),
     "gta_update_mm": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
     "gta_update_mm_t": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
-    "gta_update_mm_t_splits": (_i64, [_i64, _i64, _i64, _i32]),
+    "gta_update_mm_t_splits": (_i64, [_i64, _i64, _i64, _i32, _vp]),
     "gta_update_mm_t_split_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
     "gta_update_mm_t_split": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _i64, _vp,
                                      _i64, _vp]),

@@ -3651,7 +3651,8 @@ inline int64_t mm_kslice(int64_t K, int64_t splits) {
 }
 }  // namespace
 
-int64_t gta_update_mm_t_splits(int64_t M, int64_t K, int64_t N, int dtype) {
+int64_t gta_update_mm_t_splits(int64_t M, int64_t K, int64_t N, int dtype, void* stream) {
+  const CallTuning ct_(stream);  // the stream's attached knob set decides mm_split, as for the GEMM itself
   if (M < 0 || K <= 0 || N <= 0) return fail(GTA_ERR_ARG, "update_mm_t_splits: bad sizes");
   if (tuning().mm_split >= 0) return std::max<int64_t>(1, tuning().mm_split);
   const int nt = mm_nt(N);

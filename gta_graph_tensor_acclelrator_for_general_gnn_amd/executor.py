@@ -812,22 +812,31 @@ class Executor:
     def _spmm(self, xt, mode, wt, acc=None, self_term=None):
         """SpMM-form aggregate: column-blocked when the gathered table outgrows L2, else row-chunked.
         self_term (x, s): y = x * s + the aggregate in one launch (row-chunked form; None back when
-        x's dtype is not the gathered table's)."""
+        x's dtype is not the gathered table's, or when the column-blocked form is the better one:
+        the caller then accumulates into the formed x * s instead)."""
+        B = self._blocked_blocks(xt, mode, 0 if wt is None else wt.shape[1])
         if self_term is not None:
             xs, sc = self_term
-            if xs.dtype != xt.dtype or xs.shape[1] != xt.shape[1] or xs.shape[0] < self.graph.n_rows:
+            if B or xs.dtype != xt.dtype or xs.shape[1] != xt.shape[1] or xs.shape[0] < self.graph.n_rows:
                 return None
             return ops.aggregate(self.graph, xt, mode, wt, plan=self._plan(), self_term=(xs, sc))
-        heads = 0 if wt is None else wt.shape[1]
-        if (mode == "src" and self.blocked_blocks and xt.shape[0] * xt.shape[1] * 4 >= self.blocked_min_table_bytes
-                and ops.BlockedPlan.supports(xt.shape[1], heads)):
-            B = self.blocked_blocks
-            if B == "auto":
-                B = ops.BlockedPlan.auto_blocks(self.graph, xt.shape[1])
-                B = B if B >= 4 else 0
-            if B and self.graph.blocked_plan(B).sorted:
-                return ops.aggregate_blocked(self.graph, xt, wt, out=acc, accumulate=acc is not None, blocks=B)
+        if B:
+            return ops.aggregate_blocked(self.graph, xt, wt, out=acc, accumulate=acc is not None, blocks=B)
         return ops.aggregate(self.graph, xt, mode, wt, out=acc, accumulate=acc is not None, plan=self._plan())
+
+    def _blocked_blocks(self, xt, mode, heads):
+        """Column blocks of the blocked aggregate for this gathered table, or 0 for the row-chunked
+        form: a source table of at least blocked_min_table_bytes (its own element size) of a dtype
+        and width the blocked kernels take."""
+        if not (mode == "src" and self.blocked_blocks and xt.dtype in ops.BlockedPlan.DTYPES
+                and xt.shape[0] * xt.shape[1] * xt.element_size() >= self.blocked_min_table_bytes
+                and ops.BlockedPlan.supports(xt.shape[1], heads, xt.dtype)):
+            return 0
+        B = self.blocked_blocks
+        if B == "auto":
+            B = ops.BlockedPlan.auto_blocks(self.graph, xt.shape[1], xt.element_size())
+            B = B if B >= 4 else 0
+        return B if B and self.graph.blocked_plan(B).sorted else 0
 
     def _unweighted(self, x):
         if isinstance(x, Scat):
@@ -1117,7 +1126,7 @@ def aggregate_trace(events):
 # AUTO_GRAPH_MAX_EDGES edges (launch-bound; larger layers are kernel-bound and a graph's private
 # memory pool would hold their intermediates); AUTO_GRAPH = False turns it off (set_auto_graph(False)
 # also drops every captured graph).  A replay is keyed by the objects AND their storage (data_ptr,
-# shape, stride), the libgta knob state (ops.knob_epoch) and stays eager on a stream with an attached
+# shape, stride), the calling thread's libgta knob state (ops.knob_state) and stays eager on a stream with an attached
 # knob set; weights changed in place are re-transposed into the graph's W^T before the replay.
 AUTO_GRAPH = True
 AUTO_GRAPH_MAX_EDGES = 1 << 23
@@ -1133,7 +1142,7 @@ class _AutoEntry:
         self.calls, self.run, self.failed = 0, None, False
 
 
-_AUTO_FAST = {}  # (ids of the call's objects, id of its tensors dict, knob epoch) -> entry: the per-call lookup
+_AUTO_FAST = {}  # (ids of the call's objects, id of its tensors dict, knob state) -> entry: the per-call lookup
 
 
 def clear_auto_graphs():
@@ -1154,7 +1163,7 @@ def _auto_graph(opgraph, stream, graph, tensors, semantics, plan_chunk):
     if ops.Tuning.attached(torch.cuda.current_stream(graph.device)):
         return None  # a knob set on this stream: every call reads it (gta.h), so no cached graph
     refs = (opgraph, stream, graph, semantics)
-    fkey = (id(opgraph), id(stream), id(graph), id(semantics), plan_chunk, id(tensors), ops.knob_epoch())
+    fkey = (id(opgraph), id(stream), id(graph), id(semantics), plan_chunk, id(tensors), ops.knob_state())
     ent = _AUTO_FAST.get(fkey)
     if ent is not None and not (ent.src is tensors and all(a is b for a, b in zip(ent.refs, refs)) and
                                 len(tensors) == len(ent.tensors) and
@@ -1164,7 +1173,7 @@ def _auto_graph(opgraph, stream, graph, tensors, semantics, plan_chunk):
     if ent is None:
         if not all(torch.is_tensor(t) and t.is_cuda for t in tensors.values()):
             return None
-        key = fkey[:5] + (ops.knob_epoch(),
+        key = fkey[:5] + (fkey[6],
                           tuple(sorted((k, id(t), t.data_ptr(), tuple(t.shape), tuple(t.stride()), t.dtype)
                                        for k, t in tensors.items())))
         ent = _AUTO.get(key)

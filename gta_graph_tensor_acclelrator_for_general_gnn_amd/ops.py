@@ -11,6 +11,7 @@ One function per ISA op / fused pattern of the GTA stream:
   tile_nnz     calculate_sparsity (code/preprocessing.py:12-40)            -> gta_tile_nnz
 Shapes and strides are validated on the host before any launch.
 """
+import threading
 import weakref
 
 import torch
@@ -223,24 +224,26 @@ class BlockedPlan:
         fh, vq = F // heads, F // 16
         return fh % vq == 0 and 16 % (fh // vq) == 0
 
+    DTYPES = (torch.float32,)  # gathered-table dtypes of the blocked kernels
+
     @staticmethod
-    def auto_blocks(graph, F):
-        """Column blocks for a gathered table of graph.n_cols x F fp32: slices of ~6 MB (measured
-        optima with the lean half-wave kernel: B = 20 for the 119 MB Reddit table, B = 10 for the
-        60 MB column half of a 2-D grid tile; profiles/r01_blocks_rowmerge_sweep.json,
+    def auto_blocks(graph, F, elem=4):
+        """Column blocks for a gathered table of graph.n_cols x F elements of `elem` bytes: slices
+        of ~6 MB (measured optima with the lean half-wave kernel: B = 20 for the 119 MB Reddit
+        table, B = 10 for the 60 MB column half of a 2-D grid tile; profiles/r01_blocks_rowmerge_sweep.json,
         r01_shard_b_sweep.json), capped so a row keeps >= 24 edges per block on average (each
         (block, row) item pays a start-up and a partial row written and re-read).
         Below 4 the single-pass row-chunk kernel is the better choice."""
-        table_mb = graph.n_cols * F * 4 / 1e6
+        table_mb = graph.n_cols * F * elem / 1e6
         avg_deg = graph.nnz / max(1, graph.n_rows)
         return int(max(1, min(24, round(table_mb / 6.0), avg_deg // 24)))
 
     @staticmethod
-    def supports(F, heads, x=None):
-        """Shapes libgta's blocked kernels take: F in {64, 128, 256} and, with head weights,
-        the quarter-wave form's lanes per head (F/heads)/(F/16) in {1, 2, 4, 8, 16} or the
+    def supports(F, heads, dtype=torch.float32):
+        """Shapes libgta's blocked kernels take: an fp32 table, F in {64, 128, 256} and, with head
+        weights, the quarter-wave form's lanes per head (F/heads)/(F/16) in {1, 2, 4, 8, 16} or the
         one-item-per-wave form's (F/heads)/(F/64) in {4, 8, 16}."""
-        if F not in (64, 128, 256):
+        if dtype not in BlockedPlan.DTYPES or F not in (64, 128, 256):
             return False
         if not heads:
             return True
@@ -268,8 +271,8 @@ def aggregate_blocked(graph, x, w=None, row_scale=None, out=None, accumulate=Fal
             w = w.view(-1, 1)
         ldw = _rows(w, "w")
         heads = w.shape[1]
-    if not BlockedPlan.supports(F, heads):
-        raise ValueError(f"aggregate_blocked: unsupported F={F}, heads={heads}")
+    if not BlockedPlan.supports(F, heads, x.dtype):
+        raise ValueError(f"aggregate_blocked: unsupported F={F}, heads={heads}, dtype={x.dtype}")
     if plan is None:
         plan = graph.blocked_plan(blocks)
     if not plan.sorted:
@@ -464,7 +467,7 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
         out = torch.empty(M, N, dtype=torch.float32, device=x.device)
     ldo = _rows(out, "out")
     dt = _lib.GTA_F32_BF16 if mixed else (_lib.GTA_F32 if x.dtype == torch.float32 else _lib.GTA_BF16)
-    splits = _mm_splits(M, K, N, dt) if MM_FORM == "rows" else 1
+    splits = _mm_splits(M, K, N, dt, x.device) if MM_FORM == "rows" else 1
     if splits > 1:  # few rows: split K over blocks, slices summed in order (deterministic)
         wt = _transposed(w)
         nb = check(_L().gta_update_mm_t_split_workspace_bytes(M, K, N, splits), "update_mm_t_split_workspace_bytes")
@@ -492,11 +495,13 @@ _WT_CACHE = {}
 _CAPTURED_WT = []
 
 
-def _mm_splits(M, K, N, dtype=_lib.GTA_F32):
+def _mm_splits(M, K, N, dtype=_lib.GTA_F32, dev=None):
     """K slices for gta_update_mm_t_split, as libgta picks them (gta_update_mm_t_splits: about one
     (row group, slice) block per CU for fp32, slices of >= 64 k, only for K >= 256 on few row
-    groups; knob mm_split overrides); 1 = no split."""
-    return int(check(_L().gta_update_mm_t_splits(M, K, N, dtype), "update_mm_t_splits"))
+    groups; knob mm_split overrides: the knob set attached to dev's current stream, else the calling
+    thread's); 1 = no split."""
+    st = _stream(dev) if dev is not None and dev.type == "cuda" else None
+    return int(check(_L().gta_update_mm_t_splits(M, K, N, dtype, st), "update_mm_t_splits"))
 
 
 def _transposed(w):
@@ -531,18 +536,30 @@ def tile_nnz(graph, T):
     return counts
 
 
-_KNOB_EPOCH = [0]  # bumped by every knob change: part of the executor's HIP-graph cache key
 _ATTACHED = {}  # raw stream handle -> id of the Tuning whose values it carries (the executor stays eager on them)
+_TLS = threading.local()  # per thread: {key: (value before the first set, current value)} of knobs set here
 
 
-def knob_epoch():
-    return _KNOB_EPOCH[0]
+def knob_state():
+    """The calling thread's libgta knobs that differ from the values they had before this thread
+    first set them, as a sorted tuple of (key, value): part of the executor's HIP-graph cache key.
+    Knobs are per thread in libgta, so is this; a knob set back to its old value drops out, so a
+    set-then-restore (bench's PMC child, tests) keys the same graphs again instead of recapturing."""
+    return getattr(_TLS, "state", ())
 
 
 def set_debug(key, value):
     """Set a tuning knob of libgta for the CALLING thread (include/gta.h: gta_debug_set)."""
+    d = getattr(_TLS, "knobs", None)
+    if d is None:
+        d = _TLS.knobs = {}
+    before = d[key][0] if key in d else get_debug(key)
     check(_L().gta_debug_set(key.encode(), int(value)), "debug_set")
-    _KNOB_EPOCH[0] += 1
+    if int(value) == before:
+        d.pop(key, None)
+    else:
+        d[key] = (before, int(value))
+    _TLS.state = tuple(sorted((k, v) for k, (_, v) in d.items()))
 
 
 def get_debug(key):
@@ -590,13 +607,11 @@ class Tuning:
     def attach(self, stream):
         check(self._lib.gta_tuning_attach(self._ptr(stream), self._h), "tuning_attach")
         _ATTACHED[self._ptr(stream)] = id(self)
-        _KNOB_EPOCH[0] += 1
 
     @classmethod
     def detach(cls, stream):
         check(_L().gta_tuning_attach(cls._ptr(stream), None), "tuning_attach")
         _ATTACHED.pop(cls._ptr(stream), None)
-        _KNOB_EPOCH[0] += 1
 
     @staticmethod
     def attached(stream):
@@ -608,6 +623,5 @@ class Tuning:
         for sp in [sp for sp, owner in list(_ATTACHED.items()) if owner == id(self)]:
             self._lib.gta_tuning_attach(sp, None)  # the stream no longer carries a dead set's values
             _ATTACHED.pop(sp, None)
-            _KNOB_EPOCH[0] += 1
         if h:
             self._lib.gta_tuning_destroy(h)

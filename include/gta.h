@@ -37,13 +37,14 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 7  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+#define GTA_ABI_VERSION 8  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
                               hooks; 4: knob sets attached to streams (gta_tuning_*); 5: every UPDATE
                               on hand-written kernels (no vendor library), gta_update_mm_t_splits,
                               the blocked workspace is the slab rows alone and required, bf16
                               rows in gta_aggregate (x_dtype) and gta_apply_node (a_dtype);
                               6: gta_gat_aggregate_blocked's sf_out (an SF applied to y); 7:
-                              gta_aggregate_self (the aggregate with a scaled self term) */
+                              gta_aggregate_self (the aggregate with a scaled self term); 8:
+                              gta_update_mm_t_splits takes the stream (its attached knob set) */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -279,13 +280,14 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
  * partial [M, N] goes to the workspace (>= gta_update_mm_t_split_workspace_bytes = splits x M x N
  * floats) and a second kernel adds the slices in order and applies sf.  Deterministic; the
  * contraction order differs from gta_update_mm_t (fp32 rounding only).  fp32 with N > 32
- * (N % 4 == 0, 16-B aligned wt rows) runs every (128-row group, slice) as one k_mm_ring block
- * with an 8-deep ring (one block per CU), else k_mm_rows per slice.
- * gta_update_mm_t_splits gives the slice count the library would pick for a shape (1 = no split:
- * call gta_update_mm_t): about one (group, slice) block per CU for fp32, two for bf16, slices of
- * >= 64 k, only for K >= 256 and fewer than 128 (group, column-block) units; the tuning knob
- * mm_split overrides it.  Same reference as gta_update_mm. */
-int64_t gta_update_mm_t_splits(int64_t M, int64_t K, int64_t N, int dtype);
+ * (N % 4 == 0, 16-B aligned wt rows) runs every (64-row group, slice) as one k_mm_ring block
+ * with a 4-deep ring (three blocks per CU), else k_mm_rows per slice.
+ * gta_update_mm_t_splits gives the slice count the library would pick for a shape on `stream`
+ * (1 = no split: call gta_update_mm_t): about one (group, slice) block per CU for fp32, two for
+ * bf16, slices of >= 64 k, only for K >= 256 and fewer than 128 (group, column-block) units; the
+ * tuning knob mm_split overrides it -- the stream's attached knob set, else the calling thread's,
+ * as for every call on a stream.  Same reference as gta_update_mm. */
+int64_t gta_update_mm_t_splits(int64_t M, int64_t K, int64_t N, int dtype, void* stream);
 int64_t gta_update_mm_t_split_workspace_bytes(int64_t M, int64_t K, int64_t N, int64_t splits);
 int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                           int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, int64_t splits,

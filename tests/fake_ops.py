@@ -69,6 +69,12 @@ def blocked_ready(graph, blocks):
 
 
 class BlockedPlan:  # shape rules of the real plan (ops.BlockedPlan), no device state
+    DTYPES = (torch.float32,)
+
+    @staticmethod
+    def supports(F, heads, dtype=torch.float32):
+        return False
+
     @staticmethod
     def supports_att(F, heads):
         if F not in (64, 128, 256) or heads <= 0 or F % heads:
@@ -77,7 +83,7 @@ class BlockedPlan:  # shape rules of the real plan (ops.BlockedPlan), no device 
         return fh % vq == 0 and 16 % (fh // vq) == 0
 
     @staticmethod
-    def auto_blocks(graph, F):
+    def auto_blocks(graph, F, elem=4):
         return 1
 
 

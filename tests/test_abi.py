@@ -67,12 +67,21 @@ def test_tuning_knobs_are_per_thread(lib):
     def other():
         ops.set_debug("seg_lean", 1 - base)
         seen["other"] = ops.get_debug("seg_lean")
+        seen["state"] = ops.knob_state()
 
     t = threading.Thread(target=other)
     t.start()
     t.join()
     assert seen["other"] == 1 - base
     assert ops.get_debug("seg_lean") == base
+    # the HIP-graph cache key follows the calling thread's knobs: the other thread's
+    # change is not this thread's state, and a knob set back to its old value drops out
+    assert seen["state"] == (("seg_lean", 1 - base),)
+    state0 = ops.knob_state()
+    ops.set_debug("seg_lean", 1 - base)
+    assert ops.knob_state() == tuple(sorted(state0 + (("seg_lean", 1 - base),)))
+    ops.set_debug("seg_lean", base)
+    assert ops.knob_state() == state0
     with pytest.raises(_lib.GTAError):
         ops.set_debug("no_such_knob", 1)
     with pytest.raises(_lib.GTAError):
@@ -111,10 +120,26 @@ def test_tuning_detaches_its_streams_when_collected(lib):
     a.attach(s2)
     b = ops.Tuning(seg_lean=1)
     b.attach(s2)                                         # s2 now carries b's values
-    epoch = ops.knob_epoch()
     del a
     gc.collect()
     assert not ops.Tuning.attached(s1) and ops.Tuning.attached(s2)
-    assert ops.knob_epoch() > epoch                      # cached HIP graphs keyed on knobs see the change
     ops.Tuning.detach(s2)
     del b
+
+
+def test_split_count_reads_the_streams_knob_set(lib):
+    """gta_update_mm_t_splits takes the stream, so a knob set attached to it
+    (mm_split) decides the split count the same way it decides the GEMM's own launch."""
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
+    M, K, N = 2708, 1433, 128
+    default = lib.gta_update_mm_t_splits(M, K, N, 0, None)
+    assert default > 1
+    fake_stream = 0x5500100
+    t = ops.Tuning(mm_split=3)
+    t.attach(fake_stream)
+    try:
+        assert lib.gta_update_mm_t_splits(M, K, N, 0, fake_stream) == 3
+        assert lib.gta_update_mm_t_splits(M, K, N, 0, None) == default  # other streams keep the default
+    finally:
+        ops.Tuning.detach(fake_stream)
+    assert lib.gta_update_mm_t_splits(M, K, N, 0, fake_stream) == default

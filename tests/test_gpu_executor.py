@@ -12,6 +12,7 @@ import torch
 
 from gta_graph_tensor_acclelrator_for_general_gnn_amd import executor, graph as G, ir, workloads
 from gta_graph_tensor_acclelrator_for_general_gnn_amd.semantics import Semantics
+from oracle import isa_ref
 from oracle.exec_ref import execute_ref
 
 from .test_ir_executor_cpu import compare
@@ -302,11 +303,13 @@ def test_repeated_execute_replays_a_hip_graph(golden_dir, manifest, cora, dev, t
     from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
     try:
         ops.set_debug("mm_ring", 0)
-        ep = ops.knob_epoch()
+        ks = ops.knob_state()
+        assert ks == (("mm_ring", 0),)
         later = run()
-        assert any(k[5] == ep for k in executor._AUTO)  # a new entry under the new knob state
+        assert any(k[5] == ks for k in executor._AUTO)  # a new entry under the new knob state
     finally:
         ops.set_debug("mm_ring", 1)
+    assert ops.knob_state() == ()  # restored: the earlier entries' key again
     for k in fresh:
         assert torch.equal(later.outputs[k], fresh[k])  # k_mm_rows == k_mm_ring bitwise
     executor.set_auto_graph(False)
@@ -387,3 +390,31 @@ def test_gin_bf16_model_input_on_gpu(golden_dir, manifest, cora, dev):
     # op-local fp64 checks (the bf16 GEMMs' inputs rounded to bf16 in the reference too)
     from oracle.sampled import SampledChecker
     assert SampledChecker(ex, ip, ix).check(n_samples=400, seed=3)
+
+
+def test_bf16_source_table_takes_the_row_chunked_aggregate(golden_dir, manifest, cora, dev):
+    """a bf16 source table of a width the blocked kernels take (F = 128), above the
+    blocked-form size gate, runs the bf16 row-chunked aggregate (the blocked kernels are fp32-only),
+    and the gate sizes the table with its own element size.  Result vs the fp64 oracle."""
+    rec = [s for s in _all_streams(manifest) if s["network"] == "GIN" and not s["reorder"] and s["dataset"] == "cora"][0]
+    sem = Semantics.for_network("GIN", False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    ip, ix = cora
+    gd = G.from_numpy(ip, ix, device=dev)
+    tc = workloads.make_tensors(og, G.from_numpy(ip, ix), "GIN", seed=7)
+    ex = executor.Executor(og, st, gd, {k: v.to(dev) for k, v in tc.items()}, sem)
+    ex.blocked_min_table_bytes, ex.blocked_blocks = 0, 4
+    x = torch.randn(gd.n_cols, 128, device=dev).to(torch.bfloat16)
+    assert ex._blocked_blocks(x, "src", 0) == 0
+    assert ex._blocked_blocks(x.float(), "src", 0) == 4
+    ex.blocked_min_table_bytes = x.numel() * 2 + 1  # the bf16 table's own bytes decide, not 4 B/element
+    assert ex._blocked_blocks(x.float(), "src", 0) == 4
+    w = torch.rand(gd.nnz, 1, device=dev)
+    for wt in (None, w):
+        y = ex._spmm(x, "src", wt)
+        xr = x.float().cpu().numpy().astype(np.float64)
+        wr = None if wt is None else wt.cpu().numpy().astype(np.float64)
+        ref = isa_ref.aggregate(ip, ix, xr, "src", wr)
+        bound = 1e-5 * isa_ref.aggregate_abs(ip, ix, xr, "src", wr) + 1e-6
+        assert np.all(np.abs(y.cpu().numpy() - ref) <= bound)

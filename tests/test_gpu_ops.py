@@ -518,7 +518,7 @@ def test_gat_aggregate_lean_bitwise(dev, blocks, item_edges, ldb):
 
 
 @pytest.mark.parametrize("case", ["no_edges", "no_rows", "one_row", "dup_self"])
-def test_degenerate_graphs_every_op(dev, case):
+def test_edge_case_graphs_vs_oracle(dev, case):
     """Empty and ragged extremes through every entry point: a graph without edges, without rows,
     one row holding every edge, and duplicate edges plus self loops -- results equal the oracle."""
     rng = np.random.default_rng(5)
