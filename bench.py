@@ -24,25 +24,31 @@ Total work is fixed (one Reddit graph): "scaling": "strong"; value = E / max-ran
 Printed JSON (rank 0):
   parity        sampled output rows of every rank (incl. the heaviest and lightest) re-derived in fp64
                 by the oracle (oracle/isa_ref.aggregate), |err| <= 1e-5 * sum|terms| + 1e-6 each
-  roofline      the aggregate launch pair (k_agg_h32 + k_seg_reduce) at N = 1: traffic = HBM-side bytes
-                per launch from two rocprofv3 --pmc passes run by this bench on its own kernels
-                (FETCH_SIZE, WRITE_SIZE).  Two read factors, each calibrated in the same pass on known
-                bytes (MI355X_MICROARCH.md §HBM): streaming reads on a float4 copy (k_apply_node4),
-                gathered 512-B rows on a permutation gather with 16-B lanes; k_agg_h32's FETCH is split
-                into its known streams (indices, alpha, item records: streaming factor) and the rest
-                (its X gathers: gather factor); k_seg_reduce's partial-row reads take the streaming
-                factor; writes take the copy's write factor.  achieved = traffic / HIP-event kernel
-                time, frac = achieved / 8 TB/s.  alg_* = the SURVEY §8d byte model (548 B/edge:
+  roofline      the aggregate launch pair (k_agg_h32 + k_seg_reduce) of every rank's tile: traffic = memory-side
+                bytes per step from two rocprofv3 --pmc passes each rank runs on its own tile's kernels in
+                child processes, before it initialises the GPU (FETCH_SIZE, WRITE_SIZE; at N > 1 the child
+                rebuilds the rank's tile alone from metric.column_counts).  Two read factors, each calibrated
+                in the same pass on known bytes (MI355X_MICROARCH.md §HBM): streaming reads on a float4 copy
+                (k_apply_node4), gathered 512-B rows on a permutation gather with 16-B lanes; k_agg_h32's
+                FETCH is split into its known streams (indices, alpha, item records: streaming factor) and
+                the rest (its X gathers: gather factor); k_seg_reduce's partial-row reads take the streaming
+                factor; writes take the copy's write factor.  achieved = traffic / HIP-event time of the
+                tile's launches alone, frac = achieved / 8 TB/s.  The headline fields are the critical rank's
+                (longest compute); per_rank lists every rank's compute_ms, step_ms, exposed_exchange_ms
+                (step - compute), traffic, achieved, frac.  alg_* = the SURVEY §8d byte model (548 B/edge:
                 every gathered X row), frac_l2 = its rate against the L2-served gather ceiling.
-  cpu_baseline  oracle/spmm_ref.c (fp32, OpenMP, every core of sched_getaffinity) on a bounded row
-                sample of the same workload, rank 0 at N = 1.
+  cpu_baseline  oracle/spmm_ref.c (fp32, OpenMP, every core of sched_getaffinity and the cgroup quota) on a
+                bounded row sample of the same workload, rank 0 after the timed region, median of 5 after
+                one warm-up.
 """
 import argparse
 import csv
+import fcntl
 import glob
 import json
 import os
 import shutil
+import signal
 import subprocess
 import sys
 import tempfile
@@ -154,7 +160,8 @@ class Aggregate:
             wk.wait()
 
 
-def build(args, world, rank, dev, backend, note):
+def grid_of(args, world):
+    """(mode, pr, pc) of a world-rank run."""
     mode = "single" if world == 1 else args.mode
     if args.grid != "auto":
         pr, pc = (int(v) for v in args.grid.lower().split("x"))
@@ -162,6 +169,13 @@ def build(args, world, rank, dev, backend, note):
         pr, pc = distributed.grid_shape(world, "rows" if mode == "rows" else "edges")
     if pr * pc != world:
         raise SystemExit(f"--grid {pr}x{pc} does not match {world} ranks")
+    return mode, pr, pc
+
+
+def build(args, world, rank, dev, backend, note, col_counts=None):
+    """This rank's shard and launches.  col_counts: the whole graph's per-column nnz given directly
+    (the PMC child rebuilding one rank's tile with no process group); else all-reduced (world > 1)."""
+    mode, pr, pc = grid_of(args, world)
     if mode == "rows" and pc != 1:
         raise SystemExit("--mode rows uses a PRx1 grid")
     chunks = args.row_chunks or (1 if world == 1 else 2)
@@ -176,7 +190,7 @@ def build(args, world, rank, dev, backend, note):
         elif cf != "equal":
             fracs = [float(v) for v in cf.split(",")]
     count_reduce = None
-    if world > 1:
+    if world > 1 and col_counts is None:
         def count_reduce(t):
             dist.all_reduce(t)
             return t
@@ -192,7 +206,7 @@ def build(args, world, rank, dev, backend, note):
             shard.graph = shard.grid.graph = G.Graph(ip2, shard.graph.indices, n_cols=shard.graph.n_cols)
     else:
         shard = metric.Shard(args.n, args.e, rank, pr, pc, chunks, dev, count_reduce=count_reduce, note=note,
-                             fracs=fracs)
+                             fracs=fracs, col_counts=col_counts)
     groups = None
     if mode == "edges" and pc > 1:
         groups = distributed.row_groups(pr, pc) if pr > 1 else [None]
@@ -204,9 +218,12 @@ def build(args, world, rank, dev, backend, note):
 # PMC traffic (rocprofv3 --pmc on this very bench, child processes started before the GPU is used)
 # ----------------------------------------------------------------------------------------------
 def pmc_child(args):
-    """Runs under rocprofv3 --pmc: the known-byte calibration launches, then the metric launches.
-    Writes the metric plan's item count (its known stream bytes) to <pmc dir>/meta.json."""
-    dev = torch.device("cuda", 0)
+    """Runs under rocprofv3 --pmc: the known-byte calibration launches, then this rank's metric
+    launches (its own tile, rebuilt alone: at N > 1 the column cuts come from metric.column_counts,
+    the same whole-graph histogram the distributed run all-reduces).  Writes the tile's known
+    stream sizes (edges, items) and launch pairs per step to <pmc dir>/meta.json."""
+    world, rank = args.pmc_world, args.pmc_rank
+    dev = torch.device("cuda", args.pmc_local)
     torch.cuda.set_device(dev)
     n = CALIB_ROWS
     # streaming calibration: a float4 copy of a 1 GiB table (k_apply_node4, 16-B lanes, read once, written once)
@@ -226,17 +243,22 @@ def pmc_child(args):
     finally:
         ops.set_debug("agg_lpe", 0)
     torch.cuda.synchronize()
-    del xc, yc, gc
-    shard, agg, *_ = build(args, 1, 0, dev, "none", lambda m: None)
+    del xc, yc, gc, ip, perm
+    col_counts = None
+    if world > 1 and grid_of(args, world)[2] > 1:
+        col_counts = metric.column_counts(args.n, args.e, dev)
+    shard, agg, *_ = build(args, world, rank, dev, "none", lambda m: None, col_counts=col_counts)
+    del col_counts
+    live = [c for c, (a, b, _) in enumerate(agg.parts) if b > a]
     for _ in range(args.steps):
-        agg.step()
+        for c in live:
+            agg.launch(c)
     torch.cuda.synchronize()
     if args.pmc_meta:
-        gg = agg.parts[0][2]
-        plan = gg.blocked_plan(agg.blocks) if agg.impl == "blocked" else None
+        items = sum(agg.parts[c][2].blocked_plan(agg.blocks).n_items for c in live) if agg.impl == "blocked" else 0
         with open(args.pmc_meta, "w") as fh:
-            json.dump({"nnz": int(gg.nnz), "n_rows": int(gg.n_rows), "heads": HEADS,
-                       "n_items": int(plan.n_items) if plan is not None else 0}, fh)
+            json.dump({"nnz": int(shard.graph.nnz), "n_rows": int(shard.graph.n_rows), "heads": HEADS,
+                       "n_items": int(items), "pairs_per_step": len(live), "rank": rank, "world": world}, fh)
     return 0
 
 
@@ -251,9 +273,9 @@ def _counter_rows(d, counter):
     return rows
 
 
-def _split(rows):
-    """-> (stream calibration dispatches, gather calibration dispatches, [(agg, reduce)] metric
-    launch pairs) from ordered counter rows."""
+def _split(rows, per_step=1):
+    """-> (stream calibration dispatches, gather calibration dispatches, [(agg, reduce)] per step)
+    from ordered counter rows: a step's launch pairs (one per non-empty row chunk of the tile) summed."""
     copy, gather, pairs, cur = [], [], [], None
     for _, name, v in rows:
         if "k_agg_h32" in name or "k_agg_seg" in name:
@@ -266,56 +288,91 @@ def _split(rows):
             copy.append(v)
         elif "k_aggregate" in name and not pairs and cur is None:
             gather.append(v)
-    return copy, gather, pairs
+    k = max(1, per_step)
+    steps = [(sum(a for a, _ in pairs[i:i + k]), sum(b for _, b in pairs[i:i + k]))
+             for i in range(0, len(pairs) - k + 1, k)]
+    return copy, gather, steps
 
 
-def collect_pmc(args, out_dir):
-    """Two rocprofv3 --pmc passes over `bench.py --pmc-child` (FETCH_SIZE, WRITE_SIZE; separate passes:
-    TCC slots).  Returns the per-launch traffic record, or {"error": ...}."""
+def _run_group(cmd, env, timeout):
+    """Run cmd in its own session; on timeout kill the whole process group (rocprofv3 and its
+    child).  -> (returncode or None on timeout, stderr tail)."""
+    p = subprocess.Popen(cmd, env=env, cwd=ROOT, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        _, err = p.communicate(timeout=timeout)
+        return p.returncode, err[-400:]
+    except subprocess.TimeoutExpired:
+        try:
+            os.killpg(p.pid, signal.SIGKILL)
+        except OSError:
+            pass
+        p.communicate()
+        return None, ""
+
+
+def collect_pmc(args, out_dir, world=1, rank=0, local=0):
+    """Two rocprofv3 --pmc passes over `bench.py --pmc-child` on this rank's own tile (FETCH_SIZE,
+    WRITE_SIZE; separate passes: TCC slots), run before this process touches the GPU.  The TCC
+    counters are device-wide, so children sharing a device (a one-GPU rehearsal of N ranks) take
+    turns on a per-device lock file.  Returns the per-step traffic record, or {"error": ...}."""
     exe = shutil.which("rocprofv3")
     if not exe:
         return {"error": "rocprofv3 not found"}
     os.makedirs(out_dir, exist_ok=True)
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
     meta_path = os.path.join(out_dir, "meta.json")
-    res = {}
-    for counter in ("FETCH_SIZE", "WRITE_SIZE"):
-        d = os.path.join(out_dir, counter.lower())
-        shutil.rmtree(d, ignore_errors=True)
-        cmd = [exe, "--kernel-trace", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
-               sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--pmc-meta", meta_path,
-               "--n", str(args.n), "--e", str(args.e), "--blocks", str(args.blocks), "--impl", args.impl]
-        t0 = time.time()
-        try:
-            p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True, timeout=240,
-                               start_new_session=True)
-        except subprocess.TimeoutExpired:
-            return {"error": f"rocprofv3 --pmc {counter} timed out"}
-        if p.returncode != 0:
-            return {"error": f"rocprofv3 --pmc {counter} rc={p.returncode}: {p.stderr[-400:]}"}
-        copy, gather, pairs = _split(_counter_rows(d, counter))
-        if not copy or not gather or not pairs:
-            return {"error": f"{counter}: no calibration/metric dispatches in {d}"}
-        pairs = pairs[1:] if len(pairs) > 1 else pairs   # the first launch runs on cold caches
-        res[counter] = {"copy_kb": copy[-1], "gather_kb": gather[-1],
-                        "agg_kb": float(np.mean([a for a, _ in pairs])),
-                        "reduce_kb": float(np.mean([b for _, b in pairs])), "launches": len(pairs),
-                        "pass_s": round(time.time() - t0, 1)}
+    lock = open(os.path.join(tempfile.gettempdir(), f"gta_bench_pmc_dev{local}.lock"), "w")
+    fcntl.flock(lock, fcntl.LOCK_EX)
     try:
-        meta = json.load(open(meta_path))
-    except (OSError, ValueError):
-        return {"error": "pmc child wrote no plan metadata"}
+        res = {}
+        for counter in ("FETCH_SIZE", "WRITE_SIZE"):
+            d = os.path.join(out_dir, counter.lower())
+            shutil.rmtree(d, ignore_errors=True)
+            cmd = [exe, "--kernel-trace", "--pmc", counter, "--output-format", "csv", "-d", d, "-o", "run", "--",
+                   sys.executable, os.path.abspath(__file__), "--pmc-child", "--steps", "3", "--pmc-meta", meta_path,
+                   "--pmc-world", str(world), "--pmc-rank", str(rank), "--pmc-local", str(local),
+                   "--mode", args.mode, "--grid", args.grid, "--row-chunks", str(args.row_chunks),
+                   "--chunk-fracs", args.chunk_fracs,
+                   "--n", str(args.n), "--e", str(args.e), "--blocks", str(args.blocks), "--impl", args.impl]
+            t0 = time.time()
+            rc, err = _run_group(cmd, env, 240)
+            if rc is None:
+                return {"error": f"rocprofv3 --pmc {counter} timed out"}
+            if rc != 0:
+                return {"error": f"rocprofv3 --pmc {counter} rc={rc}: {err}"}
+            try:
+                meta = json.load(open(meta_path))
+            except (OSError, ValueError):
+                return {"error": "pmc child wrote no plan metadata"}
+            if meta.get("pairs_per_step", 1) == 0:
+                return {"error": "this rank's tile has no edges: no launches to count"}
+            copy, gather, steps = _split(_counter_rows(d, counter), meta.get("pairs_per_step", 1))
+            if not copy or not gather or not steps:
+                return {"error": f"{counter}: no calibration/metric dispatches in {d}"}
+            steps = steps[1:] if len(steps) > 1 else steps   # the first step runs on cold caches
+            res[counter] = {"copy_kb": copy[-1], "gather_kb": gather[-1],
+                            "agg_kb": float(np.mean([a for a, _ in steps])),
+                            "reduce_kb": float(np.mean([b for _, b in steps])), "launches": len(steps),
+                            "pass_s": round(time.time() - t0, 1)}
+    finally:
+        fcntl.flock(lock, fcntl.LOCK_UN)
+        lock.close()
     return pmc_traffic(res, meta)
 
 
 def pmc_traffic(res, meta, n=CALIB_ROWS):
-    """Per-launch bytes from the counter means (res[counter][...] in KB) and the plan metadata:
+    """Per-step bytes (a step = the tile's launch pairs, one per non-empty row chunk; one pair on one
+    GPU) from the counter means (res[counter][...] in KB) and the tile's plan metadata:
       read factors   kr_s = copy bytes read / copy FETCH; kr_g = permutation-gather X bytes / (gather
                      FETCH - its index + indptr streams / kr_s); write factor kw = copy bytes / copy WRITE
       k_agg_h32      streams S = 4 E (indices) + 4 H E (alpha) + 16 items (item records), read once;
                      gathers = (FETCH - S / kr_s) * kr_g; + WRITE * kw (partial rows)
       k_seg_reduce   FETCH * kr_s (partial rows, item lists) + WRITE * kw (y)
-    Recomputable from the committed CSVs (profiles/r03_pmc_*)."""
+    Why kr_s is ~2: FETCH_SIZE = TCC_EA0_RDREQ x 64 B, and a wide streaming read leaves L2 as 128-B
+    requests tallied at 64 B (MI355X_MICROARCH.md §HBM); the copy measures it on this box, in this pass.
+    The bytes are memory-side (L2 <-> fabric): Infinity-Cache hits are counted, so they bound the
+    HBM bytes from above.  Recomputable from the committed CSVs (profiles/r0*/pmc_*)."""
     fe, wr = res["FETCH_SIZE"], res["WRITE_SIZE"]
     kb = 1024.0
     copy_bytes = n * 4 * F
@@ -337,7 +394,10 @@ def pmc_traffic(res, meta, n=CALIB_ROWS):
                       "and gathered 512-B rows (kr_g, permutation gather with 16-B lanes, its index streams "
                       "taken out at kr_s); k_agg_h32 = known streams (indices, alpha, item records) + "
                       "(FETCH - streams/kr_s)*kr_g + WRITE*kw; k_seg_reduce = FETCH*kr_s + WRITE*kw; "
-                      "counts L2<->fabric bytes (Infinity-Cache hits included); first launch skipped"}
+                      "counts L2<->fabric bytes (Infinity-Cache hits included); first step skipped",
+            "traffic_side": "memory side of L2 (TCC_EA0 requests): HBM + Infinity-Cache hits, an upper bound "
+                            "on HBM bytes; kr_s ~ 2 because FETCH_SIZE tallies a 128-B streaming request "
+                            "at 64 B (MI355X_MICROARCH.md §HBM), measured in the same pass"}
 
 
 # ----------------------------------------------------------------------------------------------
@@ -363,10 +423,13 @@ def cpu_quota():
         return None
 
 
-def cpu_baseline(shard, target_s=12.0):
-    """Oracle C aggregate (OpenMP) on the first rows of the same workload, ~target_s of CPU work per
+def cpu_baseline(shard, target_s=12.0, repeats=5):
+    """Oracle C aggregate (OpenMP) on the first rows of this rank's row group of the same workload
+    (median of `repeats` timed runs after one warm-up run), ~target_s of CPU work per
     thread count: every core of sched_getaffinity(0), and -- when a cgroup quota caps the job below
-    that -- as many threads as the quota allows.  value / cores = the faster run; both are listed."""
+    that -- as many threads as the quota allows.  value / cores = the faster run; both are listed.
+    At N > 1 the rank holds only its column slice of X: the sample's X rows are regenerated (every X
+    row is a pure function of (seed, id))."""
     from oracle import cbase
     cbase.load()
     try:
@@ -379,7 +442,10 @@ def cpu_baseline(shard, target_s=12.0):
         counts.append(int(np.ceil(quota)))
     ip = shard.rows_ip.cpu().numpy()
     ix = shard.rows_src.to(torch.int32).cpu().numpy()
-    xh = shard.x.cpu().numpy()
+    if shard.x.shape[0] >= shard.n:
+        xh = shard.x.cpu().numpy()
+    else:
+        xh = metric.x_rows(torch.arange(shard.n), shard.x.device, shard.seed).cpu().numpy()
     ah = shard.rows_alpha
     n = len(ip) - 1
     a_cache = {}
@@ -396,20 +462,49 @@ def cpu_baseline(shard, target_s=12.0):
     runs = []
     for threads in counts:
         rows = min(n, 2000)
-        dt, ecount = run(rows, threads)  # calibration
+        dt, ecount = run(rows, threads)  # rate probe
         rate = ecount / max(dt, 1e-6)
-        want_edges = min(int(rate * target_s / 3), int(ip[-1]))
+        want_edges = min(int(rate * target_s / (repeats + 1)), int(ip[-1]))
         rows = int(min(n, max(1, np.searchsorted(ip, want_edges))))
-        times = [run(rows, threads)[0] for _ in range(3)]
+        run(rows, threads)               # warm-up
+        times = [run(rows, threads)[0] for _ in range(repeats)]
         ecount = int(ip[rows])
-        runs.append({"threads": threads, "value": ecount / float(np.median(times)), "rows": rows, "edges": ecount})
+        runs.append({"threads": threads, "value": ecount / float(np.median(times)), "rows": rows, "edges": ecount,
+                     "times_s": [round(t, 4) for t in times]})
     best = max(runs, key=lambda r: r["value"])
+    r0 = shard.rcuts[shard.grid.i]
     return {"value": best["value"], "unit": "edges/s", "cores": best["threads"], "kind": "port",
-            "sample": f"rows [0,{best['rows']}) = {best['edges']} edges of the same graph/X/alpha, median of 3, "
-                      f"oracle/spmm_ref.c fp32 OpenMP; sched_getaffinity = {affinity} cores, cgroup quota = "
-                      f"{quota} CPUs; runs: " + ", ".join(f"{r['threads']} threads {r['value'] / 1e6:.1f} M edges/s"
-                                                          for r in runs),
+            "sample": f"destination rows [{r0},{r0 + best['rows']}) = {best['edges']} edges of the same graph/X/alpha, "
+                      f"median of {repeats} after 1 warm-up, oracle/spmm_ref.c fp32 OpenMP; sched_getaffinity = "
+                      f"{affinity} cores, cgroup quota = {quota} CPUs; runs: "
+                      + ", ".join(f"{r['threads']} threads {r['value'] / 1e6:.1f} M edges/s" for r in runs),
             "affinity_cores": affinity, "runs": runs}
+
+
+def rank_roofline(per_rank, peak=PEAK_HBM_GBS):
+    """Roofline fields from every rank's measurements (a list of dicts: rank, tile_edges, tile_rows,
+    compute_ms = HIP-event time of the tile's launches alone, step_ms = the rank's own step time
+    before the closing barrier, traffic = PMC bytes per step or None).  The headline fields are the
+    critical rank's -- the one with the longest compute, which bounds the step; exposed_exchange_ms
+    = step_ms - compute_ms per rank (collectives not hidden under compute, plus launch gaps)."""
+    rows = []
+    for s in per_rank:
+        t = s.get("traffic")
+        t = None if t is None or not np.isfinite(t) else float(t)
+        ach = None if t is None else t / (s["compute_ms"] / 1e3) / 1e9
+        rows.append({"rank": int(s["rank"]), "tile_edges": int(s["tile_edges"]), "tile_rows": int(s["tile_rows"]),
+                     "compute_ms": s["compute_ms"], "step_ms": s["step_ms"],
+                     "exposed_exchange_ms": max(0.0, s["step_ms"] - s["compute_ms"]),
+                     "traffic": t, "achieved": ach, "frac": None if ach is None else ach / peak})
+    crit = max(rows, key=lambda r: r["compute_ms"])
+    fr = [r["frac"] for r in rows if r["frac"] is not None]
+    tot = [r["traffic"] for r in rows]
+    job = sum(tot) / (crit["compute_ms"] / 1e3) / 1e9 if all(v is not None for v in tot) else None
+    return {"achieved": crit["achieved"], "frac": crit["frac"], "traffic": crit["traffic"],
+            "kernel_ms": crit["compute_ms"], "rank_basis": crit["rank"],
+            "frac_min": min(fr) if fr else None, "frac_max": max(fr) if fr else None,
+            "job_achieved_GBps": job, "job_peak_GBps": peak * len(rows),
+            "per_rank": rows}
 
 
 # ----------------------------------------------------------------------------------------------
@@ -431,10 +526,15 @@ def main():
     ap.add_argument("--e", "--graph-edges", dest="e", type=int, default=E_REDDIT)
     ap.add_argument("--parity-rows", type=int, default=256, help="sampled rows per rank for the fp64 oracle")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-s", type=float, default=12.0,
+                    help="CPU work per thread count of the cpu_baseline leg (seconds, approx.)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
     ap.add_argument("--pmc-dir", default="", help="keep the --pmc CSVs here (default: a temp dir)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-meta", default="", help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-world", type=int, default=1, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-rank", type=int, default=0, help=argparse.SUPPRESS)
+    ap.add_argument("--pmc-local", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
     if args.pmc_child:
         return pmc_child(args)
@@ -446,12 +546,15 @@ def main():
     if os.environ.get("GTA_SINGLE_DEVICE"):
         local = 0
 
-    # PMC passes first: child processes, before this process initialises the GPU
+    # PMC passes first: child processes on this rank's own tile, before this process initialises the GPU
     pmc = None
-    if world == 1 and not args.no_pmc:
-        log(rank, "rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) on this bench's kernels")
-        keep = args.pmc_dir or tempfile.mkdtemp(prefix="gta_pmc_")
-        pmc = collect_pmc(args, keep)
+    if not args.no_pmc:
+        log(rank, "rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE) on this rank's kernels")
+        if args.pmc_dir:
+            keep = args.pmc_dir if world == 1 else os.path.join(args.pmc_dir, f"rank{rank}")
+        else:
+            keep = tempfile.mkdtemp(prefix=f"gta_pmc_r{rank}_")
+        pmc = collect_pmc(args, keep, world, rank, local)
         if not args.pmc_dir:
             shutil.rmtree(keep, ignore_errors=True)
         log(rank, f"pmc: {json.dumps({k: v for k, v in pmc.items() if k != 'passes'})[:300]}")
@@ -517,6 +620,7 @@ def main():
     for _ in range(args.steps):
         agg.step()
     torch.cuda.synchronize()
+    own_ms = (time.perf_counter() - t0) * 1e3 / args.steps   # this rank's own step, before the closing barrier
     if world > 1:
         dist.barrier()
     dt = time.perf_counter() - t0
@@ -526,7 +630,7 @@ def main():
         dt = float(t.item())
     ms_per_step = dt * 1e3 / args.steps
     value = args.e / (ms_per_step / 1e3)
-    log(rank, f"timed: {ms_per_step:.3f} ms/step")
+    log(rank, f"timed: {ms_per_step:.3f} ms/step (own {own_ms:.3f}, kernels alone {kern_ms:.3f})")
 
     # parity: this rank's own output rows (complete sums after the exchange) vs the fp64 oracle
     agg.step()
@@ -552,31 +656,50 @@ def main():
               "max_abs_err": max_err, "ok": bool(ratio <= 1.0)}
     log(rank, f"parity: {parity}")
 
-    # roofline of the dominant kernel pair (this rank's tile launches)
-    ab = metric.alg_bytes(shard.graph.n_rows if world == 1 else g.r1 - g.r0, shard.graph.nnz)
-    alg_gbps = ab / (kern_ms / 1e3) / 1e9
-    roof = {"bound": "hbm", "achieved": None, "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": None, "traffic": None,
-            "kernel_ms": kern_ms, "kernels": "k_agg_h32 + k_seg_reduce" if agg.impl == "blocked"
-            else "k_aggregate + combine",
+    # roofline of the dominant kernel pair: every rank's tile launches (compute alone), its own step
+    # time and its PMC bytes, gathered on every rank; the critical (longest-compute) rank's in front
+    traffic = pmc["bytes_per_launch"] if pmc is not None and "error" not in pmc else float("nan")
+    mine = [rank, shard.graph.nnz, g.r1 - g.r0 if world > 1 else shard.graph.n_rows, kern_ms, own_ms, traffic,
+            phase_ms[1] if phase_ms else float("nan"), phase_ms[2] if phase_ms else float("nan")]
+    stats = torch.zeros(world, len(mine), dtype=torch.float64, device=dev)
+    stats[rank] = torch.tensor(mine, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(stats)
+    stats = stats.cpu().tolist()
+    per_rank = [{"rank": r[0], "tile_edges": r[1], "tile_rows": r[2], "compute_ms": r[3], "step_ms": r[4],
+                 "traffic": r[5], "agg_ms": r[6], "reduce_ms": r[7]} for r in stats]
+    rr = rank_roofline(per_rank)
+    for row, s_ in zip(rr["per_rank"], per_rank):
+        row.update({"k_agg_h32_ms": s_["agg_ms"], "k_seg_reduce_ms": s_["reduce_ms"]})
+    crit = rr["per_rank"][rr["rank_basis"]]
+    log(rank, "per rank: " + "; ".join(f"r{r['rank']} compute {r['compute_ms']:.3f} step {r['step_ms']:.3f} "
+                                       f"exposed {r['exposed_exchange_ms']:.3f} ms frac {r['frac']}"
+                                       for r in rr["per_rank"]))
+    ab = metric.alg_bytes(crit["tile_rows"], crit["tile_edges"])
+    alg_gbps = ab / (crit["compute_ms"] / 1e3) / 1e9
+    roof = {"bound": "hbm", "achieved": rr["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": rr["frac"],
+            "traffic": rr["traffic"], "kernel_ms": rr["kernel_ms"],
+            "kernels": "k_agg_h32 + k_seg_reduce" if agg.impl == "blocked" else "k_aggregate + combine",
+            "rank_basis": rr["rank_basis"], "frac_min": rr["frac_min"], "frac_max": rr["frac_max"],
+            "job_achieved_GBps": rr["job_achieved_GBps"], "job_peak_GBps": rr["job_peak_GBps"],
             "alg_bytes_per_launch": ab, "alg_GBps": alg_gbps, "frac_l2": alg_gbps / L2_GATHER_GBS,
             "l2_gather_peak_GBps": L2_GATHER_GBS,
-            "compulsory_bytes": metric.compulsory_bytes(args.n, args.n, args.e) if world == 1 else None}
+            "compulsory_bytes": metric.compulsory_bytes(args.n, args.n, args.e) if world == 1 else None,
+            "per_rank": rr["per_rank"]}
     if pmc is not None:
         if "error" in pmc:
             roof["pmc_error"] = pmc["error"]
         else:
-            roof["traffic"] = pmc["bytes_per_launch"]
-            roof["achieved"] = pmc["bytes_per_launch"] / (kern_ms / 1e3) / 1e9
-            roof["frac"] = roof["achieved"] / PEAK_HBM_GBS
             roof["traffic_split"] = {"agg": pmc["agg_bytes"], "reduce": pmc["reduce_bytes"],
                                      "agg_split": pmc["agg_split"],
                                      "read_factor_stream": pmc["read_factor_stream"],
                                      "read_factor_gather": pmc["read_factor_gather"],
-                                     "write_factor": pmc["write_factor"]}
+                                     "write_factor": pmc["write_factor"], "rank": rank}
             roof["pmc_counters_kb"] = pmc["passes"]
             roof["pmc_meta"] = pmc["meta"]
             roof["traffic_method"] = pmc["method"]
-            if phase_ms is not None:  # each kernel alone: its PMC bytes over its own HIP-event time
+            roof["traffic_side"] = pmc["traffic_side"]
+            if phase_ms is not None:  # each kernel alone: its PMC bytes over its own HIP-event time (rank 0)
                 roof["per_kernel"] = {
                     name: {"ms": phase_ms[ph], "traffic": byt, "achieved": byt / (phase_ms[ph] / 1e3) / 1e9,
                            "frac": byt / (phase_ms[ph] / 1e3) / 1e9 / PEAK_HBM_GBS}
@@ -606,9 +729,9 @@ def main():
         "parity": parity,
         "roofline": roof,
     }
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and not args.no_cpu_baseline:  # after the timed region; other ranks wait at the barrier
         log(rank, "cpu baseline")
-        result["cpu_baseline"] = cpu_baseline(shard)
+        result["cpu_baseline"] = cpu_baseline(shard, target_s=args.cpu_baseline_s)
     elif rank == 0:
         result["cpu_baseline"] = None
     if rank == 0:

@@ -1786,6 +1786,7 @@ k_edge_softmax_v(const int64_t* __restrict__ indptr, const int32_t* __restrict__
 //   A[i = l&15][k = l>>4], B[k = l>>4][j = l&15]; D col = l&15, row = 4*(l>>4)+r.
 // ---------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // SF epilogue of the MFMA GEMMs applied to the whole accumulator tile in place, the switch on sf
 // OUTSIDE the element loops.  With sf_apply per element each of the FR x NT x 4 store sites held
@@ -1800,6 +1801,21 @@ __device__ __forceinline__ void sf_tile(int sf, f32x4 (&acc)[FR][NT]) {
     _Pragma("unroll") for (int i = 0; i < FR; ++i)                                    \
       _Pragma("unroll") for (int c = 0; c < NT; ++c)                                  \
         _Pragma("unroll") for (int r = 0; r < 4; ++r) acc[i][c][r] = sf_apply(K_, acc[i][c][r]); \
+    return;
+    GTA_SFT(GTA_SF_RELU) GTA_SFT(GTA_SF_EXP_LEAKY_RELU) GTA_SFT(GTA_SF_ELU) GTA_SFT(GTA_SF_EXP)
+    GTA_SFT(GTA_SF_LEAKY_RELU) GTA_SFT(GTA_SF_SIGMOID) GTA_SFT(GTA_SF_TANH) GTA_SFT(GTA_SF_RECIP)
+#undef GTA_SFT
+    default: return;  // GTA_SF_NONE
+  }
+}
+
+template <int T>
+__device__ __forceinline__ void sf_tile16(int sf, f32x16 (&acc)[T]) {
+  switch (sf) {
+#define GTA_SFT(K_)                                                                  \
+  case K_:                                                                           \
+    _Pragma("unroll") for (int t = 0; t < T; ++t)                                     \
+      _Pragma("unroll") for (int r = 0; r < 16; ++r) acc[t][r] = sf_apply(K_, acc[t][r]); \
     return;
     GTA_SFT(GTA_SF_RELU) GTA_SFT(GTA_SF_EXP_LEAKY_RELU) GTA_SFT(GTA_SF_ELU) GTA_SFT(GTA_SF_EXP)
     GTA_SFT(GTA_SF_LEAKY_RELU) GTA_SFT(GTA_SF_SIGMOID) GTA_SFT(GTA_SF_TANH) GTA_SFT(GTA_SF_RECIP)
@@ -2261,7 +2277,15 @@ constexpr int ring_blocks(int NT, int D, int FR) {
   return (160 / (D * (4 * FR + NT))) > 4 ? 4 : (160 / (D * (4 * FR + NT)));
 }
 
-template <int NT, int D = 3, int FR = 2>
+// M32 (FR = 2): the same ring and stage image, consumed by v_mfma_f32_32x32x2_f32 instead --
+// each wave's 32 rows x 16*NT columns as NT/2 tiles of 32 x 32, half the MFMA instructions per
+// stage (FR*NT*4 16x16x4 -> NT/2 * 8 32x32x2; the same MFMA cycles) with the same fragment reads.
+// Lane (h = l >> 5, r = l & 31) reads logical k pieces h and 2 + h of its row; instruction
+// (jj, m) takes k = 8m + jj (lane half 0) then 8m + 4 + jj (half 1), so each output sums k in
+// k_mm_rows' order (0, 4, 8, 12, 1, 5, ...): bitwise equal to the 16x16x4 form.  The DMA swizzle
+// becomes piece ^ ((row >> 2) & 3), which keeps these reads conflict-free (each ds_read_b128
+// 16-lane group reads one piece of 16 distinct fragment rows).
+template <int NT, int D = 3, int FR = 2, bool M32 = false>
 __global__ void __launch_bounds__(kBlock, ring_blocks(NT, D, FR))
 k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const float* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
@@ -2269,6 +2293,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   static_assert(NT == 4 || NT == 8, "B fragments split evenly over the 4 waves");
   static_assert(FR == 1 || FR == 2, "one or two A fragments per wave");
   static_assert(D >= 3 && D <= 8, "ring depth");
+  static_assert(!M32 || FR == 2, "32x32 tiles: 32 rows per wave");
   if (kslice > 0) {
     const int k0 = static_cast<int>(blockIdx.y) * kslice;
     x += k0;
@@ -2305,10 +2330,20 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   // piece: 16 rows per 16 consecutive lanes), bitwise equal and 1-4 % faster on every shape
   // measured (profiles/r03/mm_dma_rows_ab.log).
   const int rr = lane >> 2;
-  const int cdma = (lane & 3) ^ ((rr >> 2) & 2);  // logical 16-B k piece this lane DMAs
+  const int cdma = M32 ? ((lane & 3) ^ ((rr >> 2) & 3))         // logical 16-B k piece this lane DMAs
+                       : ((lane & 3) ^ ((rr >> 2) & 2));
   const uint32_t rdoff = static_cast<uint32_t>(r16 * 64 + ((g ^ ((r16 >> 2) & 2)) * 16));
   const bool dead = ring_tail && (S - 1) * KS + 4 * cdma >= K;  // this lane's DMA piece of the last stage
   const bool dead_rd = ring_tail && (S - 1) * KS + 4 * g >= K;  // the piece this lane reads
+  // M32 reads: lane (h, r32) reads row r32 & 15 of fragment r32 >> 4, logical pieces h and 2 + h
+  const int h32 = lane >> 5, r32 = lane & 31, f32r = r32 >> 4, q32 = (r32 & 15) >> 2;
+  uint32_t rd32[2];
+  bool dead32[2];
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    rd32[m] = static_cast<uint32_t>(f32r * 1024 + (r32 & 15) * 64 + (((2 * m + h32) ^ q32) * 16));
+    dead32[m] = ring_tail && (S - 1) * KS + 4 * (2 * m + h32) >= K;
+  }
   const int64_t T = my_groups * S;
   const float* bsrc[NT / 4];
 #pragma unroll
@@ -2351,12 +2386,21 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
       __builtin_amdgcn_global_load_lds(const_cast<float*>(bsrc[q] + ko),  // (a const source fails the host pass)
                                        GTA_TO_LDS(base + A_BYTES + (wv * (NT / 4) + q) * 1024), 16, 0, 0);
   };
-  f32x4 acc[FR][NT];
+  constexpr int T32 = NT / 2;  // M32: 32-column tiles per wave
+  f32x4 acc[M32 ? 1 : FR][M32 ? 1 : NT];
+  f32x16 acc32[M32 ? T32 : 1];
   auto zero_acc = [&]() __attribute__((always_inline)) {
+    if constexpr (M32) {
 #pragma unroll
-    for (int i = 0; i < FR; ++i)
+      for (int t = 0; t < T32; ++t)
 #pragma unroll
-      for (int c = 0; c < NT; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+        for (int r = 0; r < 16; ++r) acc32[t][r] = 0.f;
+    } else {
+#pragma unroll
+      for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int c = 0; c < NT; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   };
   auto mma = [&](const float (&av)[FR][4], const float4& b4, int c) {
     const float bj[4] = {b4.x, b4.y, b4.z, b4.w};
@@ -2368,6 +2412,52 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   const bool vstore = ldo % 4 == 0 && aligned(out, 16);
   auto epilogue = [&](int64_t j) __attribute__((always_inline)) {
     const int64_t mw = (grp0 + j * gstep) * GR + wv * (16 * FR);
+    if constexpr (M32) {
+      // 32x32 C map: lane (h, c) holds column c, rows (reg & 3) + 8 (reg >> 2) + 4 h
+      sf_tile16(sf, acc32);
+      const int p = r32 & 3, q = r32 >> 2;
+#pragma unroll
+      for (int t = 0; t < T32; ++t)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4) {
+          if (vstore) {  // the same quad transpose: lane p then holds row 8 s4 + 4 h + p, columns 4q .. 4q + 3
+            float v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = acc32[t][4 * s4 + r];
+#pragma unroll
+            for (int m2 = 0; m2 < 2; ++m2) {
+              const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
+              const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2 + 1]), 0xB1, 0xF, 0xF, false));
+              if (p & 1) v[2 * m2] = sb; else v[2 * m2 + 1] = sa;
+            }
+#pragma unroll
+            for (int m2 = 0; m2 < 2; ++m2) {
+              const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2]), 0x4E, 0xF, 0xF, false));
+              const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2 + 2]), 0x4E, 0xF, 0xF, false));
+              if (p & 2) v[m2] = sb; else v[m2 + 2] = sa;
+            }
+            const int64_t m = mw + 8 * s4 + 4 * h32 + p;
+            const int n = n0 + 32 * t + 4 * q;
+            if (m < M) {
+              if (n + 3 < N) {
+                *reinterpret_cast<float4*>(out + m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
+              } else {
+#pragma unroll
+                for (int r = 0; r < 4; ++r)
+                  if (n + r < N) out[m * ldo + n + r] = v[r];
+              }
+            }
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+              const int64_t m = mw + 8 * s4 + 4 * h32 + r;
+              const int n = n0 + 32 * t + r32;
+              if (m < M && n < N) out[m * ldo + n] = acc32[t][4 * s4 + r];
+            }
+          }
+        }
+      return;
+    }
     sf_tile(sf, acc);
     if (vstore) {  // quad-transposed 16-B row stores (k_mm_rows' epilogue)
       const int p = r16 & 3, q = r16 >> 2;
@@ -2415,6 +2505,31 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
           }
     }
   };
+  auto tail32 = [&](int64_t j) __attribute__((always_inline)) {  // M32's K tail: k = kt + 4 (2m + h) + jj < K
+    for (int kt = S * KS; kt < K; kt += 16) {
+      float av[2][4], bv[T32][2][4];
+      const float* ar = a_row(j, f32r, r32 & 15);
+#pragma unroll
+      for (int m = 0; m < 2; ++m)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj) {
+          const int k = kt + 4 * (2 * m + h32) + jj;
+          av[m][jj] = k < K ? ar[k] : 0.f;
+#pragma unroll
+          for (int t = 0; t < T32; ++t) {
+            const int n = min(n0 + 32 * t + r32, N - 1);
+            bv[t][m][jj] = k < K ? wt[static_cast<int64_t>(n) * ldwt + k] : 0.f;
+          }
+        }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int t = 0; t < T32; ++t)
+            acc32[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][jj], bv[t][m][jj], acc32[t], 0, 0, 0);
+    }
+  };
   auto tail = [&](int64_t j) __attribute__((always_inline)) {  // the K tail from registers, 16 k per step:
     for (int kt = S * KS; kt < K; kt += 16) {                     // k = kt + 4g + jj < K, zeros past it
       const int k0 = kt + 4 * g;
@@ -2458,6 +2573,41 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     // fragment reads in inline asm: hipcc cannot tell them apart from the DMA in flight into
     // another slot and would wait vmcnt(0) before a plain LDS read (draining the ring every step).
     // The asm wait names every loaded register, so no MFMA is scheduled above it.
+    if constexpr (M32) {
+      const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * 1024);
+      const uint32_t sb = GTA_LDS_ADDR(lds + slot * STAGE + A_BYTES);
+      f32x4 a4[2], b4[T32][2];
+#pragma unroll
+      for (int m = 0; m < 2; ++m) ds_read16<0>(a4[m], sa + rd32[m]);
+#pragma unroll
+      for (int t = 0; t < T32; ++t)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) ds_read16_idx(b4[t][m], sb + rd32[m], 2 * t);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int m = 0; m < 2; ++m) asm volatile("" : "+v"(a4[m]));
+#pragma unroll
+      for (int t = 0; t < T32; ++t)
+#pragma unroll
+        for (int m = 0; m < 2; ++m) asm volatile("" : "+v"(b4[t][m]));
+      if (ring_tail && s == S - 1) {  // pieces past K: zeros
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+          if (dead32[m]) {
+            a4[m] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+            for (int t = 0; t < T32; ++t) b4[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int m = 0; m < 2; ++m)
+#pragma unroll
+          for (int t = 0; t < T32; ++t)
+            acc32[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[m][jj], b4[t][m][jj], acc32[t], 0, 0, 0);
+      continue;
+    }
     const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * 1024) + rdoff;
     const uint32_t sb = GTA_LDS_ADDR(lds + slot * STAGE + A_BYTES) + rdoff;
     f32x4 a4[FR], b4[NT];
@@ -2487,7 +2637,9 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
           acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i][jj], b4[c][jj], acc[i][c], 0, 0, 0);
   }
   // the group's last stage is done: its K tail, its rows out, the next group's sums
-  if (!ring_tail && (K % KS)) tail(j);
+  if (!ring_tail && (K % KS)) {
+    if constexpr (M32) tail32(j); else tail(j);
+  }
   epilogue(j);
   zero_acc();
   // the counted waits above assume only ring DMA is outstanding; stores may retire out of order
@@ -2896,6 +3048,7 @@ struct Tuning {
   int mm_ring = 1;         // fp32 UPDATE on k_mm_ring (LDS-DMA ring) instead of k_mm_rows
   int mm_ring_fr = 0;      // k_mm_ring A fragments per wave: 2 = 128-row groups, 1 = 64-row groups, 0 = auto
   int mm_ring_depth = 0;   // k_mm_ring stages: 0 = auto (by blocks per CU), else 3, 4 or 8
+  int mm_ring_m32 = 0;     // k_mm_ring 128-row groups on v_mfma_f32_32x32x2_f32 (the M32 form)
   int mm_prefetch = 1;     // k_mm_rows A prefetch: 1 auto, 2 always, 0 never
   int64_t mm_split = -1;   // UPDATE K slices: -1 auto, 0 = never split, n = n slices
 };
@@ -2954,6 +3107,7 @@ const Knob* find_knob(const char* key) {
       {"mm_ring", &Tuning::mm_ring, nullptr},
       {"mm_ring_fr", &Tuning::mm_ring_fr, nullptr},
       {"mm_ring_depth", &Tuning::mm_ring_depth, nullptr},
+      {"mm_ring_m32", &Tuning::mm_ring_m32, nullptr},
       {"mm_prefetch", &Tuning::mm_prefetch, nullptr},
       {"mm_split", nullptr, &Tuning::mm_split},
   };
@@ -3696,6 +3850,19 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
       const int64_t per_cu = dk == 8 ? 1 : dk == 4 ? (nt == 8 && fr == 2 ? 2 : 3) : (nt == 8 ? (fr == 1 ? 4 : 3) : 4);
       D = dk;
       blocks = std::min(n_grp, std::max<int64_t>(1, 256 * per_cu / ncb)) * ncb;
+    }
+    if (fr == 2 && D == 3 && tuning().mm_ring_m32) {  // the same ring on 32x32x2 MFMAs (bitwise equal)
+      const dim3 gr(static_cast<unsigned>(blocks));
+      const float* xf = static_cast<const float*>(x);
+      const float* wf = static_cast<const float*>(wt);
+      if (nt == 8)
+        k_mm_ring<8, 3, 2, true><<<gr, dim3(kBlock), 0, S(stream)>>>(xf, ldx, row_idx, M, static_cast<int>(K), wf, ldwt,
+                                                                     static_cast<int>(N), sf, out, ldo, 0, 0);
+      else
+        k_mm_ring<4, 3, 2, true><<<gr, dim3(kBlock), 0, S(stream)>>>(xf, ldx, row_idx, M, static_cast<int>(K), wf, ldwt,
+                                                                     static_cast<int>(N), sf, out, ldo, 0, 0);
+      GTA_LAUNCHED("k_mm_ring<m32>");
+      return GTA_OK;
     }
     launch_ring(nt, D, fr, dim3(static_cast<unsigned>(blocks)), S(stream), static_cast<const float*>(x), ldx, row_idx, M,
                 static_cast<int>(K), static_cast<const float*>(wt), ldwt, static_cast<int>(N), sf, out, ldo, 0, 0);

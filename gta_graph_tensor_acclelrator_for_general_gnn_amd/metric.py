@@ -58,16 +58,29 @@ def alpha_rows(lip, gen, device, seed=SEED, heads=HEADS):
     return ex.div_(s[row])
 
 
+def column_counts(n, e, device, seed=SEED, step=1 << 24):
+    """The whole graph's per-column nnz (the column sums of the tile metadata, code/preprocessing.py:
+    12-40) without a process group: every edge's source is a pure function of its id, so one
+    process can count them all, `step` edges at a time.  Equal to what Shard's count_reduce
+    all-reduces from every rank's rows."""
+    csr = G.CounterCSR(n, e, seed)
+    counts = torch.zeros(n, dtype=torch.int64, device=device)
+    for e0 in range(0, e, step):
+        counts += torch.bincount(csr.sources(e0, min(e, e0 + step), device), minlength=n)
+    return counts
+
+
 class Shard:
     """Rank `rank`'s part of the metric workload on a pr x pc grid (distributed.GridShard layout):
     graph (its tile as a CSR over its row group's padded rows, local source ids), x (X1 rows of its
     column group), alpha (its tile's edges).  `count_reduce(counts)` sums the per-column nnz
     histogram over the ranks (an all-reduce; None on one rank): the column cuts come from the
     whole graph's tile metadata (column sums of calculate_sparsity, code/preprocessing.py:12-40)
-    although each rank generated only its rows."""
+    although each rank generated only its rows.  `col_counts`: that whole-graph histogram given
+    directly (column_counts: a rank's tile rebuilt alone, e.g. by bench's PMC child)."""
 
     def __init__(self, n, e, rank, pr, pc, chunks, device, seed=SEED, count_reduce=None, keep_rows=True,
-                 note=None, fracs=None):
+                 note=None, fracs=None, col_counts=None):
         note = note or (lambda msg: None)
         self.n, self.e, self.seed, self.device = n, e, seed, device
         self.csr = G.CounterCSR(n, e, seed)
@@ -79,7 +92,9 @@ class Shard:
         note(f"row group {i}: rows [{r0}, {r1}), {src.numel()} edges generated")
         alpha = alpha_rows(lip, gen, device, seed)
         del gen
-        if pc > 1:
+        if pc > 1 and col_counts is not None:
+            ccuts = [int(c) for c in partition.cuts_from_counts(col_counts.to(device), pc)]
+        elif pc > 1:
             counts = torch.bincount(src, minlength=n)
             if count_reduce is not None:
                 counts = count_reduce(counts) // pc  # every rank of a row group added the same counts

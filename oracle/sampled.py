@@ -94,11 +94,55 @@ class SampledChecker:
             A, B, b = B, A, "DIV"
         return isa_ref.binop(b, A, B)
 
-    def check(self, n_samples=48, seed=0, rtol=2e-4, skip_ops=()):
-        """Returns {op: normalised max error}; raises AssertionError beyond rtol."""
+    def special_rows(self, per_class=2):
+        """{class: node ids} checked in every op on top of the random sample: the first
+        and last row, the heaviest rows, the lightest non-empty and the empty rows, rows cut into
+        several work items (> 256 edges: blocked-plan items; > 512: row-chunk plan slices; > 1024:
+        three or more slices), and rows holding edges on both sides of a source-column block
+        boundary of every blocked plan the executor's graph built (B blocks of ceil(n_cols / B)
+        columns, gta_aggregate_blocked_plan_build)."""
+        deg = np.diff(self.ip)
+        N = len(deg)
+        if N == 0:
+            return {}
+        out = {"first": np.array([0]), "last": np.array([N - 1])}
+        order = np.argsort(deg, kind="stable")
+        out["heaviest"] = order[-2 * per_class:][::-1]
+        nz = np.flatnonzero(deg > 0)
+        out["lightest"] = nz[np.argsort(deg[nz], kind="stable")[:per_class]]
+        out["empty"] = np.flatnonzero(deg == 0)[:per_class]
+        for name, lo, hi in (("items_256", 256, 512), ("plan_512", 512, 1024), ("plan_1024", 1024, None)):
+            m = deg > lo if hi is None else (deg > lo) & (deg <= hi)
+            out[name] = np.flatnonzero(m)[:per_class]
+        graph = getattr(self.ex, "graph", None)
+        n_cols = getattr(graph, "n_cols", N)
+        blocks = sorted({k[1] for k in getattr(graph, "_plans", {}) if isinstance(k, tuple) and k[0] == "blocked"})
+        for B in blocks:
+            bsize = -(-n_cols // B)
+            rows = []
+            for b in sorted({bsize, (B // 2) * bsize, (B - 1) * bsize}):
+                if not 0 < b < n_cols:
+                    continue
+                lo_rows = self.dst_of(np.flatnonzero(self.ix == b - 1))
+                hi_rows = self.dst_of(np.flatnonzero(self.ix == b))
+                both = np.intersect1d(lo_rows, hi_rows)
+                rows.extend((both if both.size else hi_rows)[:1])
+            out[f"block_edge_B{B}"] = np.asarray(rows, np.int64)
+        return {k: np.asarray(v, np.int64) for k, v in out.items() if len(v)}
+
+    def check(self, n_samples=48, seed=0, rtol=2e-4, skip_ops=(), n_gather=128):
+        """Returns {op: normalised max error}; raises AssertionError beyond rtol.  Node values are
+        checked at n_samples random rows (n_gather for gathers, the aggregates) plus every row of
+        special_rows(); edge values at n_samples random edges plus the first and last edge of each
+        special row.  The special rows are named in the assertion message and kept in self.special."""
         from gta_graph_tensor_acclelrator_for_general_gnn_amd import executor as X
         rng = np.random.default_rng(seed)
         N, E = len(self.ip) - 1, len(self.ix)
+        self.special = self.special_rows()
+        sp_rows = np.unique(np.concatenate(list(self.special.values()))) if self.special else np.zeros(0, np.int64)
+        nz = sp_rows[self.ip[sp_rows + 1] > self.ip[sp_rows]]
+        sp_edges = np.unique(np.concatenate([self.ip[nz], self.ip[nz + 1] - 1])) if nz.size else np.zeros(0, np.int64)
+        listing = ", ".join(f"{k}={v.tolist()}" for k, v in self.special.items())
         report = {}
         for op in self.g.ops:
             if op.idx in skip_ops:
@@ -109,14 +153,17 @@ class SampledChecker:
             if not isinstance(v, (X.NodeT, X.EdgeT)):
                 continue
             kind = "node" if isinstance(v, X.NodeT) else "edge"
-            idx = rng.choice(N if kind == "node" else E, size=min(n_samples, N if kind == "node" else E),
-                             replace=False)
+            total = N if kind == "node" else E
+            k = n_gather if op.type == "gather" else n_samples
+            idx = rng.choice(total, size=min(k, total), replace=False)
+            idx = np.unique(np.concatenate([idx, sp_rows if kind == "node" else sp_edges]))
             got = self.value_at(v, kind, idx)
             exp = self.expected(op, kind, idx)
             fin = np.isfinite(exp)
-            assert np.array_equal(np.isfinite(got), fin), f"op {op.idx}: non-finite pattern differs"
+            assert np.array_equal(np.isfinite(got), fin), f"op {op.idx}: non-finite pattern differs ({listing})"
             scale = np.abs(exp[fin]).max() if fin.any() else 0.0
             err = float(np.abs(got[fin] - exp[fin]).max() / (scale + 1e-30)) if fin.any() else 0.0
             report[op.idx] = err
-            assert err <= rtol, f"op {op.idx} ({op.type}/{op.comp}): normalised max err {err:.2e}"
+            assert err <= rtol, (f"op {op.idx} ({op.type}/{op.comp}): normalised max err {err:.2e} over "
+                                 f"{idx.size} {kind}s incl. special rows {listing}")
         return report

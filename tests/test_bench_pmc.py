@@ -44,3 +44,38 @@ def test_agg_split_and_reduce_bytes():
     # the reduce reads every partial row once and writes y: never below that compulsory traffic
     assert r["reduce_bytes"] >= partial + 232965 * 512 - 1
     assert abs(r["bytes_per_launch"] - (r["agg_bytes"] + r["reduce_bytes"])) < 1
+
+
+def test_split_sums_a_steps_launch_pairs():
+    """A tile cut into row chunks launches one (k_agg_h32, k_seg_reduce) pair per non-empty chunk
+    per step: _split sums them per step, after the calibration dispatches."""
+    rows = [(0, "k_apply_node4", 5.0), (1, "k_apply_node4", 6.0), (2, "k_aggregate<32>", 7.0),
+            (3, "k_aggregate<32>", 8.0)]
+    did = 4
+    for step in range(3):
+        for c, (a, b) in enumerate(((100.0, 10.0), (30.0, 3.0))):
+            rows += [(did, "k_agg_h32", a + step), (did + 1, "k_seg_reduce", b)]
+            did += 2
+    copy, gather, steps = bench._split(rows, per_step=2)
+    assert copy == [5.0, 6.0] and gather == [7.0, 8.0]
+    assert steps == [(130.0, 13.0), (132.0, 13.0), (134.0, 13.0)]
+    assert len(bench._split(rows, per_step=1)[2]) == 6
+
+
+def test_rank_roofline_fields():
+    """The N > 1 line's roofline: the critical (longest-compute) rank's traffic / achieved / frac in
+    front, every rank's compute / own step / exposed exchange split, job-wide bytes over the
+    critical time; a rank without PMC bytes leaves its own fields and the job total None."""
+    per = [{"rank": 0, "tile_edges": 100, "tile_rows": 10, "compute_ms": 0.50, "step_ms": 0.60, "traffic": 3.0e9},
+           {"rank": 1, "tile_edges": 120, "tile_rows": 10, "compute_ms": 0.55, "step_ms": 0.58, "traffic": 3.3e9}]
+    r = bench.rank_roofline(per)
+    assert r["rank_basis"] == 1 and abs(r["kernel_ms"] - 0.55) < 1e-12
+    assert abs(r["achieved"] - 3.3e9 / 0.55e-3 / 1e9) < 1e-6 and abs(r["frac"] - r["achieved"] / 8000.0) < 1e-12
+    assert abs(r["job_achieved_GBps"] - 6.3e9 / 0.55e-3 / 1e9) < 1e-6 and r["job_peak_GBps"] == 16000.0
+    assert [round(x["exposed_exchange_ms"], 6) for x in r["per_rank"]] == [0.1, 0.03]
+    assert set(r["per_rank"][0]) == {"rank", "tile_edges", "tile_rows", "compute_ms", "step_ms",
+                                     "exposed_exchange_ms", "traffic", "achieved", "frac"}
+    assert r["frac_min"] <= r["frac"] <= r["frac_max"]
+    per[0]["traffic"] = float("nan")
+    r = bench.rank_roofline(per)
+    assert r["per_rank"][0]["frac"] is None and r["job_achieved_GBps"] is None and r["frac"] is not None

@@ -27,5 +27,13 @@ def test_config_full_size_sampled_parity(dev, name):
             assert fin[has_edges].all(), f"{name}: non-finite output of op {k} at a row with edges"
             if not lay.reorder:
                 assert fin.all(), f"{name}: non-finite output of op {k}"
-        report = SampledChecker(ex, ip, ix).check(n_samples=24, seed=1)
+        chk = SampledChecker(ex, ip, ix)
+        report = chk.check(n_samples=32, seed=1, n_gather=128)
         assert report, "nothing was checked"
+        # the heaviest rows, split-row and column-block boundary rows, empty rows and
+        # the first / last row are always among the checked rows
+        sp = chk.special
+        for cls in ("first", "last", "heaviest", "lightest"):
+            assert cls in sp, (name, sorted(sp))
+        assert any(c.startswith("block_edge_B") for c in sp) or not any(
+            isinstance(k, tuple) and k[0] == "blocked" for k in g._plans), (name, sorted(sp))

@@ -53,8 +53,9 @@ def test_two_rank_sage_reddit_full_size():
     recs = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")]
     assert len(recs) == 1 and recs[0]["config"] == "sage-reddit", r.stdout[-2000:]
     x = recs[0]
-    # max |d| / max |ref|: the shard's GEMMs run on M = 116k rows instead of 233k (another library
-    # algorithm, fp32 rounding of a K = 602 contraction) -- far inside the GEMM bar 1e-5 * sum|x||w|
+    # max |d| / max |ref|: the shard runs its own plans (the blocked aggregate's column blocks and item
+    # cuts follow the shard's shape, so each row's partial sums are added in another order) -- fp32
+    # rounding, far inside the aggregate bar 1e-5 * sum|terms|
     assert x["n_gpus"] == 2 and x["max_norm_diff_vs_1dev"] is not None and x["max_norm_diff_vs_1dev"] <= 1e-5, x
 
 
@@ -63,18 +64,31 @@ def test_two_rank_sage_reddit_full_size():
 def test_two_rank_bench_full_size(mode):
     """bench.py --gpus 2 at the full metric size, both ranks on one GPU over gloo (RCCL cannot
     put two ranks on one device): each rank generates only its shard, the exchange runs, and every
-    rank's sampled output rows match the fp64 oracle (the bench's own parity field)."""
+    rank's sampled output rows match the fp64 oracle (the bench's own parity field).  The N > 1 line
+    carries what the N = 1 line does: each rank's own PMC bytes (its child rebuilt the
+    tile alone) with the critical rank's frac in front, the per-rank compute / exposed-exchange
+    split, and the CPU baseline from rank 0."""
     env = dict(os.environ, GTA_DIST_BACKEND="gloo", GTA_SINGLE_DEVICE="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
-           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1", "--warmup", "1", "--mode", mode,
-           "--parity-rows", "128"]
+           os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--mode", mode,
+           "--parity-rows", "128", "--cpu-baseline-s", "3"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")][-1]
     assert rec["n_gpus"] == 2 and rec["config"]["mode"] == mode and rec["config"]["world_size_seen"] == 2
     assert rec["config"]["N"] == 232965 and rec["config"]["E"] == 114615892
     assert rec["parity"]["ok"] and rec["parity"]["max_err_over_bound"] <= 1.0, rec["parity"]
+    roof = rec["roofline"]
+    assert "pmc_error" not in roof, roof.get("pmc_error")
+    assert roof["frac"] is not None and 0.05 < roof["frac"] < 1.0, roof
+    assert len(roof["per_rank"]) == 2 and sum(p["tile_edges"] for p in roof["per_rank"]) == (
+        114615892 if mode == "edges" else sum(p["tile_edges"] for p in roof["per_rank"]))
+    for p in roof["per_rank"]:
+        assert p["frac"] is not None and p["traffic"] > 0 and p["compute_ms"] > 0
+        assert p["exposed_exchange_ms"] >= 0 and p["step_ms"] > 0
+    cb = rec["cpu_baseline"]
+    assert cb is not None and cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port", cb
 
 
 @pytest.mark.gpu

@@ -678,7 +678,8 @@ def test_update_mm_mid_rows_hand_written(dev, M, K, N, ldx_pad):
 @pytest.mark.parametrize("M,K,N,gathered,sf", [(40000, 602, 128, False, None), (20000, 602, 128, True, "RELU"),
                                                (33000, 37, 200, False, None), (3001, 64, 64, False, "RELU"),
                                                (17000, 1433, 128, False, None), (777, 100, 100, True, None),
-                                               (130, 48, 72, False, "ELU"), (89250, 500, 128, False, None)])
+                                               (130, 48, 72, False, "ELU"), (89250, 500, 128, False, None),
+                                               (20000, 600, 66, False, "RELU"), (20000, 604, 64, True, None)])
 def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     """k_mm_ring (fp32 UPDATE through the LDS-DMA ring, the default for fp32 GEMMs) == k_mm_rows
     bitwise (same per-lane k order and MFMA chain), and both within the fp64 bound: K tails
@@ -697,14 +698,18 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     old_min = ops.MM_ROWS_MIN_M
     try:
         ops.MM_ROWS_MIN_M = 0
-        # k_mm_rows, then the ring with 128-row groups, 64-row groups, and the automatic choice
-        for ring, fr in ((0, 0), (1, 2), (1, 1), (1, 0)):
+        # k_mm_rows, then the ring with 128-row groups, 64-row groups, the automatic choice, and
+        # 128-row groups on 32x32x2 MFMAs (the M32 form: K tails in registers (602, 1433) and as a
+        # ring stage (600, 604), 32-column tiles past N (66, 100, 200), non-vector stores (N = 66))
+        for ring, fr, m32 in ((0, 0, 0), (1, 2, 0), (1, 1, 0), (1, 0, 0), (1, 2, 1)):
             ops.set_debug("mm_ring", ring)
             ops.set_debug("mm_ring_fr", fr)
+            ops.set_debug("mm_ring_m32", m32)
             outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
     finally:
         ops.set_debug("mm_ring", 1)
         ops.set_debug("mm_ring_fr", 0)
+        ops.set_debug("mm_ring_m32", 0)
         ops.MM_ROWS_MIN_M = old_min
     torch.cuda.synchronize()
     for o in outs[1:]:

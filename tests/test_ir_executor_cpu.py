@@ -295,3 +295,32 @@ def test_sibling_weight_concat_is_cached_and_follows_in_place_updates(golden_dir
     assert wc2 is not wc and torch.equal(wc2[:, -sib.shape[1]:], sib)
     ref = execute_ref(og, sem, ip, ix, {k: v.numpy() for k, v in tensors.items()})
     compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
+
+
+def test_sampled_checker_always_checks_the_special_rows(golden_dir, manifest, monkeypatch):
+    """oracle/sampled.py (the full-size config check): the heaviest, lightest, empty, first and
+    last rows are checked in every op whatever the random sample, so an error confined to the
+    heaviest row of an aggregate is caught even with a tiny random sample."""
+    from oracle.sampled import SampledChecker
+    rec = [s for s in _streams(manifest) if s["network"] == "GCN" and not s["reorder"]][0]
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    g, ip, ix = _cora_graph(golden_dir)
+    sem = Semantics.for_network("GCN", False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    ex = executor.Executor(og, st, g, workloads.make_tensors(og, g, "GCN", seed=2), sem, plan_chunk=0)
+    ex.run()
+    chk = SampledChecker(ex, ip, ix)
+    assert chk.check(n_samples=2, seed=0, n_gather=2)
+    sp = chk.special
+    deg = np.diff(ip)
+    assert set(sp) >= {"first", "last", "heaviest", "lightest"}
+    assert deg[sp["heaviest"][0]] == deg.max() and sp["last"][0] == len(deg) - 1
+    vals = {op.idx: ex.values.get(op.idx) for op in og.ops if op.type == "gather"}
+    vals = {i: (v.force() if isinstance(v, executor.Lazy) else v) for i, v in vals.items()}
+    gat = [i for i, v in vals.items() if isinstance(v, executor.NodeT)]
+    assert gat, "a materialised aggregate to corrupt"
+    t = vals[gat[0]].t
+    t[int(sp["heaviest"][0])] += 1.0
+    with pytest.raises(AssertionError, match="heaviest"):
+        chk.check(n_samples=2, seed=0, n_gather=2)

@@ -210,3 +210,18 @@ def test_bench_exchange_gloo(world, mode, n, e):
     assert sum(o[5] for o in out) == (e if mode == "edges" else sum(o[5] for o in out))
     if e < world:
         assert any(o[5] == 0 for o in out)  # at least one rank held an empty tile
+
+
+@pytest.mark.parametrize("pr,pc", [(1, 2), (2, 2), (4, 2)])
+def test_column_counts_rebuild_a_tile_alone(pr, pc):
+    """metric.column_counts (one process counting every edge's source, no process group) equals the
+    all-reduced row-group histograms, so a rank's tile rebuilt alone -- bench's per-rank PMC child --
+    has the same column cuts, edges and alpha as the tile the distributed run builds."""
+    cc = metric.column_counts(N, E, "cpu", step=7777)
+    assert torch.equal(cc * pc, _global_counts(pr, pc)(None))
+    for r in range(pr * pc):
+        a = metric.Shard(N, E, r, pr, pc, 2, "cpu", count_reduce=_global_counts(pr, pc), fracs=(0.7, 0.3))
+        b = metric.Shard(N, E, r, pr, pc, 2, "cpu", col_counts=cc, fracs=(0.7, 0.3), keep_rows=False)
+        assert (a.grid.c0, a.grid.c1) == (b.grid.c0, b.grid.c1)
+        assert torch.equal(a.graph.indptr, b.graph.indptr) and torch.equal(a.graph.indices, b.graph.indices)
+        assert torch.equal(a.alpha, b.alpha) and torch.equal(a.x, b.x)
