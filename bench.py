@@ -278,7 +278,7 @@ def _split(rows, per_step=1):
     from ordered counter rows: a step's launch pairs (one per non-empty row chunk of the tile) summed."""
     copy, gather, pairs, cur = [], [], [], None
     for _, name, v in rows:
-        if "k_agg_h32" in name or "k_agg_seg" in name:
+        if "k_agg_h32" in name or "k_agg_seg" in name or "k_agg_xl" in name:
             cur = [v, 0.0]
         elif "k_seg_reduce" in name and cur is not None:
             cur[1] = v
@@ -334,7 +334,8 @@ def collect_pmc(args, out_dir, world=1, rank=0, local=0):
                    "--pmc-world", str(world), "--pmc-rank", str(rank), "--pmc-local", str(local),
                    "--mode", args.mode, "--grid", args.grid, "--row-chunks", str(args.row_chunks),
                    "--chunk-fracs", args.chunk_fracs,
-                   "--n", str(args.n), "--e", str(args.e), "--blocks", str(args.blocks), "--impl", args.impl]
+                   "--n", str(args.n), "--e", str(args.e), "--blocks", str(args.blocks), "--impl", args.impl,
+                   "--knobs", args.knobs]
             t0 = time.time()
             rc, err = _run_group(cmd, env, 240)
             if rc is None:
@@ -530,12 +531,17 @@ def main():
                     help="CPU work per thread count of the cpu_baseline leg (seconds, approx.)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
     ap.add_argument("--pmc-dir", default="", help="keep the --pmc CSVs here (default: a temp dir)")
+    ap.add_argument("--knobs", default="", help="libgta tuning knobs for every launch, e.g. seg_xcd=2,seg_nt=3 "
+                                               "(also passed to the PMC children)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-meta", default="", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-world", type=int, default=1, help=argparse.SUPPRESS)
     ap.add_argument("--pmc-rank", type=int, default=0, help=argparse.SUPPRESS)
     ap.add_argument("--pmc-local", type=int, default=0, help=argparse.SUPPRESS)
     args = ap.parse_args()
+    for kv in filter(None, args.knobs.split(",")):
+        k, v = kv.split("=")
+        ops.set_debug(k.strip(), int(v))
     if args.pmc_child:
         return pmc_child(args)
 

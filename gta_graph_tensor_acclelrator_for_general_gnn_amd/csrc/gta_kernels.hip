@@ -845,6 +845,136 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
   }
 }
 
+// XCD line split of k_agg_h32 (F = 128; knob seg_xcd = NL = 2 or 4 line groups).  The chip's
+// 8 XCDs each have a private 4 MiB L2, and the dispatcher deals blocks round-robin over them, so
+// blocks b and b + 8 share one (MI355X_MICROARCH.md §Workgroup dispatch: a speed hint, never a
+// correctness one).  Here block b's label x = b % 8 picks a feature LINE L = x % NL (the
+// 512 / NL bytes [L * 512/NL, +512/NL) of every X row) and a PART x / NL of the items; every item
+// is run NL times, once per line, by blocks of NL different labels.  An XCD then gathers only its
+// line of the rows of the current column block: its L2 footprint is 1/NL of the full-row
+// form's, so the same column block stays L2-resident at NL x fewer blocks -- fewer items, fewer
+// partial rows -- or the same blocks hit L2 more often.  The indices and weights of an item are read
+// by the NL line groups at about the same time (each XCD reads its heads' weights), so the repeats
+// come from the Infinity Cache.  Per item-line: G = 32 / NL lanes x float4, 64 / G items per
+// wave; lane l of a group holds columns 4 (L G + l) .. +3, so its head, weight loads (two per
+// 8-edge step, DPP quad broadcast), fma chain and partial slots are k_agg_h32's for those
+// columns: partial rows bitwise equal to k_agg_h32's, and the same k_seg_reduce follows.
+template <int G>
+__device__ __forceinline__ int bcast8_16(int v, int k) {  // lane k of each G-lane group, G = 8 or 16
+  static_assert(G == 8 || G == 16, "group of 8 or 16 lanes");
+  switch (k) {
+#define GTA_BG(K_) case K_: return __builtin_amdgcn_ds_swizzle(v, (0x1F & ~(G - 1)) | (((K_) % G) << 5));
+    GTA_BG(0) GTA_BG(1) GTA_BG(2) GTA_BG(3) GTA_BG(4) GTA_BG(5) GTA_BG(6) GTA_BG(7)
+    GTA_BG(8) GTA_BG(9) GTA_BG(10) GTA_BG(11) GTA_BG(12) GTA_BG(13) GTA_BG(14) GTA_BG(15)
+#undef GTA_BG
+  }
+  return v;
+}
+
+template <bool WEIGHTED, int NT, bool W1, int G>
+__global__ void __launch_bounds__(kBlock)
+k_agg_xl(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
+         uint32_t row_bytes, const float* __restrict__ w, int64_t ldw, float* __restrict__ slabs,
+         const SegItem* __restrict__ items) {
+  constexpr int F = 128, U = 8, NL = 32 / G, P = 8 / NL, IW = kWave / G;
+  static_assert(G == 8 || G == 16, "line groups of 8 or 16 lanes");
+  const int lane = threadIdx.x & (kWave - 1);
+  const int lg = lane & (G - 1);
+  const int xl = static_cast<int>(blockIdx.x & 7);             // the blocks sharing an XCD
+  const int L = xl % NL, part = xl / NL;
+  const int64_t slot = blockIdx.x >> 3;
+  const int64_t k = ((slot * P + part) * kWavesPerBlock + wave_id_uniform()) * IW + lane / G;
+  const int64_t n_items = *n_items_p;
+  SegItem it{0, 0, 0};
+  if (k < n_items) it = items[k];
+  const int len = it.len;
+  int mx = len, mn = len;
+#pragma unroll
+  for (int off = G; off < kWave; off <<= 1) {
+    mx = max(mx, __shfl_xor(mx, off));
+    mn = min(mn, __shfl_xor(mn, off));
+  }
+  const int maxlen = __builtin_amdgcn_readfirstlane(mx);
+  const int minlen = __builtin_amdgcn_readfirstlane(mn);
+  if (maxlen == 0) return;
+  const int cl = L * G + lg;                                    // this lane's float4 of the row
+  const uint32_t colb = static_cast<uint32_t>(cl) * 16u;
+  const char* xb = reinterpret_cast<const char*>(x);
+  const int h = cl >> 2, q = cl & 3;
+  const int ldw32 = static_cast<int>(ldw);
+  const int32_t* ic = indices + it.beg;
+  const float* wc = WEIGHTED ? w + it.beg * ldw + (W1 ? 0 : h) : nullptr;
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  auto ldi = [&](const int32_t* p) { return (NT & 1) ? __builtin_nontemporal_load(p) : *p; };
+  auto ldw_ = [&](const float* p) { return (NT & 4) ? __builtin_nontemporal_load(p) : *p; };
+  auto row = [&](int src) -> float4 {
+    return *reinterpret_cast<const float4*>(xb + (__umul24(static_cast<uint32_t>(src), row_bytes) + colb));
+  };
+  int idxv = (lg < len) ? ldi(ic + lg) : 0;
+  float wv = (W1 && lg < len) ? ldw_(wc + lg * ldw32) : 0.f;
+  for (int c = 0; c < maxlen; c += G) {
+    const int idxn = (c + G + lg < len) ? ldi(ic + G + lg) : 0;
+    const float wvn = (W1 && c + G + lg < len) ? ldw_(wc + (G + lg) * ldw32) : 0.f;
+#pragma unroll
+    for (int s = 0; s < G; s += U) {
+      if (c + s >= maxlen) break;
+      float4 xv[U];
+      float wu[U];
+      if (c + s + U <= minlen) {  // full step for every item of the wave: no masks
+#pragma unroll
+        for (int u = 0; u < U; ++u) xv[u] = row(bcast8_16<G>(idxv, s + u));
+        if (WEIGHTED && W1) {
+#pragma unroll
+          for (int u = 0; u < U; ++u) wu[u] = __int_as_float(bcast8_16<G>(__float_as_int(wv), s + u));
+        } else if (WEIGHTED) {
+          const float* wp = wc + (s + 2 * q) * ldw32;
+          const float w0 = ldw_(wp), w1 = ldw_(wp + ldw32);
+          wu[0] = quad_bcast<0>(w0); wu[1] = quad_bcast<0>(w1);
+          wu[2] = quad_bcast<1>(w0); wu[3] = quad_bcast<1>(w1);
+          wu[4] = quad_bcast<2>(w0); wu[5] = quad_bcast<2>(w1);
+          wu[6] = quad_bcast<3>(w0); wu[7] = quad_bcast<3>(w1);
+        }
+      } else {
+        const int rem = len - c - s;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int src = bcast8_16<G>(idxv, s + u);
+          if (u < rem) {
+            xv[u] = row(src);
+            if (WEIGHTED) wu[u] = W1 ? __int_as_float(bcast8_16<G>(__float_as_int(wv), s + u)) : ldw_(wc + (s + u) * ldw32);
+          } else {
+            xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (WEIGHTED) wu[u] = 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        if (WEIGHTED) {
+          acc[0] = fmaf(wu[u], xv[u].x, acc[0]);
+          acc[1] = fmaf(wu[u], xv[u].y, acc[1]);
+          acc[2] = fmaf(wu[u], xv[u].z, acc[2]);
+          acc[3] = fmaf(wu[u], xv[u].w, acc[3]);
+        } else {
+          acc[0] += xv[u].x; acc[1] += xv[u].y; acc[2] += xv[u].z; acc[3] += xv[u].w;
+        }
+      }
+    }
+    idxv = idxn;
+    if (W1) wv = wvn;
+    ic += G;
+    if (WEIGHTED) wc += static_cast<int64_t>(G) * ldw;
+  }
+  if (len > 0) {
+    float* o = slabs + k * F + cl * 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (NT & 2) __builtin_nontemporal_store(acc[t], o + t);
+      else o[t] = acc[t];
+    }
+  }
+}
+
 // Lean half-wave form of the fused GAT attention item (k_agg_seg4<4, 8, ATT, SFC = exp-leaky-
 // relu, G = 32>) for F = 128, 8 heads: the weighted k_agg_h32 loop with the edge weight computed,
 // v = exp(leaky_relu(a[row, h] + b[src, h])), instead of loaded.  Per full 8-edge step lane
@@ -3039,6 +3169,7 @@ struct Tuning {
   int agg_lean = 1;        // k_agg_lean for F = 64*VW SpMM shapes (0: k_aggregate, the form of other shapes)
   int seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
   int seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
+  int seg_xcd = 1;         // k_agg_xl line groups (2 or 4: each XCD gathers 1/NL of every row; 1 = k_agg_h32)
   int seg_phase = 0;       // blocked aggregate: 0 = items + reduce, 1 = items only, 2 = reduce only (bench timing)
   int att_lean = 1;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads (0: the generic half-wave form)
   int att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
@@ -3097,6 +3228,7 @@ const Knob* find_knob(const char* key) {
       {"agg_vw", &Tuning::force_vw, nullptr},
       {"agg_lean", &Tuning::agg_lean, nullptr},
       {"seg_lean", &Tuning::seg_lean, nullptr},
+      {"seg_xcd", &Tuning::seg_xcd, nullptr},
       {"seg_lean_w1", &Tuning::seg_lean_w1, nullptr},
       {"seg_phase", &Tuning::seg_phase, nullptr},
       {"att_lean", &Tuning::att_lean, nullptr},
@@ -3455,7 +3587,15 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     const uint32_t rb = static_cast<uint32_t>(ldx * 4);
     // NT template bits: 1 = non-temporal index loads, 2 = non-temporal slab stores (measured -0.5 % / -1 %;
     // non-temporal weight loads +3 %: profiles/r02_nt_bits_ab.json)
-    if (lean) {
+    const int nl = tuning().seg_xcd;
+    if (lean && (nl == 2 || nl == 4)) {
+      // every item once per line group: 8 block labels x one 64-item slot each
+      const dim3 gx(static_cast<unsigned>(8 * ((items + 63) / 64)));
+#define GTA_XL(G_)                                                                                     if (w && heads == 1) k_agg_xl<true, 2, true, G_><<<gx, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);   else if (w) k_agg_xl<true, 3, false, G_><<<gx, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);         else k_agg_xl<false, 2, false, G_><<<gx, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its)
+      if (nl == 4) { GTA_XL(8); } else { GTA_XL(16); }
+#undef GTA_XL
+      GTA_LAUNCHED("k_agg_xl");
+    } else if (lean) {
       if (w && heads == 1) k_agg_h32<true, 2, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
       else if (w) k_agg_h32<true, 3><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
       else k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);

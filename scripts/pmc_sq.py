@@ -18,7 +18,7 @@ GROUPS = {
                  "SQ_ACTIVE_INST_LDS", "SQ_INSTS_SMEM", "GRBM_GUI_ACTIVE"],
     "l2": ["TCC_HIT_sum", "TCC_MISS_sum", "TCP_TCC_READ_REQ_sum"],
 }
-KERNELS = ("k_agg_h32", "k_seg_reduce")
+KERNELS = ("k_agg_h32", "k_agg_xl", "k_seg_reduce")
 
 
 def summarize(d):
@@ -39,6 +39,9 @@ def summarize(d):
     return out
 
 
+EXTRA = []  # bench.py arguments after OUT_DIR (e.g. --blocks 16 --knobs seg_xcd=2)
+
+
 def main(out_dir):
     os.makedirs(out_dir, exist_ok=True)
     env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
@@ -48,7 +51,7 @@ def main(out_dir):
         shutil.rmtree(d, ignore_errors=True)
         cmd = ["timeout", "-s", "KILL", "120", shutil.which("rocprofv3") or "rocprofv3", "--kernel-trace", "--pmc",
                *counters, "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable,
-               os.path.join(ROOT, "bench.py"), "--pmc-child", "--steps", "4"]
+               os.path.join(ROOT, "bench.py"), "--pmc-child", "--steps", "4", *EXTRA]
         p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True)
         print(gname, "rc", p.returncode, p.stderr[-300:] if p.returncode else "", flush=True)
         if p.returncode != 0:
@@ -64,4 +67,10 @@ def main(out_dir):
 
 
 if __name__ == "__main__":
+    EXTRA.extend(sys.argv[2:])
+    if os.environ.get("PMC_GROUPS"):  # e.g. PMC_GROUPS=l2: only those counter groups
+        keep = os.environ["PMC_GROUPS"].split(",")
+        for g in list(GROUPS):
+            if g not in keep:
+                del GROUPS[g]
     sys.exit(main(sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc_sq"))

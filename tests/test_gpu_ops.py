@@ -388,11 +388,12 @@ def test_edge_softmax_other_sf_and_errors(dev):
         ops.edge_softmax(g, a, b[:, :4].contiguous())
 
 
-@pytest.mark.parametrize("knobs", [{"seg_lean": 0}, {"seg_lean_w1": 0}])
+@pytest.mark.parametrize("knobs", [{"seg_lean": 0}, {"seg_lean_w1": 0}, {"seg_xcd": 2}, {"seg_xcd": 4}])
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 0), (64, 4), (256, 16), (128, 1)])
 def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     """The lean half-wave kernels (k_agg_h32, also with one weight per edge) == the generic
-    half-wave form bitwise (same per-item edge order and fma chain), and == the fp64 oracle."""
+    half-wave form bitwise (same per-item edge order and fma chain), and == the fp64 oracle; so do
+    the XCD line-split forms (k_agg_xl: 2 or 4 line groups, each item run once per line)."""
     n, e = 900, 30000
     g = G.synthetic(n, e, seed=F + heads, device=dev)
     ip, ix = g.numpy()
