@@ -11,3 +11,5 @@ for v in "20 1" "16 2" "8 4"; do
   rc=$?; echo "pmc l2 B=$1 NL=$2 rc=$rc"; tail -1 gpurun_out/pmc_l2_b$1_x$2.log; [ $rc -eq 0 ] || exit $rc
 done
 STEPS="tests smoke bench bench2" PYTEST_ARGS="--timeout 300 --timeout-method thread" BENCH2_MODES=edges bash scripts/gpu_round.sh
+timeout -k 10 300 python -u scripts/gin_ic_probe.py > gpurun_out/gin_ic_probe.log 2>&1
+rc=$?; echo "gin_ic_probe rc=$rc"; cat gpurun_out/gin_ic_probe.log | grep '^{'
