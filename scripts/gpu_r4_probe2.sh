@@ -13,3 +13,5 @@ done
 STEPS="tests smoke bench bench2" PYTEST_ARGS="--timeout 300 --timeout-method thread" BENCH2_MODES=edges bash scripts/gpu_round.sh
 timeout -k 10 300 python -u scripts/gin_ic_probe.py > gpurun_out/gin_ic_probe.log 2>&1
 rc=$?; echo "gin_ic_probe rc=$rc"; cat gpurun_out/gin_ic_probe.log | grep '^{'
+timeout -k 10 400 python -u scripts/tile_chunks.py --grid 4x2 --rank 0 1 0.5,0.5 0.7,0.3 0.6,0.4 0.55,0.3,0.15 0.5,0.3,0.2 0.6,0.25,0.15 > gpurun_out/tile_chunks.log 2>&1
+rc=$?; echo "tile_chunks rc=$rc"; grep '^{' gpurun_out/tile_chunks.log
