@@ -208,8 +208,8 @@ def build(args, world, rank, dev, backend, note, col_counts=None):
         shard = metric.Shard(args.n, args.e, rank, pr, pc, chunks, dev, count_reduce=count_reduce, note=note,
                              fracs=fracs, col_counts=col_counts)
     groups = None
-    if mode == "edges" and pc > 1:
-        groups = distributed.row_groups(pr, pc) if pr > 1 else [None]
+    if mode == "edges" and pc > 1:  # the row groups' sub-groups (none for a tile rebuilt alone: backend "none")
+        groups = distributed.row_groups(pr, pc) if pr > 1 and backend != "none" else [None] * pr
     agg = Aggregate(shard, mode, pc, world, args.blocks, args.impl, groups, backend, rank)
     return shard, agg, mode, pr, pc, chunks
 
@@ -278,7 +278,7 @@ def _split(rows, per_step=1):
     from ordered counter rows: a step's launch pairs (one per non-empty row chunk of the tile) summed."""
     copy, gather, pairs, cur = [], [], [], None
     for _, name, v in rows:
-        if "k_agg_h32" in name or "k_agg_seg" in name or "k_agg_xl" in name:
+        if "k_agg_h32" in name or "k_agg_seg" in name:
             cur = [v, 0.0]
         elif "k_seg_reduce" in name and cur is not None:
             cur[1] = v
@@ -531,7 +531,7 @@ def main():
                     help="CPU work per thread count of the cpu_baseline leg (seconds, approx.)")
     ap.add_argument("--no-pmc", action="store_true", help="skip the rocprofv3 --pmc traffic passes")
     ap.add_argument("--pmc-dir", default="", help="keep the --pmc CSVs here (default: a temp dir)")
-    ap.add_argument("--knobs", default="", help="libgta tuning knobs for every launch, e.g. seg_xcd=2,seg_nt=3 "
+    ap.add_argument("--knobs", default="", help="libgta tuning knobs for every launch, e.g. seg_lean=0,mm_ring=0 "
                                                "(also passed to the PMC children)")
     ap.add_argument("--pmc-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--pmc-meta", default="", help=argparse.SUPPRESS)

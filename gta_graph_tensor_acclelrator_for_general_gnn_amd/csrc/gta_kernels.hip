@@ -845,136 +845,6 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
   }
 }
 
-// XCD line split of k_agg_h32 (F = 128; knob seg_xcd = NL = 2 or 4 line groups).  The chip's
-// 8 XCDs each have a private 4 MiB L2, and the dispatcher deals blocks round-robin over them, so
-// blocks b and b + 8 share one (MI355X_MICROARCH.md §Workgroup dispatch: a speed hint, never a
-// correctness one).  Here block b's label x = b % 8 picks a feature LINE L = x % NL (the
-// 512 / NL bytes [L * 512/NL, +512/NL) of every X row) and a PART x / NL of the items; every item
-// is run NL times, once per line, by blocks of NL different labels.  An XCD then gathers only its
-// line of the rows of the current column block: its L2 footprint is 1/NL of the full-row
-// form's, so the same column block stays L2-resident at NL x fewer blocks -- fewer items, fewer
-// partial rows -- or the same blocks hit L2 more often.  The indices and weights of an item are read
-// by the NL line groups at about the same time (each XCD reads its heads' weights), so the repeats
-// come from the Infinity Cache.  Per item-line: G = 32 / NL lanes x float4, 64 / G items per
-// wave; lane l of a group holds columns 4 (L G + l) .. +3, so its head, weight loads (two per
-// 8-edge step, DPP quad broadcast), fma chain and partial slots are k_agg_h32's for those
-// columns: partial rows bitwise equal to k_agg_h32's, and the same k_seg_reduce follows.
-template <int G>
-__device__ __forceinline__ int bcast8_16(int v, int k) {  // lane k of each G-lane group, G = 8 or 16
-  static_assert(G == 8 || G == 16, "group of 8 or 16 lanes");
-  switch (k) {
-#define GTA_BG(K_) case K_: return __builtin_amdgcn_ds_swizzle(v, (0x1F & ~(G - 1)) | (((K_) % G) << 5));
-    GTA_BG(0) GTA_BG(1) GTA_BG(2) GTA_BG(3) GTA_BG(4) GTA_BG(5) GTA_BG(6) GTA_BG(7)
-    GTA_BG(8) GTA_BG(9) GTA_BG(10) GTA_BG(11) GTA_BG(12) GTA_BG(13) GTA_BG(14) GTA_BG(15)
-#undef GTA_BG
-  }
-  return v;
-}
-
-template <bool WEIGHTED, int NT, bool W1, int G>
-__global__ void __launch_bounds__(kBlock)
-k_agg_xl(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
-         uint32_t row_bytes, const float* __restrict__ w, int64_t ldw, float* __restrict__ slabs,
-         const SegItem* __restrict__ items) {
-  constexpr int F = 128, U = 8, NL = 32 / G, P = 8 / NL, IW = kWave / G;
-  static_assert(G == 8 || G == 16, "line groups of 8 or 16 lanes");
-  const int lane = threadIdx.x & (kWave - 1);
-  const int lg = lane & (G - 1);
-  const int xl = static_cast<int>(blockIdx.x & 7);             // the blocks sharing an XCD
-  const int L = xl % NL, part = xl / NL;
-  const int64_t slot = blockIdx.x >> 3;
-  const int64_t k = ((slot * P + part) * kWavesPerBlock + wave_id_uniform()) * IW + lane / G;
-  const int64_t n_items = *n_items_p;
-  SegItem it{0, 0, 0};
-  if (k < n_items) it = items[k];
-  const int len = it.len;
-  int mx = len, mn = len;
-#pragma unroll
-  for (int off = G; off < kWave; off <<= 1) {
-    mx = max(mx, __shfl_xor(mx, off));
-    mn = min(mn, __shfl_xor(mn, off));
-  }
-  const int maxlen = __builtin_amdgcn_readfirstlane(mx);
-  const int minlen = __builtin_amdgcn_readfirstlane(mn);
-  if (maxlen == 0) return;
-  const int cl = L * G + lg;                                    // this lane's float4 of the row
-  const uint32_t colb = static_cast<uint32_t>(cl) * 16u;
-  const char* xb = reinterpret_cast<const char*>(x);
-  const int h = cl >> 2, q = cl & 3;
-  const int ldw32 = static_cast<int>(ldw);
-  const int32_t* ic = indices + it.beg;
-  const float* wc = WEIGHTED ? w + it.beg * ldw + (W1 ? 0 : h) : nullptr;
-  float acc[4] = {0.f, 0.f, 0.f, 0.f};
-  auto ldi = [&](const int32_t* p) { return (NT & 1) ? __builtin_nontemporal_load(p) : *p; };
-  auto ldw_ = [&](const float* p) { return (NT & 4) ? __builtin_nontemporal_load(p) : *p; };
-  auto row = [&](int src) -> float4 {
-    return *reinterpret_cast<const float4*>(xb + (__umul24(static_cast<uint32_t>(src), row_bytes) + colb));
-  };
-  int idxv = (lg < len) ? ldi(ic + lg) : 0;
-  float wv = (W1 && lg < len) ? ldw_(wc + lg * ldw32) : 0.f;
-  for (int c = 0; c < maxlen; c += G) {
-    const int idxn = (c + G + lg < len) ? ldi(ic + G + lg) : 0;
-    const float wvn = (W1 && c + G + lg < len) ? ldw_(wc + (G + lg) * ldw32) : 0.f;
-#pragma unroll
-    for (int s = 0; s < G; s += U) {
-      if (c + s >= maxlen) break;
-      float4 xv[U];
-      float wu[U];
-      if (c + s + U <= minlen) {  // full step for every item of the wave: no masks
-#pragma unroll
-        for (int u = 0; u < U; ++u) xv[u] = row(bcast8_16<G>(idxv, s + u));
-        if (WEIGHTED && W1) {
-#pragma unroll
-          for (int u = 0; u < U; ++u) wu[u] = __int_as_float(bcast8_16<G>(__float_as_int(wv), s + u));
-        } else if (WEIGHTED) {
-          const float* wp = wc + (s + 2 * q) * ldw32;
-          const float w0 = ldw_(wp), w1 = ldw_(wp + ldw32);
-          wu[0] = quad_bcast<0>(w0); wu[1] = quad_bcast<0>(w1);
-          wu[2] = quad_bcast<1>(w0); wu[3] = quad_bcast<1>(w1);
-          wu[4] = quad_bcast<2>(w0); wu[5] = quad_bcast<2>(w1);
-          wu[6] = quad_bcast<3>(w0); wu[7] = quad_bcast<3>(w1);
-        }
-      } else {
-        const int rem = len - c - s;
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const int src = bcast8_16<G>(idxv, s + u);
-          if (u < rem) {
-            xv[u] = row(src);
-            if (WEIGHTED) wu[u] = W1 ? __int_as_float(bcast8_16<G>(__float_as_int(wv), s + u)) : ldw_(wc + (s + u) * ldw32);
-          } else {
-            xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (WEIGHTED) wu[u] = 0.f;
-          }
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if (WEIGHTED) {
-          acc[0] = fmaf(wu[u], xv[u].x, acc[0]);
-          acc[1] = fmaf(wu[u], xv[u].y, acc[1]);
-          acc[2] = fmaf(wu[u], xv[u].z, acc[2]);
-          acc[3] = fmaf(wu[u], xv[u].w, acc[3]);
-        } else {
-          acc[0] += xv[u].x; acc[1] += xv[u].y; acc[2] += xv[u].z; acc[3] += xv[u].w;
-        }
-      }
-    }
-    idxv = idxn;
-    if (W1) wv = wvn;
-    ic += G;
-    if (WEIGHTED) wc += static_cast<int64_t>(G) * ldw;
-  }
-  if (len > 0) {
-    float* o = slabs + k * F + cl * 4;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (NT & 2) __builtin_nontemporal_store(acc[t], o + t);
-      else o[t] = acc[t];
-    }
-  }
-}
-
 // Lean half-wave form of the fused GAT attention item (k_agg_seg4<4, 8, ATT, SFC = exp-leaky-
 // relu, G = 32>) for F = 128, 8 heads: the weighted k_agg_h32 loop with the edge weight computed,
 // v = exp(leaky_relu(a[row, h] + b[src, h])), instead of loaded.  Per full 8-edge step lane
@@ -1916,7 +1786,6 @@ k_edge_softmax_v(const int64_t* __restrict__ indptr, const int32_t* __restrict__
 //   A[i = l&15][k = l>>4], B[k = l>>4][j = l&15]; D col = l&15, row = 4*(l>>4)+r.
 // ---------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // SF epilogue of the MFMA GEMMs applied to the whole accumulator tile in place, the switch on sf
 // OUTSIDE the element loops.  With sf_apply per element each of the FR x NT x 4 store sites held
@@ -1931,21 +1800,6 @@ __device__ __forceinline__ void sf_tile(int sf, f32x4 (&acc)[FR][NT]) {
     _Pragma("unroll") for (int i = 0; i < FR; ++i)                                    \
       _Pragma("unroll") for (int c = 0; c < NT; ++c)                                  \
         _Pragma("unroll") for (int r = 0; r < 4; ++r) acc[i][c][r] = sf_apply(K_, acc[i][c][r]); \
-    return;
-    GTA_SFT(GTA_SF_RELU) GTA_SFT(GTA_SF_EXP_LEAKY_RELU) GTA_SFT(GTA_SF_ELU) GTA_SFT(GTA_SF_EXP)
-    GTA_SFT(GTA_SF_LEAKY_RELU) GTA_SFT(GTA_SF_SIGMOID) GTA_SFT(GTA_SF_TANH) GTA_SFT(GTA_SF_RECIP)
-#undef GTA_SFT
-    default: return;  // GTA_SF_NONE
-  }
-}
-
-template <int T>
-__device__ __forceinline__ void sf_tile16(int sf, f32x16 (&acc)[T]) {
-  switch (sf) {
-#define GTA_SFT(K_)                                                                  \
-  case K_:                                                                           \
-    _Pragma("unroll") for (int t = 0; t < T; ++t)                                     \
-      _Pragma("unroll") for (int r = 0; r < 16; ++r) acc[t][r] = sf_apply(K_, acc[t][r]); \
     return;
     GTA_SFT(GTA_SF_RELU) GTA_SFT(GTA_SF_EXP_LEAKY_RELU) GTA_SFT(GTA_SF_ELU) GTA_SFT(GTA_SF_EXP)
     GTA_SFT(GTA_SF_LEAKY_RELU) GTA_SFT(GTA_SF_SIGMOID) GTA_SFT(GTA_SF_TANH) GTA_SFT(GTA_SF_RECIP)
@@ -2407,15 +2261,7 @@ constexpr int ring_blocks(int NT, int D, int FR) {
   return (160 / (D * (4 * FR + NT))) > 4 ? 4 : (160 / (D * (4 * FR + NT)));
 }
 
-// M32 (FR = 2): the same ring and stage image, consumed by v_mfma_f32_32x32x2_f32 instead --
-// each wave's 32 rows x 16*NT columns as NT/2 tiles of 32 x 32, half the MFMA instructions per
-// stage (FR*NT*4 16x16x4 -> NT/2 * 8 32x32x2; the same MFMA cycles) with the same fragment reads.
-// Lane (h = l >> 5, r = l & 31) reads logical k pieces h and 2 + h of its row; instruction
-// (jj, m) takes k = 8m + jj (lane half 0) then 8m + 4 + jj (half 1), so each output sums k in
-// k_mm_rows' order (0, 4, 8, 12, 1, 5, ...): bitwise equal to the 16x16x4 form.  The DMA swizzle
-// becomes piece ^ ((row >> 2) & 3), which keeps these reads conflict-free (each ds_read_b128
-// 16-lane group reads one piece of 16 distinct fragment rows).
-template <int NT, int D = 3, int FR = 2, bool M32 = false>
+template <int NT, int D = 3, int FR = 2>
 __global__ void __launch_bounds__(kBlock, ring_blocks(NT, D, FR))
 k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row_idx, int64_t M, int K,
           const float* __restrict__ wt, int64_t ldwt, int N, int sf, float* __restrict__ out, int64_t ldo,
@@ -2423,7 +2269,6 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   static_assert(NT == 4 || NT == 8, "B fragments split evenly over the 4 waves");
   static_assert(FR == 1 || FR == 2, "one or two A fragments per wave");
   static_assert(D >= 3 && D <= 8, "ring depth");
-  static_assert(!M32 || FR == 2, "32x32 tiles: 32 rows per wave");
   if (kslice > 0) {
     const int k0 = static_cast<int>(blockIdx.y) * kslice;
     x += k0;
@@ -2460,20 +2305,10 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   // piece: 16 rows per 16 consecutive lanes), bitwise equal and 1-4 % faster on every shape
   // measured (profiles/r03/mm_dma_rows_ab.log).
   const int rr = lane >> 2;
-  const int cdma = M32 ? ((lane & 3) ^ ((rr >> 2) & 3))         // logical 16-B k piece this lane DMAs
-                       : ((lane & 3) ^ ((rr >> 2) & 2));
+  const int cdma = (lane & 3) ^ ((rr >> 2) & 2);  // logical 16-B k piece this lane DMAs
   const uint32_t rdoff = static_cast<uint32_t>(r16 * 64 + ((g ^ ((r16 >> 2) & 2)) * 16));
   const bool dead = ring_tail && (S - 1) * KS + 4 * cdma >= K;  // this lane's DMA piece of the last stage
   const bool dead_rd = ring_tail && (S - 1) * KS + 4 * g >= K;  // the piece this lane reads
-  // M32 reads: lane (h, r32) reads row r32 & 15 of fragment r32 >> 4, logical pieces h and 2 + h
-  const int h32 = lane >> 5, r32 = lane & 31, f32r = r32 >> 4, q32 = (r32 & 15) >> 2;
-  uint32_t rd32[2];
-  bool dead32[2];
-#pragma unroll
-  for (int m = 0; m < 2; ++m) {
-    rd32[m] = static_cast<uint32_t>(f32r * 1024 + (r32 & 15) * 64 + (((2 * m + h32) ^ q32) * 16));
-    dead32[m] = ring_tail && (S - 1) * KS + 4 * (2 * m + h32) >= K;
-  }
   const int64_t T = my_groups * S;
   const float* bsrc[NT / 4];
 #pragma unroll
@@ -2516,21 +2351,12 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
       __builtin_amdgcn_global_load_lds(const_cast<float*>(bsrc[q] + ko),  // (a const source fails the host pass)
                                        GTA_TO_LDS(base + A_BYTES + (wv * (NT / 4) + q) * 1024), 16, 0, 0);
   };
-  constexpr int T32 = NT / 2;  // M32: 32-column tiles per wave
-  f32x4 acc[M32 ? 1 : FR][M32 ? 1 : NT];
-  f32x16 acc32[M32 ? T32 : 1];
+  f32x4 acc[FR][NT];
   auto zero_acc = [&]() __attribute__((always_inline)) {
-    if constexpr (M32) {
 #pragma unroll
-      for (int t = 0; t < T32; ++t)
+    for (int i = 0; i < FR; ++i)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc32[t][r] = 0.f;
-    } else {
-#pragma unroll
-      for (int i = 0; i < FR; ++i)
-#pragma unroll
-        for (int c = 0; c < NT; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+      for (int c = 0; c < NT; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
   auto mma = [&](const float (&av)[FR][4], const float4& b4, int c) {
     const float bj[4] = {b4.x, b4.y, b4.z, b4.w};
@@ -2542,52 +2368,6 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   const bool vstore = ldo % 4 == 0 && aligned(out, 16);
   auto epilogue = [&](int64_t j) __attribute__((always_inline)) {
     const int64_t mw = (grp0 + j * gstep) * GR + wv * (16 * FR);
-    if constexpr (M32) {
-      // 32x32 C map: lane (h, c) holds column c, rows (reg & 3) + 8 (reg >> 2) + 4 h
-      sf_tile16(sf, acc32);
-      const int p = r32 & 3, q = r32 >> 2;
-#pragma unroll
-      for (int t = 0; t < T32; ++t)
-#pragma unroll
-        for (int s4 = 0; s4 < 4; ++s4) {
-          if (vstore) {  // the same quad transpose: lane p then holds row 8 s4 + 4 h + p, columns 4q .. 4q + 3
-            float v[4];
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = acc32[t][4 * s4 + r];
-#pragma unroll
-            for (int m2 = 0; m2 < 2; ++m2) {
-              const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
-              const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2 + 1]), 0xB1, 0xF, 0xF, false));
-              if (p & 1) v[2 * m2] = sb; else v[2 * m2 + 1] = sa;
-            }
-#pragma unroll
-            for (int m2 = 0; m2 < 2; ++m2) {
-              const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2]), 0x4E, 0xF, 0xF, false));
-              const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2 + 2]), 0x4E, 0xF, 0xF, false));
-              if (p & 2) v[m2] = sb; else v[m2 + 2] = sa;
-            }
-            const int64_t m = mw + 8 * s4 + 4 * h32 + p;
-            const int n = n0 + 32 * t + 4 * q;
-            if (m < M) {
-              if (n + 3 < N) {
-                *reinterpret_cast<float4*>(out + m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
-              } else {
-#pragma unroll
-                for (int r = 0; r < 4; ++r)
-                  if (n + r < N) out[m * ldo + n + r] = v[r];
-              }
-            }
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) {
-              const int64_t m = mw + 8 * s4 + 4 * h32 + r;
-              const int n = n0 + 32 * t + r32;
-              if (m < M && n < N) out[m * ldo + n] = acc32[t][4 * s4 + r];
-            }
-          }
-        }
-      return;
-    }
     sf_tile(sf, acc);
     if (vstore) {  // quad-transposed 16-B row stores (k_mm_rows' epilogue)
       const int p = r16 & 3, q = r16 >> 2;
@@ -2635,31 +2415,6 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
           }
     }
   };
-  auto tail32 = [&](int64_t j) __attribute__((always_inline)) {  // M32's K tail: k = kt + 4 (2m + h) + jj < K
-    for (int kt = S * KS; kt < K; kt += 16) {
-      float av[2][4], bv[T32][2][4];
-      const float* ar = a_row(j, f32r, r32 & 15);
-#pragma unroll
-      for (int m = 0; m < 2; ++m)
-#pragma unroll
-        for (int jj = 0; jj < 4; ++jj) {
-          const int k = kt + 4 * (2 * m + h32) + jj;
-          av[m][jj] = k < K ? ar[k] : 0.f;
-#pragma unroll
-          for (int t = 0; t < T32; ++t) {
-            const int n = min(n0 + 32 * t + r32, N - 1);
-            bv[t][m][jj] = k < K ? wt[static_cast<int64_t>(n) * ldwt + k] : 0.f;
-          }
-        }
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-          for (int t = 0; t < T32; ++t)
-            acc32[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[m][jj], bv[t][m][jj], acc32[t], 0, 0, 0);
-    }
-  };
   auto tail = [&](int64_t j) __attribute__((always_inline)) {  // the K tail from registers, 16 k per step:
     for (int kt = S * KS; kt < K; kt += 16) {                     // k = kt + 4g + jj < K, zeros past it
       const int k0 = kt + 4 * g;
@@ -2703,41 +2458,6 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
     // fragment reads in inline asm: hipcc cannot tell them apart from the DMA in flight into
     // another slot and would wait vmcnt(0) before a plain LDS read (draining the ring every step).
     // The asm wait names every loaded register, so no MFMA is scheduled above it.
-    if constexpr (M32) {
-      const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * 1024);
-      const uint32_t sb = GTA_LDS_ADDR(lds + slot * STAGE + A_BYTES);
-      f32x4 a4[2], b4[T32][2];
-#pragma unroll
-      for (int m = 0; m < 2; ++m) ds_read16<0>(a4[m], sa + rd32[m]);
-#pragma unroll
-      for (int t = 0; t < T32; ++t)
-#pragma unroll
-        for (int m = 0; m < 2; ++m) ds_read16_idx(b4[t][m], sb + rd32[m], 2 * t);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-      for (int m = 0; m < 2; ++m) asm volatile("" : "+v"(a4[m]));
-#pragma unroll
-      for (int t = 0; t < T32; ++t)
-#pragma unroll
-        for (int m = 0; m < 2; ++m) asm volatile("" : "+v"(b4[t][m]));
-      if (ring_tail && s == S - 1) {  // pieces past K: zeros
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-          if (dead32[m]) {
-            a4[m] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-            for (int t = 0; t < T32; ++t) b4[t][m] = f32x4{0.f, 0.f, 0.f, 0.f};
-          }
-      }
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-#pragma unroll
-        for (int m = 0; m < 2; ++m)
-#pragma unroll
-          for (int t = 0; t < T32; ++t)
-            acc32[t] = __builtin_amdgcn_mfma_f32_32x32x2f32(a4[m][jj], b4[t][m][jj], acc32[t], 0, 0, 0);
-      continue;
-    }
     const uint32_t sa = GTA_LDS_ADDR(lds + slot * STAGE + (wv * FR) * 1024) + rdoff;
     const uint32_t sb = GTA_LDS_ADDR(lds + slot * STAGE + A_BYTES) + rdoff;
     f32x4 a4[FR], b4[NT];
@@ -2767,9 +2487,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
           acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a4[i][jj], b4[c][jj], acc[i][c], 0, 0, 0);
   }
   // the group's last stage is done: its K tail, its rows out, the next group's sums
-  if (!ring_tail && (K % KS)) {
-    if constexpr (M32) tail32(j); else tail(j);
-  }
+  if (!ring_tail && (K % KS)) tail(j);
   epilogue(j);
   zero_acc();
   // the counted waits above assume only ring DMA is outstanding; stores may retire out of order
@@ -3169,7 +2887,6 @@ struct Tuning {
   int agg_lean = 1;        // k_agg_lean for F = 64*VW SpMM shapes (0: k_aggregate, the form of other shapes)
   int seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
   int seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
-  int seg_xcd = 1;         // k_agg_xl line groups (2 or 4: each XCD gathers 1/NL of every row; 1 = k_agg_h32)
   int seg_phase = 0;       // blocked aggregate: 0 = items + reduce, 1 = items only, 2 = reduce only (bench timing)
   int att_lean = 1;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads (0: the generic half-wave form)
   int att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
@@ -3179,7 +2896,6 @@ struct Tuning {
   int mm_ring = 1;         // fp32 UPDATE on k_mm_ring (LDS-DMA ring) instead of k_mm_rows
   int mm_ring_fr = 0;      // k_mm_ring A fragments per wave: 2 = 128-row groups, 1 = 64-row groups, 0 = auto
   int mm_ring_depth = 0;   // k_mm_ring stages: 0 = auto (by blocks per CU), else 3, 4 or 8
-  int mm_ring_m32 = 0;     // k_mm_ring 128-row groups on v_mfma_f32_32x32x2_f32 (the M32 form)
   int mm_prefetch = 1;     // k_mm_rows A prefetch: 1 auto, 2 always, 0 never
   int64_t mm_split = -1;   // UPDATE K slices: -1 auto, 0 = never split, n = n slices
 };
@@ -3228,7 +2944,6 @@ const Knob* find_knob(const char* key) {
       {"agg_vw", &Tuning::force_vw, nullptr},
       {"agg_lean", &Tuning::agg_lean, nullptr},
       {"seg_lean", &Tuning::seg_lean, nullptr},
-      {"seg_xcd", &Tuning::seg_xcd, nullptr},
       {"seg_lean_w1", &Tuning::seg_lean_w1, nullptr},
       {"seg_phase", &Tuning::seg_phase, nullptr},
       {"att_lean", &Tuning::att_lean, nullptr},
@@ -3239,7 +2954,6 @@ const Knob* find_knob(const char* key) {
       {"mm_ring", &Tuning::mm_ring, nullptr},
       {"mm_ring_fr", &Tuning::mm_ring_fr, nullptr},
       {"mm_ring_depth", &Tuning::mm_ring_depth, nullptr},
-      {"mm_ring_m32", &Tuning::mm_ring_m32, nullptr},
       {"mm_prefetch", &Tuning::mm_prefetch, nullptr},
       {"mm_split", nullptr, &Tuning::mm_split},
   };
@@ -3587,15 +3301,7 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     const uint32_t rb = static_cast<uint32_t>(ldx * 4);
     // NT template bits: 1 = non-temporal index loads, 2 = non-temporal slab stores (measured -0.5 % / -1 %;
     // non-temporal weight loads +3 %: profiles/r02_nt_bits_ab.json)
-    const int nl = tuning().seg_xcd;
-    if (lean && (nl == 2 || nl == 4)) {
-      // every item once per line group: 8 block labels x one 64-item slot each
-      const dim3 gx(static_cast<unsigned>(8 * ((items + 63) / 64)));
-#define GTA_XL(G_)                                                                                     if (w && heads == 1) k_agg_xl<true, 2, true, G_><<<gx, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);   else if (w) k_agg_xl<true, 3, false, G_><<<gx, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);         else k_agg_xl<false, 2, false, G_><<<gx, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its)
-      if (nl == 4) { GTA_XL(8); } else { GTA_XL(16); }
-#undef GTA_XL
-      GTA_LAUNCHED("k_agg_xl");
-    } else if (lean) {
+    if (lean) {
       if (w && heads == 1) k_agg_h32<true, 2, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
       else if (w) k_agg_h32<true, 3><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
       else k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
@@ -3990,19 +3696,6 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
       const int64_t per_cu = dk == 8 ? 1 : dk == 4 ? (nt == 8 && fr == 2 ? 2 : 3) : (nt == 8 ? (fr == 1 ? 4 : 3) : 4);
       D = dk;
       blocks = std::min(n_grp, std::max<int64_t>(1, 256 * per_cu / ncb)) * ncb;
-    }
-    if (fr == 2 && D == 3 && tuning().mm_ring_m32) {  // the same ring on 32x32x2 MFMAs (bitwise equal)
-      const dim3 gr(static_cast<unsigned>(blocks));
-      const float* xf = static_cast<const float*>(x);
-      const float* wf = static_cast<const float*>(wt);
-      if (nt == 8)
-        k_mm_ring<8, 3, 2, true><<<gr, dim3(kBlock), 0, S(stream)>>>(xf, ldx, row_idx, M, static_cast<int>(K), wf, ldwt,
-                                                                     static_cast<int>(N), sf, out, ldo, 0, 0);
-      else
-        k_mm_ring<4, 3, 2, true><<<gr, dim3(kBlock), 0, S(stream)>>>(xf, ldx, row_idx, M, static_cast<int>(K), wf, ldwt,
-                                                                     static_cast<int>(N), sf, out, ldo, 0, 0);
-      GTA_LAUNCHED("k_mm_ring<m32>");
-      return GTA_OK;
     }
     launch_ring(nt, D, fr, dim3(static_cast<unsigned>(blocks)), S(stream), static_cast<const float*>(x), ldx, row_idx, M,
                 static_cast<int>(K), static_cast<const float*>(wt), ldwt, static_cast<int>(N), sf, out, ldo, 0, 0);

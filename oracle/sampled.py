@@ -116,7 +116,8 @@ class SampledChecker:
             out[name] = np.flatnonzero(m)[:per_class]
         graph = getattr(self.ex, "graph", None)
         n_cols = getattr(graph, "n_cols", N)
-        blocks = sorted({k[1] for k in getattr(graph, "_plans", {}) if isinstance(k, tuple) and k[0] == "blocked"})
+        blocks = sorted({k[1] for k in getattr(graph, "_plans", {})
+                         if isinstance(k, tuple) and k[0] == "blocked" and k[1] > 1})
         for B in blocks:
             bsize = -(-n_cols // B)
             rows = []

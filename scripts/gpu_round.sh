@@ -47,6 +47,15 @@ for s in $STEPS; do
     pmcsq)
       timeout -k 10 ${T_PMCSQ:-420} python scripts/pmc_sq.py gpurun_out/pmc_sq > gpurun_out/pmc_sq.log 2>&1
       rc=$?; echo "pmcsq rc=$rc"; tail -3 gpurun_out/pmc_sq.log; stop_if_fatal $rc pmcsq ;;
+    metricab)
+      timeout -k 10 ${T_AB:-400} python -u scripts/metric_ab.py ${AB_ARGS:-20 16} > gpurun_out/metric_ab.log 2>&1
+      rc=$?; echo "metricab rc=$rc"; grep '^{' gpurun_out/metric_ab.log; stop_if_fatal $rc metricab ;;
+    tile)
+      timeout -k 10 ${T_TILE:-400} python -u scripts/tile_chunks.py ${TILE_ARGS} > gpurun_out/tile_chunks.log 2>&1
+      rc=$?; echo "tile rc=$rc"; grep '^{' gpurun_out/tile_chunks.log; stop_if_fatal $rc tile ;;
+    xcd)
+      timeout -k 10 60 ./scripts/xcd_probe > gpurun_out/xcd_probe.log 2>&1
+      rc=$?; echo "xcd rc=$rc"; cat gpurun_out/xcd_probe.log; stop_if_fatal $rc xcd ;;
     *) echo "unknown step $s";;
   esac
 done

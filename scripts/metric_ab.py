@@ -7,7 +7,7 @@ checks each variant's output bitwise against the first variant's at the same blo
 Prints one JSON line per variant (median over rounds).
 
 Usage: python scripts/metric_ab.py [--rounds R] [--reps K] VARIANT ...
-  VARIANT = B[:knob=v[,knob=v...]], e.g.  20  20:seg_xcd=4  8:seg_xcd=4
+  VARIANT = B[:knob=v[,knob=v...]], e.g.  20  16  20:seg_lean=0
 """
 import json
 import os
@@ -48,7 +48,7 @@ def main():
         i = args.index("--reps")
         reps = int(args[i + 1])
         del args[i:i + 2]
-    variants = [parse(v) for v in (args or ["20", "20:seg_xcd=4"])]
+    variants = [parse(v) for v in (args or ["20", "20:seg_lean=0"])]
     dev = torch.device("cuda", 0)
     sh = metric.Shard(metric.N_REDDIT, metric.E_REDDIT, 0, 1, 1, 1, dev, keep_rows=False)
     g, x, a = sh.graph, sh.x, sh.alpha
@@ -60,6 +60,7 @@ def main():
     for r in range(rounds):
         for i, (B, knobs) in enumerate(variants):
             y = outs.setdefault(i, torch.empty(g.n_rows, metric.F, device=dev))
+            old = {k: ops.get_debug(k) for k in knobs}
             try:
                 for k, v in knobs.items():
                     ops.set_debug(k, v)
@@ -78,8 +79,8 @@ def main():
                 ops.set_debug("seg_phase", 0)
             finally:
                 ops.set_debug("seg_phase", 0)
-                for k in knobs:
-                    ops.set_debug(k, 1 if k in ("seg_xcd", "seg_lean", "seg_lean_w1") else 0)
+                for k, v in old.items():
+                    ops.set_debug(k, v)
     for i, (B, knobs) in enumerate(variants):
         d = res[i]
         rec = {"blocks": B, "knobs": knobs, "n_items": g.blocked_plan(B).n_items,

@@ -18,7 +18,7 @@ GROUPS = {
                  "SQ_ACTIVE_INST_LDS", "SQ_INSTS_SMEM", "GRBM_GUI_ACTIVE"],
     "l2": ["TCC_HIT_sum", "TCC_MISS_sum", "TCP_TCC_READ_REQ_sum"],
 }
-KERNELS = ("k_agg_h32", "k_agg_xl", "k_seg_reduce")
+KERNELS = ("k_agg_h32", "k_seg_reduce")
 
 
 def summarize(d):
@@ -39,7 +39,7 @@ def summarize(d):
     return out
 
 
-EXTRA = []  # bench.py arguments after OUT_DIR (e.g. --blocks 16 --knobs seg_xcd=2)
+EXTRA = []  # bench.py arguments after OUT_DIR (e.g. --blocks 16 --knobs seg_lean=0)
 
 
 def main(out_dir):

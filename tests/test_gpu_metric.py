@@ -57,19 +57,3 @@ def test_metric_single_pass_full_reddit_vs_oracle(shard):
     torch.cuda.synchronize()
     _check(shard, y, k=128)
 
-
-@pytest.mark.parametrize("nl,blocks", [(4, 8), (4, 20), (2, 12)])
-def test_metric_xcd_line_split_full_reddit(shard, nl, blocks):
-    """The XCD line-split item kernel (k_agg_xl, knob seg_xcd = 2 / 4 line groups) at full size:
-    bitwise equal to k_agg_h32 at the same block count (same partial rows, same ordered reduce),
-    and within the oracle bound."""
-    g = shard.graph
-    y0 = ops.aggregate_blocked(g, shard.x, shard.alpha, blocks=blocks)
-    try:
-        ops.set_debug("seg_xcd", nl)
-        y = ops.aggregate_blocked(g, shard.x, shard.alpha, blocks=blocks)
-    finally:
-        ops.set_debug("seg_xcd", 1)
-    torch.cuda.synchronize()
-    assert torch.equal(y, y0)
-    _check(shard, y, k=128)

@@ -388,12 +388,11 @@ def test_edge_softmax_other_sf_and_errors(dev):
         ops.edge_softmax(g, a, b[:, :4].contiguous())
 
 
-@pytest.mark.parametrize("knobs", [{"seg_lean": 0}, {"seg_lean_w1": 0}, {"seg_xcd": 2}, {"seg_xcd": 4}])
+@pytest.mark.parametrize("knobs", [{"seg_lean": 0}, {"seg_lean_w1": 0}])
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 0), (64, 4), (256, 16), (128, 1)])
 def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
     """The lean half-wave kernels (k_agg_h32, also with one weight per edge) == the generic
-    half-wave form bitwise (same per-item edge order and fma chain), and == the fp64 oracle; so do
-    the XCD line-split forms (k_agg_xl: 2 or 4 line groups, each item run once per line)."""
+    half-wave form bitwise (same per-item edge order and fma chain), and == the fp64 oracle."""
     n, e = 900, 30000
     g = G.synthetic(n, e, seed=F + heads, device=dev)
     ip, ix = g.numpy()
@@ -699,18 +698,16 @@ def test_update_mm_ring_bitwise(dev, M, K, N, gathered, sf):
     old_min = ops.MM_ROWS_MIN_M
     try:
         ops.MM_ROWS_MIN_M = 0
-        # k_mm_rows, then the ring with 128-row groups, 64-row groups, the automatic choice, and
-        # 128-row groups on 32x32x2 MFMAs (the M32 form: K tails in registers (602, 1433) and as a
-        # ring stage (600, 604), 32-column tiles past N (66, 100, 200), non-vector stores (N = 66))
-        for ring, fr, m32 in ((0, 0, 0), (1, 2, 0), (1, 1, 0), (1, 0, 0), (1, 2, 1)):
+        # k_mm_rows, then the ring with 128-row groups, 64-row groups, and the automatic choice
+        # (K tails in registers (602, 1433) and as a ring stage (600, 604), N past the last 16-column
+        # fragment (66, 100, 200), non-vector stores (N = 66))
+        for ring, fr in ((0, 0), (1, 2), (1, 1), (1, 0)):
             ops.set_debug("mm_ring", ring)
             ops.set_debug("mm_ring_fr", fr)
-            ops.set_debug("mm_ring_m32", m32)
             outs.append(ops.update_mm(xd, wd, idd, sf=sf, m=None if gathered else M))
     finally:
         ops.set_debug("mm_ring", 1)
         ops.set_debug("mm_ring_fr", 0)
-        ops.set_debug("mm_ring_m32", 0)
         ops.MM_ROWS_MIN_M = old_min
     torch.cuda.synchronize()
     for o in outs[1:]:

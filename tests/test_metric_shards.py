@@ -225,3 +225,32 @@ def test_column_counts_rebuild_a_tile_alone(pr, pc):
         assert (a.grid.c0, a.grid.c1) == (b.grid.c0, b.grid.c1)
         assert torch.equal(a.graph.indptr, b.graph.indptr) and torch.equal(a.graph.indices, b.graph.indices)
         assert torch.equal(a.alpha, b.alpha) and torch.equal(a.x, b.x)
+
+
+@pytest.mark.parametrize("world,mode", [(8, "edges"), (4, "edges"), (2, "edges"), (4, "rows")])
+def test_bench_builds_a_tile_alone_without_a_process_group(monkeypatch, world, mode):
+    """bench.py's PMC child (and scripts/tile_chunks.py) rebuild one rank's tile in a process with
+    no process group: bench.build with backend "none" and the whole-graph column histogram must not
+    touch torch.distributed (the 4 x 2 grid's row sub-groups included), and must give the tile the
+    distributed run builds."""
+    import types
+
+    import bench
+    monkeypatch.setattr(bench.ops.BlockedPlan, "auto_blocks", staticmethod(lambda g, f, elem=4: 1))
+    monkeypatch.setattr(bench.G.Graph, "plan", lambda self, chunk=512: None)
+    assert not dist.is_initialized()
+    args = types.SimpleNamespace(mode=mode, grid="auto", row_chunks=2, chunk_fracs="auto", n=N, e=E, blocks=0,
+                                 impl="plan")
+    cc = metric.column_counts(N, E, "cpu")
+    pr, pc = distributed.grid_shape(world, mode)
+    tot = 0
+    for r in range(world):
+        shard, agg, m, pr_, pc_, chunks = bench.build(args, world, r, torch.device("cpu"), "none", lambda s: None,
+                                                      col_counts=cc)
+        assert (pr_, pc_) == (pr, pc) and agg.group is None
+        ref = metric.Shard(N, E, r, pr, pc, 2, "cpu", count_reduce=(_global_counts(pr, pc) if pc > 1 else None),
+                           fracs=(0.7, 0.3) if (mode == "edges" and pc > 1) else None)
+        if mode == "edges":
+            assert torch.equal(shard.graph.indices, ref.graph.indices) and torch.equal(shard.alpha, ref.alpha)
+        tot += shard.graph.nnz
+    assert tot == E
