@@ -10,7 +10,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgta.so")
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 # enum mirrors of include/gta.h
 GTA_F32, GTA_BF16, GTA_F32_BF16 = 0, 1, 2
@@ -50,6 +50,8 @@ SIGNATURES = {
     "gta_update_mm": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
     "gta_update_mm_t": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
     "gta_update_mm_t_splits": (_i64, [_i64, _i64, _i64, _i32, _vp]),
+    "gta_update_mlp": (_i32, [_vp, _i64, _i64, _i64, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _i32, _i32, _vp, _i64,
+                              _vp]),
     "gta_update_mm_t_split_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),
     "gta_update_mm_t_split": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _i64, _vp,
                                      _i64, _vp]),

@@ -2755,6 +2755,206 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   }
 }
 
+// Two chained node GEMMs in one pass (GIN's MLP, `vTCAD/GraphOP/genGraphOP.py:103-108`: applynode
+// MM -> SF -> MM -> SF, `template/ISA_defination.yaml:1-31` j,ij->i twice):
+//   out = sf2(bf16(sf1(x W1)) W2), x fp32 [M, K1 <= 128], W1 bf16 [K1, N1 <= 128], W2 bf16 [N1, N2 <= 128].
+// The unfused path writes z = sf1(x W1) as fp32 [M, N1] and the second GEMM reads it back, rounding
+// it to bf16 as it stages it (GTA_F32_BF16): 2 x M x N1 x 4 bytes of HBM traffic (2.5 GB for GIN
+// products) that this kernel never moves -- x is read once and out written once.
+// Per wave: 16-row groups, persistent.  x fragments go straight to registers (lane (g, r) loads
+// x[r][32s + 8g .. +7] as two float4s, the next group's loads in flight during this group's
+// MFMAs) and are rounded to bf16 (RNE) as k_mm_ring_bf rounds them; W1^T and W2^T stay resident in
+// LDS in k_mm_ring_bf's fragment layout (zero past K and N).  GEMM 1 is NT x ceil(K1/32)
+// v_mfma_f32_16x16x32_bf16 in k_mm_ring_bf's k order; its tile goes sf1 -> bf16 (RNE, as the
+// second GEMM's staging rounds the fp32 z) -> the wave's own 16 x 128 bf16 LDS image (quad-transposed
+// 8-B writes, 16-B pieces XOR-swizzled by row so the A-fragment reads are conflict-free) -> GEMM 2
+// (4 steps of 32 k, zero past N1).  Same operands, k order and rounding as the two unfused
+// launches: bitwise equal to them.  LDS 80 KiB: two blocks per CU.
+__global__ void __launch_bounds__(kBlock, 2)
+k_mlp_bf(const float* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint16_t* __restrict__ w1t,
+         int64_t ldw1, int N1, int sf1, const uint16_t* __restrict__ w2t, int64_t ldw2, int N2, int sf2,
+         float* __restrict__ out, int64_t ldo) {
+  constexpr int NT = 8, SB = 4;  // 128 columns, 128 k of resident W^T per GEMM
+  __shared__ __attribute__((aligned(16))) char wres[2 * NT * SB * 1024];
+  __shared__ __attribute__((aligned(16))) char zimg[kWavesPerBlock * 16 * 256];
+  const int lane = threadIdx.x & (kWave - 1);
+  const int wv = wave_id_uniform();
+  const int g = lane >> 4, r16 = lane & 15;
+  // W1^T, W2^T resident: fragment (w, c, s) at wres + ((w * NT + c) * SB + s) KiB: lane L's 8 bf16 of
+  // row 16c + (L & 15), k = 32s + 8(L >> 4); zeros past K (W1: K1, W2: N1) and N
+  for (int e = threadIdx.x; e < 2 * NT * SB * kWave; e += kBlock) {
+    const int L = e & (kWave - 1), f = e >> 6, w = f / (NT * SB), c = (f / SB) % NT, st = f % SB;
+    const int n = 16 * c + (L & 15), k = 32 * st + 8 * (L >> 4);
+    const uint16_t* wt = w ? w2t : w1t;
+    const int64_t ldw = w ? ldw2 : ldw1;
+    const int Kw = w ? N1 : K1, Nw = w ? N2 : N1;
+    uint16_t tmp[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) tmp[q] = (n < Nw && k + q < Kw) ? wt[static_cast<int64_t>(n) * ldw + k + q] : 0;
+    *reinterpret_cast<uint4*>(wres + f * 1024 + L * 16) = *reinterpret_cast<const uint4*>(tmp);
+  }
+  __syncthreads();
+  const int S1 = (K1 + 31) / 32;
+  const int64_t n_groups = (M + 15) / 16;
+  const int64_t gstep = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
+  int64_t grp = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wv;
+  const bool xvec = ldx % 4 == 0 && aligned(x, 16);
+  auto load_x = [&](int64_t gi, float4 (&xa)[SB][2]) __attribute__((always_inline)) {
+    const float* xr = x + min<int64_t>(gi * 16 + r16, M - 1) * ldx;
+#pragma unroll
+    for (int st = 0; st < SB; ++st)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int k = 32 * st + 8 * g + 4 * h;
+        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (st < S1) {
+          if (xvec && k + 4 <= K1) {
+            v = *reinterpret_cast<const float4*>(xr + k);
+          } else {
+            if (k < K1) v.x = xr[k];
+            if (k + 1 < K1) v.y = xr[k + 1];
+            if (k + 2 < K1) v.z = xr[k + 2];
+            if (k + 3 < K1) v.w = xr[k + 3];
+          }
+        }
+        xa[st][h] = v;
+      }
+  };
+  const uint32_t wbase = GTA_LDS_ADDR(wres) + static_cast<uint32_t>(lane) * 16u;
+  const uint32_t zw = GTA_LDS_ADDR(zimg) + static_cast<uint32_t>(wv) * 4096u;
+  const bool vstore = ldo % 4 == 0 && aligned(out, 16);
+  const int p = r16 & 3, qq = r16 >> 2;
+  float4 xa[SB][2];
+  if (grp < n_groups) load_x(grp, xa);
+  for (; grp < n_groups; grp += gstep) {
+    float4 xn[SB][2];
+    if (grp + gstep < n_groups) load_x(grp + gstep, xn);
+    f32x4 acc[1][NT];
+#pragma unroll
+    for (int c = 0; c < NT; ++c) acc[0][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    // GEMM 1: k_mm_ring_bf's step order, every step padded with zeros past K1
+#pragma unroll
+    for (int st = 0; st < SB; ++st) {
+      if (st >= S1) break;
+      bf16x8 a8;  // x rounded to bf16 (RNE) as k_mm_ring_bf rounds it
+      a8[0] = static_cast<short>(to_bf16_bits(xa[st][0].x));
+      a8[1] = static_cast<short>(to_bf16_bits(xa[st][0].y));
+      a8[2] = static_cast<short>(to_bf16_bits(xa[st][0].z));
+      a8[3] = static_cast<short>(to_bf16_bits(xa[st][0].w));
+      a8[4] = static_cast<short>(to_bf16_bits(xa[st][1].x));
+      a8[5] = static_cast<short>(to_bf16_bits(xa[st][1].y));
+      a8[6] = static_cast<short>(to_bf16_bits(xa[st][1].z));
+      a8[7] = static_cast<short>(to_bf16_bits(xa[st][1].w));
+      f32x4 b4[NT];
+#pragma unroll
+      for (int c = 0; c < NT; ++c) ds_read16_kib(b4[c], wbase, c * SB + st);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(b4[c]));
+#pragma unroll
+      for (int c = 0; c < NT; ++c)
+        acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, __builtin_bit_cast(bf16x8, b4[c]), acc[0][c], 0, 0, 0);
+    }
+    sf_tile(sf1, acc);
+    // z tile -> bf16 image [16 rows][128 k] of this wave: lane (g, 4qq + p) holds rows 4g + r, column
+    // 16c + 4qq + p; the quad transpose leaves row 4g + p, columns 16c + 4qq .. +3 (one 8-B write).
+    // 16-B piece P of row r sits at piece P ^ r (conflict-free A-fragment reads below)
+#pragma unroll
+    for (int c = 0; c < NT; ++c) {
+      float v[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) v[r] = acc[0][c][r];
+#pragma unroll
+      for (int m2 = 0; m2 < 2; ++m2) {
+        const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
+        const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2 + 1]), 0xB1, 0xF, 0xF, false));
+        if (p & 1) v[2 * m2] = sb; else v[2 * m2 + 1] = sa;
+      }
+#pragma unroll
+      for (int m2 = 0; m2 < 2; ++m2) {
+        const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2]), 0x4E, 0xF, 0xF, false));
+        const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2 + 2]), 0x4E, 0xF, 0xF, false));
+        if (p & 2) v[m2] = sb; else v[m2 + 2] = sa;
+      }
+      const int row = 4 * g + p, col = 16 * c + 4 * qq;  // columns past N1 are zero (K of GEMM 2)
+      uint32_t lo = 0, hi = 0;
+      if (col < N1) lo |= to_bf16_bits(v[0]);
+      if (col + 1 < N1) lo |= static_cast<uint32_t>(to_bf16_bits(v[1])) << 16;
+      if (col + 2 < N1) hi |= to_bf16_bits(v[2]);
+      if (col + 3 < N1) hi |= static_cast<uint32_t>(to_bf16_bits(v[3])) << 16;
+      const uint32_t a = zw + static_cast<uint32_t>(row * 256 + (((2 * c + (qq >> 1)) ^ row) * 16) + (qq & 1) * 8);
+      asm volatile("ds_write_b64 %0, %1" ::"v"(a), "v"(make_uint2(lo, hi)) : "memory");
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    // GEMM 2: A fragment (row r16, k = 32 s + 8 g .. +7) = logical piece 4 s + g of row r16
+#pragma unroll
+    for (int c = 0; c < NT; ++c) acc[0][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int st = 0; st < SB; ++st) {
+      f32x4 a4, b4[NT];
+      const uint32_t ra = zw + static_cast<uint32_t>(r16 * 256 + (((4 * st + g) ^ r16) * 16));
+      ds_read16<0>(a4, ra);
+#pragma unroll
+      for (int c = 0; c < NT; ++c) ds_read16_kib(b4[c], wbase, NT * SB + c * SB + st);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      asm volatile("" : "+v"(a4));
+#pragma unroll
+      for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(b4[c]));
+      const bf16x8 a8 = __builtin_bit_cast(bf16x8, a4);
+#pragma unroll
+      for (int c = 0; c < NT; ++c)
+        acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, __builtin_bit_cast(bf16x8, b4[c]), acc[0][c], 0, 0, 0);
+    }
+    sf_tile(sf2, acc);
+    const int64_t mw = grp * 16;
+    if (vstore) {
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[0][c][r];
+#pragma unroll
+        for (int m2 = 0; m2 < 2; ++m2) {
+          const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
+          const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2 + 1]), 0xB1, 0xF, 0xF, false));
+          if (p & 1) v[2 * m2] = sb; else v[2 * m2 + 1] = sa;
+        }
+#pragma unroll
+        for (int m2 = 0; m2 < 2; ++m2) {
+          const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2]), 0x4E, 0xF, 0xF, false));
+          const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2 + 2]), 0x4E, 0xF, 0xF, false));
+          if (p & 2) v[m2] = sb; else v[m2 + 2] = sa;
+        }
+        const int64_t m = mw + 4 * g + p;
+        const int n = 16 * c + 4 * qq;
+        if (m < M) {
+          if (n + 3 < N2) {
+            *reinterpret_cast<float4*>(out + m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < N2) out[m * ldo + n + r] = v[r];
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < NT; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t m = mw + 4 * g + r;
+          const int n = 16 * c + r16;
+          if (m < M && n < N2) out[m * ldo + n] = acc[0][c][r];
+        }
+    }
+#pragma unroll
+    for (int st = 0; st < SB; ++st) {
+      xa[st][0] = xn[st][0];
+      xa[st][1] = xn[st][1];
+    }
+  }
+}
+
 // out[m, n] = sf(sum_s ws[s][m][n]) in slice order (split-K UPDATE; ws slices are [M, N] dense).
 // Float4 form: four consecutive columns per thread, the slices' loads issued four at a time, the
 // adds in slice order (bitwise equal to the scalar form).
@@ -3751,6 +3951,25 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
 #undef GTA_MMR_NT
 #undef GTA_MMR
   GTA_LAUNCHED("k_mm_rows");
+  return GTA_OK;
+}
+
+int gta_update_mlp(const float* x, int64_t ldx, int64_t M, int64_t K1, const void* w1t, int64_t ldw1, int64_t N1,
+                   int sf1, const void* w2t, int64_t ldw2, int64_t N2, int sf2, int dtype, float* out, int64_t ldo,
+                   void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
+  if (M < 0 || K1 <= 0 || N1 <= 0 || N2 <= 0 || ldw1 < K1 || ldw2 < N1 || ldx < K1 || ldo < N2)
+    return fail(GTA_ERR_ARG, "update_mlp: bad sizes");
+  if (M == 0) return GTA_OK;
+  if (!x || !w1t || !w2t || !out) return fail(GTA_ERR_ARG, "update_mlp: bad arguments");
+  if (dtype != GTA_F32_BF16) return fail(GTA_ERR_UNSUPPORTED, "update_mlp: fp32 x with bf16 weights only");
+  if (K1 > 128 || N1 > 128 || N2 > 128) return fail(GTA_ERR_UNSUPPORTED, "update_mlp: K1, N1, N2 <= 128");
+  const int64_t n_groups = (M + 15) / 16;
+  const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n_groups + kWavesPerBlock - 1) / kWavesPerBlock, 512));
+  k_mlp_bf<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, S(stream)>>>(
+      x, ldx, M, static_cast<int>(K1), static_cast<const uint16_t*>(w1t), ldw1, static_cast<int>(N1), sf1,
+      static_cast<const uint16_t*>(w2t), ldw2, static_cast<int>(N2), sf2, out, ldo);
+  GTA_LAUNCHED("k_mlp_bf");
   return GTA_OK;
 }
 

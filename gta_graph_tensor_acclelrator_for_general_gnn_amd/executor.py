@@ -161,6 +161,8 @@ class Executor:
         #   fuse_sf: an SF whose producer feeds only it runs as the producer's post-op
         self.elide_scatter_stores = True
         self.fuse_sf = True
+        #   fuse_mlp: MM -> SF -> MM -> SF chains of node GEMMs (GIN's MLP) as one gta_update_mlp launch
+        self.fuse_mlp = FUSE_MLP
         # weighted/unweighted SpMM aggregates whose gathered table exceeds the chip's L2
         # run column-blocked (L2-resident slices) when the shape allows it
         self.blocked_min_table_bytes = 32 << 20
@@ -924,6 +926,10 @@ class Executor:
             c = fused_into.get(op.idx)
             if c is not None and self.g.ops[c].type == "gather" and op.comp in ("MUL", "MM"):
                 return Deferred(op.idx)
+        if self.fuse_mlp and op.type == "applynode" and op.comp == "MM":
+            v = self._eval_mlp(op)
+            if v is not None:
+                return v
         sf_child = self._sf_child(op, block)
         if sf_child is not None:
             ev = self._eval_applyedge if op.type == "applyedge" else self._eval_applynode
@@ -970,6 +976,45 @@ class Executor:
             return None
         self.values[c.idx] = y
         return Lazy(lambda: self._gather_value(op))
+
+    def _only_consumer(self, op, comp):
+        """op's single consumer when it is an applynode of kind comp reading only op, else None."""
+        cons = self.consumers[op.idx]
+        if len(cons) != 1:
+            return None
+        c = self.g.ops[cons[0]]
+        if c.type != "applynode" or c.comp != comp or len(self.g.inputs[c.idx]) != 1 or self._ext(c, 1) is not None:
+            return None
+        return c
+
+    def _eval_mlp(self, a):
+        """Two chained node GEMMs a -> [SF b] -> MM c -> [SF d] (GIN's MLP, genGraphOP.py:103-108),
+        each intermediate read only by the next op, as one gta_update_mlp launch when the shapes
+        allow it (fp32 x, bf16 weights, widths <= 128).  The chain's last value is set; a, b and c
+        stay available, recomputed unfused if something reads them (the tests read them all).
+        None when the chain or its operands do not fit."""
+        b = self._only_consumer(a, "SF") if self.fuse_sf else None
+        c = self._only_consumer(b if b is not None else a, "MM")
+        if c is None:
+            return None
+        d = self._only_consumer(c, "SF") if self.fuse_sf else None
+        ins = self._inputs(a)
+        if len(ins) != 1:
+            return None
+        x = self._node(ins[0])
+        w1, w2 = self.tensors[f"w:{a.idx}"], self.tensors[f"w:{c.idx}"]
+        if not ops.update_mlp_supported(x, w1, w2):
+            return None
+        sf1 = self.sem.sf_of(b) if b is not None else None
+        sf2 = self.sem.sf_of(d) if d is not None else None
+        out = ops.update_mlp(x, w1, w2, sf1=sf1, sf2=sf2)
+        self._count(x.shape[0] * (x.shape[1] * 4 + w2.shape[1] * 4) + w1.numel() * 2 + w2.numel() * 2)
+        self.values[(d if d is not None else c).idx] = NodeT(out)
+        if d is not None:
+            self.values[c.idx] = Lazy(lambda: self._eval_applynode(c))
+        if b is not None:
+            self.values[b.idx] = Lazy(lambda: self._eval_applynode(a, post_sf=sf1))
+        return Lazy(lambda: self._eval_applynode(a))
 
     def _sf_child(self, op, block):
         """The SF op this op's output feeds exclusively (same kind, same block), if fusable."""
@@ -1128,6 +1173,7 @@ def aggregate_trace(events):
 # also drops every captured graph).  A replay is keyed by the objects AND their storage (data_ptr,
 # shape, stride), the calling thread's libgta knob state (ops.knob_state) and stays eager on a stream with an attached
 # knob set; weights changed in place are re-transposed into the graph's W^T before the replay.
+FUSE_MLP = True  # default of Executor.fuse_mlp (layer benches A/B it)
 AUTO_GRAPH = True
 AUTO_GRAPH_MAX_EDGES = 1 << 23
 AUTO_GRAPH_MAX_ENTRIES = 32

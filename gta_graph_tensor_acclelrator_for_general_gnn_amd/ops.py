@@ -485,6 +485,34 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
     return out
 
 
+def update_mlp_supported(x, w1, w2):
+    """Shapes gta_update_mlp takes: fp32 x [M, K1] with unit column stride, bf16 W1 [K1, N1] and
+    W2 [N1, N2], K1, N1, N2 <= 128."""
+    return (x.dtype == torch.float32 and x.dim() == 2 and w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16
+            and w1.dim() == 2 and w2.dim() == 2 and x.shape[1] == w1.shape[0] and w1.shape[1] == w2.shape[0]
+            and max(w1.shape[0], w1.shape[1], w2.shape[1]) <= 128 and (x.shape[0] <= 1 or x.stride(1) == 1))
+
+
+def update_mlp(x, w1, w2, sf1=None, sf2=None, out=None):
+    """out = sf2(bf16(sf1(x W1)) W2) in one launch (gta_update_mlp: GIN's MM -> SF -> MM -> SF,
+    genGraphOP.py:103-108), bitwise equal to update_mm(update_mm(x, w1, sf=sf1), w2, sf=sf2) with
+    fp32 x and bf16 weights, without the [M, N1] intermediate in HBM."""
+    _need_gpu(x, w1, w2, out)
+    if not update_mlp_supported(x, w1, w2):
+        raise ValueError("update_mlp: fp32 x [M, K1], bf16 W1 [K1, N1], bf16 W2 [N1, N2], K1, N1, N2 <= 128")
+    M, K1 = x.shape
+    N1, N2 = w1.shape[1], w2.shape[1]
+    w1t, w2t = _transposed(w1), _transposed(w2)
+    if out is None:
+        out = torch.empty(M, N2, dtype=torch.float32, device=x.device)
+    if out.shape[0] < M or out.shape[1] != N2:
+        raise ValueError("update_mlp: out must be [M, N2]")
+    check(_L().gta_update_mlp(_ptr(x), _rows(x, "x"), M, K1, _ptr(w1t), _rows(w1t, "w1^T", torch.bfloat16), N1, _sf(sf1),
+                              _ptr(w2t), _rows(w2t, "w2^T", torch.bfloat16), N2, _sf(sf2), _lib.GTA_F32_BF16,
+                              _ptr(out), _rows(out, "out"), _stream(x.device)), "update_mlp")
+    return out
+
+
 MM_FORM = "rows"  # "rows": gta_update_mm_t (x read once per output); "tile": gta_update_mm 64x64 tiles
 MM_ROWS_MIN_M = 0  # smallest M for the row-streaming entry (k_mm_ring / k_mm_rows); below, the
                    # 64x64-tile kernel. With the ring the row form wins at every M measured: GCN Cora's

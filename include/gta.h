@@ -37,14 +37,15 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 8  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+#define GTA_ABI_VERSION 9  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
                               hooks; 4: knob sets attached to streams (gta_tuning_*); 5: every UPDATE
                               on hand-written kernels (no vendor library), gta_update_mm_t_splits,
                               the blocked workspace is the slab rows alone and required, bf16
                               rows in gta_aggregate (x_dtype) and gta_apply_node (a_dtype);
                               6: gta_gat_aggregate_blocked's sf_out (an SF applied to y); 7:
                               gta_aggregate_self (the aggregate with a scaled self term); 8:
-                              gta_update_mm_t_splits takes the stream (its attached knob set) */
+                              gta_update_mm_t_splits takes the stream (its attached knob set); 9:
+                              gta_update_mlp (two chained node GEMMs in one pass) */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -289,6 +290,18 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
  * as for every call on a stream.  Same reference as gta_update_mm. */
 int64_t gta_update_mm_t_splits(int64_t M, int64_t K, int64_t N, int dtype, void* stream);
 int64_t gta_update_mm_t_split_workspace_bytes(int64_t M, int64_t K, int64_t N, int64_t splits);
+
+/* Two chained applynode MMs with their SFs in one pass (GIN's MLP, vTCAD/GraphOP/genGraphOP.py:103-108:
+ * MM -> SF -> MM -> SF; replaces two gta_update_mm_t calls and the [M, N1] intermediate they pass
+ * through HBM): out = sf2(bf16(sf1(x W1)) W2).  x fp32 [M, K1] (rounded to bf16, RNE, as
+ * GTA_F32_BF16 rounds it), w1t = W1^T bf16 [N1][ldw1], w2t = W2^T bf16 [N2][ldw2]; K1, N1, N2 <= 128;
+ * dtype must be GTA_F32_BF16.  The intermediate is rounded to bf16 (RNE) exactly as the second
+ * unfused GEMM's staging rounds its fp32 input, and both products run the unfused kernels' k order:
+ * bitwise equal to gta_update_mm_t(x, W1, sf1) followed by gta_update_mm_t(z, W2, sf2).
+ * Reference: the two COMP_MM of interpreter.py's lowering (code/interpreter.py:335-343). */
+int gta_update_mlp(const float* x, int64_t ldx, int64_t M, int64_t K1, const void* w1t, int64_t ldw1, int64_t N1,
+                   int sf1, const void* w2t, int64_t ldw2, int64_t N2, int sf2, int dtype, float* out, int64_t ldo,
+                   void* stream);
 int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,
                           int64_t ldwt, int64_t N, int dtype, int sf, float* out, int64_t ldo, int64_t splits,
                           void* workspace, int64_t workspace_bytes, void* stream);

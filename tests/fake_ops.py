@@ -98,6 +98,21 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
     return _t(isa_ref.mm(xr, _np(w), None if row_idx is None else row_idx.cpu().numpy(), sf))
 
 
+MLP_CALLS = [0]  # fused MM -> SF -> MM -> SF launches (the executor's GIN MLP fusion)
+
+
+def update_mlp_supported(x, w1, w2):
+    return (x.dtype == torch.float32 and w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16
+            and max(w1.shape[0], w1.shape[1], w2.shape[1]) <= 128)
+
+
+def update_mlp(x, w1, w2, sf1=None, sf2=None, out=None):
+    """The two products in fp64, as this module's update_mm computes each (the bf16 rounding of the
+    real kernel is the GPU tests' business)."""
+    MLP_CALLS[0] += 1
+    return _t(isa_ref.mm(isa_ref.mm(_np(x), _np(w1), None, sf1), _np(w2), None, sf2))
+
+
 def tile_nnz(graph, T):
     ip, ix = graph.numpy()
     return torch.from_numpy(isa_ref.tile_nnz(ip, ix, graph.n_cols, T).astype(np.int32))

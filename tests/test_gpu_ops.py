@@ -1115,3 +1115,33 @@ def test_aggregate_self_term(dev, dt, F, heads, plan):
     got = ops.aggregate(g, x, "src", w, plan=plan, self_term=(x, s))
     torch.cuda.synchronize()
     assert torch.equal(got, want)
+
+
+@pytest.mark.parametrize("M,K1,N1,N2,sf1,sf2", [(20000, 100, 128, 128, "RELU", "RELU"), (4099, 128, 128, 128, None, "ELU"),
+                                                (3001, 64, 96, 48, "SIGMOID", None), (777, 100, 128, 100, "RELU", None),
+                                                (33, 37, 20, 8, "EXP", "RELU"), (5, 128, 128, 128, "RELU", "RELU")])
+def test_update_mlp_bitwise(dev, M, K1, N1, N2, sf1, sf2):
+    """gta_update_mlp (GIN's MM -> SF -> MM -> SF in one pass, no [M, N1] intermediate in HBM) ==
+    the two unfused mixed-precision UPDATEs bitwise: fp32 x rounded to bf16 as the first GEMM stages
+    it, the SF'd intermediate rounded to bf16 as the second GEMM stages it, the same k order; K and N
+    tails (37, 20, 8, 100, 96, 48), an SF with sf(0) != 0 in front of zero-padded k (SIGMOID, EXP),
+    row counts not a multiple of 16.  Both within the fp32 bound of fp64 on the bf16-rounded operands."""
+    rng = np.random.default_rng(M + K1 + N1 + N2)
+    x = torch.from_numpy(rng.standard_normal((M, K1)).astype(np.float32)).to(dev)
+    w1 = torch.from_numpy((rng.standard_normal((K1, N1)) / np.sqrt(K1)).astype(np.float32)).to(torch.bfloat16).to(dev)
+    w2 = torch.from_numpy((rng.standard_normal((N1, N2)) / np.sqrt(N1)).astype(np.float32)).to(torch.bfloat16).to(dev)
+    assert ops.update_mlp_supported(x, w1, w2)
+    fused = ops.update_mlp(x, w1, w2, sf1=sf1, sf2=sf2)
+    z = ops.update_mm(x, w1, sf=sf1)
+    ref2 = ops.update_mm(z, w2, sf=sf2)
+    torch.cuda.synchronize()
+    assert torch.equal(fused, ref2)
+    xb = x.to(torch.bfloat16).double().cpu().numpy()
+    zr = isa_ref.mm(xb, w1.double().cpu().numpy(), sf_kind=sf1)
+    zb = torch.from_numpy(zr.astype(np.float32)).to(torch.bfloat16).double().numpy()
+    # the fp64 intermediate and the GPU's fp32 one may round to neighbouring bf16 values: compare
+    # against fp64 of the GPU's own bf16 intermediate, bound from |z| |W2|
+    zg = z.to(torch.bfloat16).double().cpu().numpy()
+    ref = isa_ref.mm(zg, w2.double().cpu().numpy(), sf_kind=sf2)
+    _check(fused, ref, np.abs(zg) @ np.abs(w2.double().cpu().numpy()), "update_mlp")
+    assert np.abs(zb - zg).max() <= 2 ** -7 * np.abs(zb).max() + 1e-6  # neighbouring bf16 values at most

@@ -324,3 +324,26 @@ def test_sampled_checker_always_checks_the_special_rows(golden_dir, manifest, mo
     t[int(sp["heaviest"][0])] += 1.0
     with pytest.raises(AssertionError, match="heaviest"):
         chk.check(n_samples=2, seed=0, n_gather=2)
+
+
+@pytest.mark.parametrize("layer", ["layer2", "layer3"])
+def test_mlp_chain_fusion_cpu(golden_dir, manifest, monkeypatch, layer):
+    """GIN's MLP (applynode MM -> SF -> MM -> SF, genGraphOP.py:103-108) with bf16 weights and
+    widths <= 128 runs as one fused launch (ops.update_mlp); every op of the stream -- the fused-away
+    MM and SF values recomputed on demand -- equals the fp64 oracle; with the fusion off, no fused
+    launch."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    rec = [s for s in _streams(manifest) if s["network"] == "GIN" and not s["reorder"] and layer in s["file"]][0]
+    sem = Semantics.for_network("GIN", False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    gc, ip, ix = _cora_graph(golden_dir)
+    tensors = workloads.make_tensors(og, gc, "GIN", seed=9, dtype_w=torch.bfloat16)
+    ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
+    for fuse in (True, False):
+        calls = fake_ops.MLP_CALLS[0]
+        ex = executor.Executor(og, st, gc, tensors, sem)
+        ex.fuse_mlp = fuse
+        ex.run()
+        assert fake_ops.MLP_CALLS[0] == calls + (1 if fuse else 0)
+        compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
