@@ -2770,6 +2770,11 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
 // 8-B writes, 16-B pieces XOR-swizzled by row so the A-fragment reads are conflict-free) -> GEMM 2
 // (4 steps of 32 k, zero past N1).  Same operands, k order and rounding as the two unfused
 // launches: bitwise equal to them.  LDS 80 KiB: two blocks per CU.
+// SF1 / SF2: the SFs as template constants (RELU / NONE: the GIN configurations), -1 = the runtime
+// sf1 / sf2 (every other SF; a switch per tile).  x rows 16-B aligned with K1 % 4 == 0 (the host
+// checks), so every 16-B piece of x is wholly inside K1 or wholly past it: clamped loads and a
+// select, no branches -- a branchy masked load made the compiler drain every load in flight.
+template <int SF1, int SF2>
 __global__ void __launch_bounds__(kBlock, 2)
 k_mlp_bf(const float* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint16_t* __restrict__ w1t,
          int64_t ldw1, int N1, int sf1, const uint16_t* __restrict__ w2t, int64_t ldw2, int N2, int sf2,
@@ -2794,48 +2799,52 @@ k_mlp_bf(const float* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint
     *reinterpret_cast<uint4*>(wres + f * 1024 + L * 16) = *reinterpret_cast<const uint4*>(tmp);
   }
   __syncthreads();
-  const int S1 = (K1 + 31) / 32;
   const int64_t n_groups = (M + 15) / 16;
   const int64_t gstep = static_cast<int64_t>(gridDim.x) * kWavesPerBlock;
   int64_t grp = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wv;
-  const bool xvec = ldx % 4 == 0 && aligned(x, 16);
+  // x pieces by buffer loads through a descriptor over the group's rows: a piece past K1 (or a row
+  // past M) takes an out-of-range offset and reads zeros -- no branch around the loads, so nothing
+  // makes the compiler drain the next groups' loads in flight
+  const uint32_t row_bytes = static_cast<uint32_t>(ldx) * 4u;
   auto load_x = [&](int64_t gi, float4 (&xa)[SB][2]) __attribute__((always_inline)) {
-    const float* xr = x + min<int64_t>(gi * 16 + r16, M - 1) * ldx;
+    const int64_t row0 = gi * 16;
+    const int64_t rows = max<int64_t>(0, min<int64_t>(16, M - row0));  // 0 past the last group: all zeros
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(x + row0 * ldx), 0, static_cast<int>(rows * row_bytes), 0x00020000);
+    const uint32_t roff = static_cast<uint32_t>(r16) * row_bytes;
 #pragma unroll
     for (int st = 0; st < SB; ++st)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int k = 32 * st + 8 * g + 4 * h;
-        float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-        if (st < S1) {
-          if (xvec && k + 4 <= K1) {
-            v = *reinterpret_cast<const float4*>(xr + k);
-          } else {
-            if (k < K1) v.x = xr[k];
-            if (k + 1 < K1) v.y = xr[k + 1];
-            if (k + 2 < K1) v.z = xr[k + 2];
-            if (k + 3 < K1) v.w = xr[k + 3];
-          }
-        }
-        xa[st][h] = v;
+        const uint32_t off = k < K1 ? roff + static_cast<uint32_t>(k) * 4u : 0x80000000u;
+        xa[st][h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
       }
+  };
+  auto sf_acc = [&](f32x4 (&acc)[1][NT], int sfc, auto tag) __attribute__((always_inline)) {
+    constexpr int K = decltype(tag)::value;
+    if constexpr (K < 0) {
+      sf_tile(sfc, acc);
+    } else if constexpr (K != GTA_SF_NONE) {
+#pragma unroll
+      for (int c = 0; c < NT; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) acc[0][c][r] = sf_apply(K, acc[0][c][r]);
+    }
   };
   const uint32_t wbase = GTA_LDS_ADDR(wres) + static_cast<uint32_t>(lane) * 16u;
   const uint32_t zw = GTA_LDS_ADDR(zimg) + static_cast<uint32_t>(wv) * 4096u;
   const bool vstore = ldo % 4 == 0 && aligned(out, 16);
   const int p = r16 & 3, qq = r16 >> 2;
-  float4 xa[SB][2];
-  if (grp < n_groups) load_x(grp, xa);
-  for (; grp < n_groups; grp += gstep) {
-    float4 xn[SB][2];
-    if (grp + gstep < n_groups) load_x(grp + gstep, xn);
+  // one 16-row group: GEMM 1, the z image, GEMM 2, the stores
+  auto compute = [&](const float4 (&xa)[SB][2], int64_t grp) __attribute__((always_inline)) {
     f32x4 acc[1][NT];
 #pragma unroll
     for (int c = 0; c < NT; ++c) acc[0][c] = f32x4{0.f, 0.f, 0.f, 0.f};
     // GEMM 1: k_mm_ring_bf's step order, every step padded with zeros past K1
 #pragma unroll
     for (int st = 0; st < SB; ++st) {
-      if (st >= S1) break;
+      if (32 * st >= K1) break;  // (wave-uniform)
       bf16x8 a8;  // x rounded to bf16 (RNE) as k_mm_ring_bf rounds it
       a8[0] = static_cast<short>(to_bf16_bits(xa[st][0].x));
       a8[1] = static_cast<short>(to_bf16_bits(xa[st][0].y));
@@ -2855,7 +2864,7 @@ k_mlp_bf(const float* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint
       for (int c = 0; c < NT; ++c)
         acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, __builtin_bit_cast(bf16x8, b4[c]), acc[0][c], 0, 0, 0);
     }
-    sf_tile(sf1, acc);
+    sf_acc(acc, sf1, std::integral_constant<int, SF1>{});
     // z tile -> bf16 image [16 rows][128 k] of this wave: lane (g, 4qq + p) holds rows 4g + r, column
     // 16c + 4qq + p; the quad transpose leaves row 4g + p, columns 16c + 4qq .. +3 (one 8-B write).
     // 16-B piece P of row r sits at piece P ^ r (conflict-free A-fragment reads below)
@@ -2905,7 +2914,7 @@ k_mlp_bf(const float* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint
       for (int c = 0; c < NT; ++c)
         acc[0][c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a8, __builtin_bit_cast(bf16x8, b4[c]), acc[0][c], 0, 0, 0);
     }
-    sf_tile(sf2, acc);
+    sf_acc(acc, sf2, std::integral_constant<int, SF2>{});
     const int64_t mw = grp * 16;
     if (vstore) {
 #pragma unroll
@@ -2947,11 +2956,26 @@ k_mlp_bf(const float* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint
           if (m < M && n < N2) out[m * ldo + n] = acc[0][c][r];
         }
     }
-#pragma unroll
-    for (int st = 0; st < SB; ++st) {
-      xa[st][0] = xn[st][0];
-      xa[st][1] = xn[st][1];
-    }
+  };
+  // three register buffers, two groups' x loads in flight while one group computes (a group's MFMA
+  // work is shorter than an HBM round trip; one group ahead left the waves waiting on their loads)
+  // The loop body is straight-line (no exits between the loads and their use, which would let the
+  // compiler sink the loads next to their use): every wave runs whole rounds of three groups, and a
+  // group past the last reads zeros (empty descriptor) and stores nothing (rows past M are masked).
+  const int64_t mine = grp < n_groups ? (n_groups - grp + gstep - 1) / gstep : 0;
+  const int64_t rounds = (mine + 2) / 3;
+  float4 xa[SB][2], xb[SB][2], xc[SB][2];
+  if (rounds > 0) {
+    load_x(grp, xa);
+    load_x(grp + gstep, xb);
+  }
+  for (int64_t t = 0; t < rounds; ++t, grp += 3 * gstep) {
+    load_x(grp + 2 * gstep, xc);
+    compute(xa, grp);
+    load_x(grp + 3 * gstep, xa);
+    compute(xb, grp + gstep);
+    load_x(grp + 4 * gstep, xb);
+    compute(xc, grp + 2 * gstep);
   }
 }
 
@@ -3964,11 +3988,24 @@ int gta_update_mlp(const float* x, int64_t ldx, int64_t M, int64_t K1, const voi
   if (!x || !w1t || !w2t || !out) return fail(GTA_ERR_ARG, "update_mlp: bad arguments");
   if (dtype != GTA_F32_BF16) return fail(GTA_ERR_UNSUPPORTED, "update_mlp: fp32 x with bf16 weights only");
   if (K1 > 128 || N1 > 128 || N2 > 128) return fail(GTA_ERR_UNSUPPORTED, "update_mlp: K1, N1, N2 <= 128");
+  if (K1 % 4 || ldx % 4 || !aligned(x, 16) || ldx > (1 << 20))
+    return fail(GTA_ERR_UNSUPPORTED, "update_mlp: x rows 16-B aligned with K1 % 4 == 0");
   const int64_t n_groups = (M + 15) / 16;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n_groups + kWavesPerBlock - 1) / kWavesPerBlock, 512));
-  k_mlp_bf<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, S(stream)>>>(
-      x, ldx, M, static_cast<int>(K1), static_cast<const uint16_t*>(w1t), ldw1, static_cast<int>(N1), sf1,
-      static_cast<const uint16_t*>(w2t), ldw2, static_cast<int>(N2), sf2, out, ldo);
+  const dim3 gr(static_cast<unsigned>(blocks));
+  const uint16_t* w1 = static_cast<const uint16_t*>(w1t);
+  const uint16_t* w2 = static_cast<const uint16_t*>(w2t);
+  const int k1 = static_cast<int>(K1), n1 = static_cast<int>(N1), n2 = static_cast<int>(N2);
+  const bool c1 = sf1 == GTA_SF_NONE || sf1 == GTA_SF_RELU, c2 = sf2 == GTA_SF_NONE || sf2 == GTA_SF_RELU;
+#define GTA_MLP(A_, B_) \
+  k_mlp_bf<A_, B_><<<gr, dim3(kBlock), 0, S(stream)>>>(x, ldx, M, k1, w1, ldw1, n1, sf1, w2, ldw2, n2, sf2, out, ldo)
+  if (c1 && c2) {
+    if (sf1 == GTA_SF_RELU) { if (sf2 == GTA_SF_RELU) GTA_MLP(GTA_SF_RELU, GTA_SF_RELU); else GTA_MLP(GTA_SF_RELU, GTA_SF_NONE); }
+    else { if (sf2 == GTA_SF_RELU) GTA_MLP(GTA_SF_NONE, GTA_SF_RELU); else GTA_MLP(GTA_SF_NONE, GTA_SF_NONE); }
+  } else {
+    GTA_MLP(-1, -1);
+  }
+#undef GTA_MLP
   GTA_LAUNCHED("k_mlp_bf");
   return GTA_OK;
 }

@@ -486,11 +486,12 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
 
 
 def update_mlp_supported(x, w1, w2):
-    """Shapes gta_update_mlp takes: fp32 x [M, K1] with unit column stride, bf16 W1 [K1, N1] and
-    W2 [N1, N2], K1, N1, N2 <= 128."""
+    """Shapes gta_update_mlp takes: fp32 x [M, K1] with unit column stride and 16-B aligned rows,
+    K1 % 4 == 0, bf16 W1 [K1, N1] and W2 [N1, N2], K1, N1, N2 <= 128."""
     return (x.dtype == torch.float32 and x.dim() == 2 and w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16
             and w1.dim() == 2 and w2.dim() == 2 and x.shape[1] == w1.shape[0] and w1.shape[1] == w2.shape[0]
-            and max(w1.shape[0], w1.shape[1], w2.shape[1]) <= 128 and (x.shape[0] <= 1 or x.stride(1) == 1))
+            and max(w1.shape[0], w1.shape[1], w2.shape[1]) <= 128 and (x.shape[0] <= 1 or x.stride(1) == 1)
+            and x.shape[1] % 4 == 0 and (x.shape[0] <= 1 or x.stride(0) % 4 == 0) and x.data_ptr() % 16 == 0)
 
 
 def update_mlp(x, w1, w2, sf1=None, sf2=None, out=None):

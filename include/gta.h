@@ -294,8 +294,8 @@ int64_t gta_update_mm_t_split_workspace_bytes(int64_t M, int64_t K, int64_t N, i
 /* Two chained applynode MMs with their SFs in one pass (GIN's MLP, vTCAD/GraphOP/genGraphOP.py:103-108:
  * MM -> SF -> MM -> SF; replaces two gta_update_mm_t calls and the [M, N1] intermediate they pass
  * through HBM): out = sf2(bf16(sf1(x W1)) W2).  x fp32 [M, K1] (rounded to bf16, RNE, as
- * GTA_F32_BF16 rounds it), w1t = W1^T bf16 [N1][ldw1], w2t = W2^T bf16 [N2][ldw2]; K1, N1, N2 <= 128;
- * dtype must be GTA_F32_BF16.  The intermediate is rounded to bf16 (RNE) exactly as the second
+ * GTA_F32_BF16 rounds it; rows 16-B aligned, K1 % 4 == 0), w1t = W1^T bf16 [N1][ldw1], w2t = W2^T bf16
+ * [N2][ldw2]; K1, N1, N2 <= 128; dtype must be GTA_F32_BF16 (GTA_ERR_UNSUPPORTED otherwise).  The intermediate is rounded to bf16 (RNE) exactly as the second
  * unfused GEMM's staging rounds its fp32 input, and both products run the unfused kernels' k order:
  * bitwise equal to gta_update_mm_t(x, W1, sf1) followed by gta_update_mm_t(z, W2, sf2).
  * Reference: the two COMP_MM of interpreter.py's lowering (code/interpreter.py:335-343). */

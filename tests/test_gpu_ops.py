@@ -1119,12 +1119,12 @@ def test_aggregate_self_term(dev, dt, F, heads, plan):
 
 @pytest.mark.parametrize("M,K1,N1,N2,sf1,sf2", [(20000, 100, 128, 128, "RELU", "RELU"), (4099, 128, 128, 128, None, "ELU"),
                                                 (3001, 64, 96, 48, "SIGMOID", None), (777, 100, 128, 100, "RELU", None),
-                                                (33, 37, 20, 8, "EXP", "RELU"), (5, 128, 128, 128, "RELU", "RELU")])
+                                                (33, 36, 20, 8, "EXP", "RELU"), (5, 128, 128, 128, "RELU", "RELU")])
 def test_update_mlp_bitwise(dev, M, K1, N1, N2, sf1, sf2):
     """gta_update_mlp (GIN's MM -> SF -> MM -> SF in one pass, no [M, N1] intermediate in HBM) ==
     the two unfused mixed-precision UPDATEs bitwise: fp32 x rounded to bf16 as the first GEMM stages
     it, the SF'd intermediate rounded to bf16 as the second GEMM stages it, the same k order; K and N
-    tails (37, 20, 8, 100, 96, 48), an SF with sf(0) != 0 in front of zero-padded k (SIGMOID, EXP),
+    tails (36, 20, 8, 100, 96, 48), an SF with sf(0) != 0 in front of zero-padded k (SIGMOID, EXP),
     row counts not a multiple of 16.  Both within the fp32 bound of fp64 on the bf16-rounded operands."""
     rng = np.random.default_rng(M + K1 + N1 + N2)
     x = torch.from_numpy(rng.standard_normal((M, K1)).astype(np.float32)).to(dev)
