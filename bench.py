@@ -14,8 +14,9 @@ before the timed region.
       rows and column groups of source columns, both nnz-balanced from the tile metadata (column
       cuts from the all-reduced per-column nnz).  Each rank aggregates its tile into partial
       vertex aggregates; the pc ranks of a row group sum them with an RCCL reduce-scatter per
-      destination-row chunk, issued while the next chunk aggregates.  Every rank ends with its
-      complete rows of Y.  Grid 1x2, 2x2, 4x2 at N = 2, 4, 8 (--grid PRxPC to override).
+      destination-row chunk (three chunks of 55 / 30 / 15 % of the rows by default), issued while the
+      next chunk aggregates.  Every rank ends with its complete rows of Y.  Grid 1x2, 2x2, 4x2 at
+      N = 2, 4, 8 (--grid PRxPC to override).
   --mode rows: destination-row tiles (complete rows, no reduction) followed by the RCCL
       all-gather of Y that the next layer's scatter C needs, per row chunk, overlapped likewise.
 Each rank generates only its row group's edges and its column slice of X (metric.Shard).
@@ -178,15 +179,18 @@ def build(args, world, rank, dev, backend, note, col_counts=None):
     mode, pr, pc = grid_of(args, world)
     if mode == "rows" and pc != 1:
         raise SystemExit("--mode rows uses a PRx1 grid")
-    chunks = args.row_chunks or (1 if world == 1 else 2)
     # edges mode: the last chunk's reduce-scatter is the exchange left exposed after the last launch,
-    # so the chunks shrink toward the end (default 70 / 30 for two: the first chunk's exchange still
-    # hides under the second's compute at up to ~2x the modelled xGMI time)
+    # so the chunks shrink toward the end: default three chunks of 55 / 30 / 15 % of the rows, the
+    # split whose modelled 8-GPU step degrades least as the link rate falls (6.53x at 64 GB/s per
+    # direction, 6.35x at 40; two chunks of 70 / 30: 6.70x and 5.95x; every chunk launch costs
+    # 0.02-0.06 ms of compute; per-chunk times of the 4 x 2 tile: profiles/r04/tile_chunks_4x2_r0.log,
+    # DESIGN §6).  rows mode: two equal chunks.
+    chunks = args.row_chunks or (1 if world == 1 else (3 if mode == "edges" and pc > 1 else 2))
     fracs = None
     if mode == "edges" and pc > 1 and chunks > 1:
         cf = getattr(args, "chunk_fracs", "auto")
         if cf == "auto":
-            fracs = [0.7, 0.3] if chunks == 2 else None
+            fracs = {2: [0.7, 0.3], 3: [0.55, 0.3, 0.15]}.get(chunks)
         elif cf != "equal":
             fracs = [float(v) for v in cf.split(",")]
     count_reduce = None
@@ -520,7 +524,8 @@ def main():
     ap.add_argument("--grid", default="auto", help="PRxPC rank grid (auto: 1x2, 2x2, 4x2; rows: Nx1)")
     ap.add_argument("--row-chunks", type=int, default=0, help="row chunks per tile for comm overlap (0 = auto)")
     ap.add_argument("--chunk-fracs", default="auto",
-                    help="edges mode: relative row-chunk sizes, e.g. 0.7,0.3 ('equal'; 'auto' = 0.7,0.3 for two)")
+                    help="edges mode: relative row-chunk sizes, e.g. 0.7,0.3 ('equal'; 'auto' = 0.55,0.3,0.15 for "
+                         "three, the default count, and 0.7,0.3 for two)")
     ap.add_argument("--impl", choices=["blocked", "plan"], default="blocked")
     ap.add_argument("--blocks", type=int, default=0, help="column blocks (0 = auto, ~6 MB X slices)")
     ap.add_argument("--n", "--graph-nodes", dest="n", type=int, default=N_REDDIT)

@@ -130,7 +130,7 @@ def test_default_grids():
     assert [distributed.grid_shape(w, "rows") for w in (2, 4, 8)] == [(2, 1), (4, 1), (8, 1)]
 
 
-def _bench_worker(rank, world, port, mode, q, n=N, e=E):
+def _bench_worker(rank, world, port, mode, q, n=N, e=E, chunks=2):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), WORLD_SIZE=str(world), RANK=str(rank))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -148,9 +148,11 @@ def _bench_worker(rank, world, port, mode, q, n=N, e=E):
         bench.Aggregate.launch = launch
         bench.ops.BlockedPlan.auto_blocks = staticmethod(lambda g, f: 1)   # single-pass plan, no device plan
         bench.G.Graph.plan = lambda self, chunk=512: None
-        args = types.SimpleNamespace(mode=mode, grid="auto", row_chunks=2, chunk_fracs="auto", n=n, e=e, blocks=0,
+        args = types.SimpleNamespace(mode=mode, grid="auto", row_chunks=chunks, chunk_fracs="auto", n=n, e=e, blocks=0,
                                      impl="plan")
-        shard, agg, m, pr, pc, chunks = bench.build(args, world, rank, torch.device("cpu"), "gloo", lambda s: None)
+        shard, agg, m, pr, pc, n_chunks = bench.build(args, world, rank, torch.device("cpu"), "gloo", lambda s: None)
+        if chunks == 0:  # bench's default: three weighted chunks in edges mode, two in rows mode
+            assert n_chunks == (3 if (mode == "edges" and pc > 1) else 2)
         for _ in range(2):
             agg.step()
         g = shard.grid
@@ -184,19 +186,21 @@ def _bench_worker(rank, world, port, mode, q, n=N, e=E):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world,mode,n,e", [(2, "edges", N, E), (4, "edges", N, E), (2, "rows", N, E),
-                                           (3, "rows", N, E), (8, "edges", N, E), (8, "edges", 400, 9),
-                                           (8, "edges", 8, 20)])
-def test_bench_exchange_gloo(world, mode, n, e):
+@pytest.mark.parametrize("world,mode,n,e,chunks", [(2, "edges", N, E, 2), (4, "edges", N, E, 2), (2, "rows", N, E, 2),
+                                                  (3, "rows", N, E, 2), (8, "edges", N, E, 2), (8, "edges", 400, 9, 2),
+                                                  (8, "edges", 8, 20, 2), (8, "edges", N, E, 0), (2, "edges", N, E, 0),
+                                                  (8, "edges", 8, 20, 0)])
+def test_bench_exchange_gloo(world, mode, n, e, chunks):
     """bench.py's N-rank step (gloo, oracle kernels): every rank's rows after the exchange match the
     fp64 oracle; in rows mode the gathered table is the whole Y.  World 8 runs the driver's 8-GPU
     layout, the 4 x 2 grid with one row-group sub-group per pair of ranks (distributed.row_groups),
     every rank's owned rows checked; the 9-edge graph leaves ranks with empty tiles; the 8-row graph
-    gives row blocks of one row per rank, so the 70 / 30 chunking leaves an empty last chunk."""
+    gives row blocks of one row per rank, so the 70 / 30 chunking leaves an empty last chunk.  chunks = 0:
+    bench's default count (three chunks of 55 / 30 / 15 % in edges mode)."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, mode, q, n, e)) for r in range(world)]
+    procs = [ctx.Process(target=_bench_worker, args=(r, world, port, mode, q, n, e, chunks)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
