@@ -531,6 +531,9 @@ def main():
     ap.add_argument("--n", "--graph-nodes", dest="n", type=int, default=N_REDDIT)
     ap.add_argument("--e", "--graph-edges", dest="e", type=int, default=E_REDDIT)
     ap.add_argument("--parity-rows", type=int, default=256, help="sampled rows per rank for the fp64 oracle")
+    ap.add_argument("--layers", default="sage-reddit,gin-products",
+                    help="BASELINE-config layers timed after the metric at the same N (destination-row shards; "
+                         "'none' to skip): the 'layers' field")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-s", type=float, default=12.0,
                     help="CPU work per thread count of the cpu_baseline leg (seconds, approx.)")
@@ -740,6 +743,20 @@ def main():
         "parity": parity,
         "roofline": roof,
     }
+    # whole BASELINE-config layers at the same N (configs #4 / #5: GraphSAGE Reddit, GIN products), every
+    # rank, after the metric (secondary numbers: the metric above is the headline)
+    if args.layers and args.layers != "none":
+        del agg
+        torch.cuda.empty_cache()
+        recs = []
+        for name in args.layers.split(","):
+            log(rank, f"layer {name}")
+            try:
+                recs.append(distributed.layer_record(name.strip(), dev, rank, world, reps=3, backend=backend))
+            except Exception as exc:  # reported, not fatal: the metric line above stands on its own
+                recs.append({"config": name, "n_gpus": world, "error": f"{type(exc).__name__}: {exc}"[:300]})
+            log(rank, f"layer {name}: {json.dumps(recs[-1])[:200]}")
+        result["layers"] = recs
     if rank == 0 and not args.no_cpu_baseline:  # after the timed region; other ranks wait at the barrier
         log(rank, "cpu baseline")
         result["cpu_baseline"] = cpu_baseline(shard, target_s=args.cpu_baseline_s)

@@ -321,6 +321,67 @@ def run_stream(opgraph, stream, shard, tensors, semantics=None, group=None, plan
     return res, ex
 
 
+def layer_record(name, dev, rank, world, reps=3, backend=None, check=True):
+    """One BASELINE config (configs.CONFIGS) forward on this rank's destination-row shard (RowShard,
+    replicated model inputs), timed over `reps` forwards after one warm-up: barrier + device sync
+    around each, the max over ranks.  With check, rank 0 re-assembles the output rows and compares
+    them with a one-device execution of the same stream on the same inputs (max |d| / max |ref|).
+    -> the record bench.py's "layers" field and scripts/dist_layers.py print (every rank gets it)."""
+    import time
+
+    from . import configs, executor
+    layers, g, tensors = configs.build(name, dev)
+    shard = RowShard(g, rank, world) if world > 1 else None
+    times, comm_bytes = [], 0
+    x = ex = None
+    for r in range(reps + 1):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        x = None
+        for lay, t in zip(layers, tensors):
+            t = dict(t)
+            if x is not None:
+                t["x"] = x
+            if world > 1:
+                res, ex = run_stream(lay.opgraph, lay.stream, shard, t, lay.sem)
+                if r == 0:
+                    comm_bytes += ex.dist.bytes
+            else:
+                res, ex = executor.run_stream(lay.opgraph, lay.stream, g, t, lay.sem, sync=False)
+            x = res.outputs[sorted(res.outputs)[-1]]
+        torch.cuda.synchronize(dev)
+        dt = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                          device=dev if backend in (None, "nccl") else "cpu")
+        if world > 1:
+            dist.all_reduce(dt, op=dist.ReduceOp.MAX)
+        if r:
+            times.append(float(dt))
+    err = None
+    if world > 1 and check:
+        full = ex.dist.full_rows(x)
+        if rank == 0:
+            y = None
+            for lay, t in zip(layers, tensors):
+                t = dict(t)
+                if y is not None:
+                    t["x"] = y
+                r1, _ = executor.run_stream(lay.opgraph, lay.stream, g, t, lay.sem)
+                y = r1.outputs[sorted(r1.outputs)[-1]]
+            fin = torch.isfinite(y)
+            err = float(((full - y).abs()[fin]).max() / (y.abs()[fin].max() + 1e-30))
+    ms = 1e3 * sorted(times)[len(times) // 2]
+    rec = {"config": name, "n_gpus": world, "N": g.n_rows, "E": g.nnz, "layers": [l.layer for l in layers],
+           "shard_edges": shard.graph.nnz if shard is not None else g.nnz, "ms_per_forward": ms,
+           "edges_per_s": g.nnz * len(layers) / (ms / 1e3), "exchanged_bytes_per_rank": comm_bytes,
+           "layout": "destination-row shards, replicated model inputs, all-gathered computed tables" if world > 1
+           else "one GPU", "max_norm_diff_vs_1dev": err}
+    del layers, g, tensors, shard, ex, x
+    torch.cuda.empty_cache()
+    return rec
+
+
 def grid_shape(world, mode="edges"):
     """Default rank grid (row groups pr x column groups pc) of the metric aggregate.
 

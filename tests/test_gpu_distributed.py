@@ -72,7 +72,7 @@ def test_two_rank_bench_full_size(mode):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()),
            os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1", "--mode", mode,
-           "--parity-rows", "128", "--cpu-baseline-s", "3"]
+           "--parity-rows", "128", "--cpu-baseline-s", "3", "--layers", "gcn-cora"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=170)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = [json.loads(line) for line in r.stdout.splitlines() if line.startswith("{")][-1]
@@ -89,6 +89,11 @@ def test_two_rank_bench_full_size(mode):
         assert p["exposed_exchange_ms"] >= 0 and p["step_ms"] > 0
     cb = rec["cpu_baseline"]
     assert cb is not None and cb["value"] > 0 and cb["cores"] >= 1 and cb["kind"] == "port", cb
+    # the whole-layer records at the same N (row shards; GCN Cora keeps the rehearsal short)
+    (lay,) = rec["layers"]
+    assert "error" not in lay, lay
+    assert lay["config"] == "gcn-cora" and lay["n_gpus"] == 2 and lay["ms_per_forward"] > 0
+    assert lay["max_norm_diff_vs_1dev"] is not None and lay["max_norm_diff_vs_1dev"] <= 1e-5, lay
 
 
 @pytest.mark.gpu
