@@ -21,7 +21,7 @@ for s in $STEPS; do
     prof)
       export TMPDIR=/tmp
       timeout -k 10 ${T_PROF:-600} rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run \
-        -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-pmc ${BENCH_ARGS} > gpurun_out/prof.log 2>&1
+        -- python3 bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-pmc --layers none ${BENCH_ARGS} > gpurun_out/prof.log 2>&1
       rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.log; stop_if_fatal $rc prof ;;
     pmc)
       export TMPDIR=/tmp
