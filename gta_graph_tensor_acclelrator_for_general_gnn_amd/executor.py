@@ -1166,16 +1166,18 @@ def aggregate_trace(events):
 # with the same op graph, stream, CSR and input tensors (same objects; their CONTENTS may change in
 # place) captures the whole stream execution once (GraphedRun) and every later call replays it --
 # one graph launch instead of one Python-driven launch per op, which is what small layers (Cora,
-# Flickr) are bound by.  The outputs of a replayed call are the graph's own tensors: the next
-# call with the same inputs overwrites them (clone what must survive it).  Only graphs of at most
-# AUTO_GRAPH_MAX_EDGES edges (launch-bound; larger layers are kernel-bound and a graph's private
-# memory pool would hold their intermediates); AUTO_GRAPH = False turns it off (set_auto_graph(False)
-# also drops every captured graph).  A replay is keyed by the objects AND their storage (data_ptr,
+# Flickr) are bound by, and no host gaps between the kernels of large ones (round 4, every size:
+# GAT Reddit 5.61 -> 5.30 ms, GraphSAGE Reddit 4.84 -> 4.73, GIN products 6.54 -> 6.47,
+# profiles/r04/layer_bench_graph_all.log).  The outputs of a replayed call are the graph's own
+# tensors: the next call with the same inputs overwrites them (clone what must survive it).  A
+# captured graph keeps its intermediates in a private memory pool (a few GB for the Reddit-scale
+# layers, against 288 GB of HBM); AUTO_GRAPH_MAX_EDGES bounds the graphs it applies to,
+# AUTO_GRAPH = False turns it off (set_auto_graph(False) also drops every captured graph).  A replay is keyed by the objects AND their storage (data_ptr,
 # shape, stride), the calling thread's libgta knob state (ops.knob_state) and stays eager on a stream with an attached
 # knob set; weights changed in place are re-transposed into the graph's W^T before the replay.
 FUSE_MLP = True  # default of Executor.fuse_mlp (layer benches A/B it)
 AUTO_GRAPH = True
-AUTO_GRAPH_MAX_EDGES = 1 << 23
+AUTO_GRAPH_MAX_EDGES = 1 << 40  # every graph (round 3: 1 << 23, launch-bound layers only)
 AUTO_GRAPH_MAX_ENTRIES = 32
 _AUTO = {}
 
@@ -1339,7 +1341,7 @@ def execute(tile_size_list, dataset, network, layer, isReorder, isSinput=False, 
     Chrome trace JSON of the measured per-op device time, as the reference's chrome_timeline.json.
 
     From the second call with the same stream, CSR and input tensor objects on (graphs of at most
-    AUTO_GRAPH_MAX_EDGES edges), the execution replays a captured HIP graph: the outputs are then
+    AUTO_GRAPH_MAX_EDGES edges: every graph by default), the execution replays a captured HIP graph: the outputs are then
     the graph's own tensors and the next such call overwrites them -- clone what must outlive it
     (AUTO_GRAPH = False keeps every call eager, with fresh outputs)."""
     op_path = op_path or ir.op_yaml_path(network, dataset, layer, isReorder, op_root)
