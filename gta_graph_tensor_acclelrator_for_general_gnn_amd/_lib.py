@@ -10,7 +10,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgta.so")
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 # enum mirrors of include/gta.h
 GTA_F32, GTA_BF16, GTA_F32_BF16 = 0, 1, 2
@@ -30,7 +30,7 @@ SIGNATURES = {
     "gta_aggregate": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _i64,
                              _i32, _vp, _i64, _vp, _vp]),
     "gta_aggregate_self": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _i64,
-                                  _vp, _vp, _i64, _vp, _i64, _vp, _vp]),
+                                  _vp, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
     "gta_aggregate_plan_bytes": (_i64, [_i64, _i64, _i64]),
     "gta_aggregate_plan_build": (_i32, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
     "gta_aggregate_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),

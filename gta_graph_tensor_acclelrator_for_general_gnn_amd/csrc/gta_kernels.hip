@@ -119,6 +119,10 @@ __device__ __forceinline__ void load_row(Vec<VW>& o, const uint16_t* p) {
 }
 __device__ __forceinline__ float load_elem(const float* p) { return *p; }
 __device__ __forceinline__ float load_elem(const uint16_t* p) { return __uint_as_float(static_cast<uint32_t>(*p) << 16); }
+__device__ __forceinline__ uint16_t to_bf16_bits(float f) {
+  return __builtin_bit_cast(uint16_t, __float2bfloat16(f));  // round to nearest even
+}
+__device__ __forceinline__ uint16_t to_bf16_bits(uint16_t b) { return b; }
 
 __device__ __forceinline__ int wave_id_uniform() {
   return __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
@@ -239,9 +243,11 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
             const float* __restrict__ w, int64_t ldw, int gsz,
             const float* __restrict__ row_scale, float* __restrict__ y, int64_t ldy, int accumulate,
             float* __restrict__ partial, const TX* __restrict__ xs = nullptr, int64_t ldxs = 0,
-            const float* __restrict__ self_scale = nullptr) {
+            const float* __restrict__ self_scale = nullptr, int y_bf16 = 0) {
   // xs (gta_aggregate_self): y[row] = self_scale * xs[row] + row_scale[row] * sum, the self term
-  // formed exactly as an applynode MUL by a broadcast scalar would (GIN op 3 + op 4)
+  // formed exactly as an applynode MUL by a broadcast scalar would (GIN op 3 + op 4).
+  // y_bf16: y holds bf16 (RNE of the fp32 value; ldy in bf16 elements) -- for a consumer that rounds
+  // its input to bf16 anyway (the fused GIN MLP), so the rounding happens once, here
   constexpr int EPI = kWave / LPE;                 // edges per wave instruction
   // row loads in flight per lane: ~64 B of each lane's rows per unrolled step
   constexpr int XB = NV * VW * static_cast<int>(sizeof(TX));
@@ -380,7 +386,13 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
 #pragma unroll
             for (int k = 0; k < VW; ++k) o.v[k] = scale * acc[v][k];
           }
-          o.store(yp);
+          if (y_bf16) {
+            uint16_t* yb = reinterpret_cast<uint16_t*>(y) + row * ldy + col[v];
+#pragma unroll
+            for (int k = 0; k < VW; ++k) yb[k] = to_bf16_bits(o.v[k]);
+          } else {
+            o.store(yp);
+          }
         }
       }
     }
@@ -1400,7 +1412,8 @@ __global__ void k_items_permute(BlockedView v, int64_t n_rows, int B) {
 __global__ void __launch_bounds__(kBlock)
 k_aggregate_combine(PlanView plan, int F, const float* __restrict__ row_scale, float* __restrict__ y, int64_t ldy,
                     int accumulate, const float* __restrict__ partial, const void* __restrict__ xs = nullptr,
-                    int64_t ldxs = 0, int xs_bf16 = 0, const float* __restrict__ self_scale = nullptr) {
+                    int64_t ldxs = 0, int xs_bf16 = 0, const float* __restrict__ self_scale = nullptr,
+                    int y_bf16 = 0) {
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t s = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
   if (s >= plan.hdr[1]) return;
@@ -1412,14 +1425,17 @@ k_aggregate_combine(PlanView plan, int F, const float* __restrict__ row_scale, f
     float a = 0.f;
     for (int j = 0; j < cnt; ++j) a += partial[(first + j) * F + c];
     float* yp = y + row * ldy + c;
+    float v;
     if (xs != nullptr) {  // the self term, as k_aggregate forms it
 #pragma clang fp contract(off)
       const float xv = xs_bf16 ? load_elem(static_cast<const uint16_t*>(xs) + row * ldxs + c)
                                : static_cast<const float*>(xs)[row * ldxs + c];
-      *yp = xv * (self_scale ? *self_scale : 1.f) + scale * a;
+      v = xv * (self_scale ? *self_scale : 1.f) + scale * a;
     } else {
-      *yp = accumulate ? (*yp + scale * a) : scale * a;
+      v = accumulate ? (*yp + scale * a) : scale * a;
     }
+    if (y_bf16) reinterpret_cast<uint16_t*>(y)[row * ldy + c] = to_bf16_bits(v);
+    else *yp = v;
   }
 }
 
@@ -1876,10 +1892,6 @@ k_mm_f32(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ r
 // fragments are one 16-B LDS read.
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
 
-__device__ __forceinline__ uint16_t to_bf16_bits(float f) {
-  return __builtin_bit_cast(uint16_t, __float2bfloat16(f));  // round to nearest even
-}
-__device__ __forceinline__ uint16_t to_bf16_bits(uint16_t b) { return b; }
 
 template <typename TA>
 __global__ void __launch_bounds__(kBlock)
@@ -2774,9 +2786,11 @@ k_mm_ring_bf(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
 // sf1 / sf2 (every other SF; a switch per tile).  x rows 16-B aligned with K1 % 4 == 0 (the host
 // checks), so every 16-B piece of x is wholly inside K1 or wholly past it: clamped loads and a
 // select, no branches -- a branchy masked load made the compiler drain every load in flight.
-template <int SF1, int SF2>
+// TA = uint16_t: x is bf16 already (the aggregate rounded it, gta_aggregate_self y_dtype BF16): one
+// 16-B piece of 8 values per lane and 32-k step, pairs past K1 zeroed; no rounding (exact values).
+template <int SF1, int SF2, typename TA = float>
 __global__ void __launch_bounds__(kBlock, 2)
-k_mlp_bf(const float* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint16_t* __restrict__ w1t,
+k_mlp_bf(const TA* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint16_t* __restrict__ w1t,
          int64_t ldw1, int N1, int sf1, const uint16_t* __restrict__ w2t, int64_t ldw2, int N2, int sf2,
          float* __restrict__ out, int64_t ldo) {
   constexpr int NT = 8, SB = 4;  // 128 columns, 128 k of resident W^T per GEMM
@@ -2804,22 +2818,36 @@ k_mlp_bf(const float* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint
   int64_t grp = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wv;
   // x pieces by buffer loads through a descriptor over the group's rows: a piece past K1 (or a row
   // past M) takes an out-of-range offset and reads zeros -- no branch around the loads, so nothing
-  // makes the compiler drain the next groups' loads in flight
-  const uint32_t row_bytes = static_cast<uint32_t>(ldx) * 4u;
+  // makes the compiler drain the next groups' loads in flight.  fp32 x: two 16-B pieces per step;
+  // bf16 x: one (held in xa[st][0]), its 4-B pairs past K1 zeroed by a select
+  constexpr bool XB = sizeof(TA) == 2;
+  const uint32_t row_bytes = static_cast<uint32_t>(ldx) * static_cast<uint32_t>(sizeof(TA));
   auto load_x = [&](int64_t gi, float4 (&xa)[SB][2]) __attribute__((always_inline)) {
     const int64_t row0 = gi * 16;
     const int64_t rows = max<int64_t>(0, min<int64_t>(16, M - row0));  // 0 past the last group: all zeros
     const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<float*>(x + row0 * ldx), 0, static_cast<int>(rows * row_bytes), 0x00020000);
+        const_cast<TA*>(x + row0 * ldx), 0, static_cast<int>(rows * row_bytes), 0x00020000);
     const uint32_t roff = static_cast<uint32_t>(r16) * row_bytes;
 #pragma unroll
-    for (int st = 0; st < SB; ++st)
+    for (int st = 0; st < SB; ++st) {
+      if constexpr (XB) {
+        const int k = 32 * st + 8 * g;
+        const uint32_t off = k < K1 ? roff + static_cast<uint32_t>(k) * 2u : 0x80000000u;
+        uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        v.x = k < K1 ? v.x : 0u;  // (K1 is even: a pair is wholly inside or past K1)
+        v.y = k + 2 < K1 ? v.y : 0u;
+        v.z = k + 4 < K1 ? v.z : 0u;
+        v.w = k + 6 < K1 ? v.w : 0u;
+        xa[st][0] = __builtin_bit_cast(float4, v);
+      } else {
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int k = 32 * st + 8 * g + 4 * h;
-        const uint32_t off = k < K1 ? roff + static_cast<uint32_t>(k) * 4u : 0x80000000u;
-        xa[st][h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        for (int h = 0; h < 2; ++h) {
+          const int k = 32 * st + 8 * g + 4 * h;
+          const uint32_t off = k < K1 ? roff + static_cast<uint32_t>(k) * 4u : 0x80000000u;
+          xa[st][h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+        }
       }
+    }
   };
   auto sf_acc = [&](f32x4 (&acc)[1][NT], int sfc, auto tag) __attribute__((always_inline)) {
     constexpr int K = decltype(tag)::value;
@@ -2845,7 +2873,10 @@ k_mlp_bf(const float* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint
 #pragma unroll
     for (int st = 0; st < SB; ++st) {
       if (32 * st >= K1) break;  // (wave-uniform)
-      bf16x8 a8;  // x rounded to bf16 (RNE) as k_mm_ring_bf rounds it
+      bf16x8 a8;  // x rounded to bf16 (RNE) as k_mm_ring_bf rounds it (a bf16 x: its own bits)
+      if constexpr (XB) {
+        a8 = __builtin_bit_cast(bf16x8, xa[st][0]);
+      } else {
       a8[0] = static_cast<short>(to_bf16_bits(xa[st][0].x));
       a8[1] = static_cast<short>(to_bf16_bits(xa[st][0].y));
       a8[2] = static_cast<short>(to_bf16_bits(xa[st][0].z));
@@ -2854,6 +2885,7 @@ k_mlp_bf(const float* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint
       a8[5] = static_cast<short>(to_bf16_bits(xa[st][1].y));
       a8[6] = static_cast<short>(to_bf16_bits(xa[st][1].z));
       a8[7] = static_cast<short>(to_bf16_bits(xa[st][1].w));
+      }
       f32x4 b4[NT];
 #pragma unroll
       for (int c = 0; c < NT; ++c) ds_read16_kib(b4[c], wbase, c * SB + st);
@@ -3049,6 +3081,7 @@ struct AggArgs {
   const float* w; int64_t ldw; int gsz;
   const float* row_scale; float* y; int64_t ldy; int accumulate; float* partial;
   const void* xs; int64_t ldxs; const float* self_scale;  // gta_aggregate_self's term (xs: x's dtype)
+  int y_bf16;                                            // y stored as bf16 (gta_aggregate_self, y_dtype)
 };
 
 template <int LPE, int VW, int NV, int XM, int WM, typename TX>
@@ -3057,7 +3090,7 @@ void launch_agg(const AggArgs& a, int64_t n_items_bound, hipStream_t s) {
   k_aggregate<LPE, VW, NV, XM, WM, TX><<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
       a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, a.x_is_row, static_cast<const TX*>(a.x), a.ldx, a.F,
       a.w, a.ldw, a.gsz, a.row_scale, a.y, a.ldy, a.accumulate, a.partial, static_cast<const TX*>(a.xs), a.ldxs,
-      a.self_scale);
+      a.self_scale, a.y_bf16);
 }
 
 // (non-temporal index/weight loads measured +3 %: plain loads throughout)
@@ -3280,9 +3313,10 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
                    const void* x, int64_t ldx, int64_t F, int x_dtype, const float* w, int64_t ldw, int64_t heads,
                    const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
                    int64_t plan_chunk, void* workspace, void* stream, const void* xs, int64_t ldxs,
-                   const float* self_scale) {
+                   const float* self_scale, int y_bf16 = 0) {
   const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n_rows < 0 || nnz < 0 || F <= 0) return fail(GTA_ERR_ARG, "aggregate: bad sizes");
+  if (y_bf16 && (accumulate || ldy < F)) return fail(GTA_ERR_ARG, "aggregate: a bf16 y takes no accumulate; ldy >= F");
   if (xs && (accumulate || ldxs < F)) return fail(GTA_ERR_ARG, "aggregate_self: no accumulate; ld_self >= F");
   if (x_mode != GTA_IDX_EDGE && x_mode != GTA_IDX_SRC && x_mode != GTA_IDX_DST)
     return fail(GTA_ERR_ARG, "aggregate: bad x_mode");
@@ -3309,7 +3343,7 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
   const int xm = (x_mode == GTA_IDX_EDGE) ? XM_EDGE : XM_IDX;
   // widest vector that keeps every access aligned
   auto ok_vw = [&](int vw) {
-    if (F % vw || ldx % vw || ldy % vw || !aligned(x, xe * vw) || !aligned(y, 4 * vw)) return false;
+    if (F % vw || ldx % vw || ldy % vw || !aligned(x, xe * vw) || !aligned(y, (y_bf16 ? 2 : 4) * vw)) return false;
     if (xs && (ldxs % vw || !aligned(xs, xe * vw))) return false;
     if (wm == WM_HEAD && gsz % vw) return false;
     if (wm == WM_FULL && (ldw % vw || !aligned(w, 4 * vw))) return false;
@@ -3339,7 +3373,7 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
   a.x = x; a.ldx = ldx; a.F = static_cast<int>(F); a.w = w; a.ldw = ldw; a.gsz = gsz;
   a.row_scale = row_scale; a.y = y; a.ldy = ldy; a.accumulate = accumulate;
   a.partial = static_cast<float*>(workspace);
-  a.xs = xs; a.ldxs = ldxs; a.self_scale = self_scale;
+  a.xs = xs; a.ldxs = ldxs; a.self_scale = self_scale; a.y_bf16 = y_bf16;
   int64_t bound = n_rows;
   if (plan) {
     if (plan_chunk <= 0 || !workspace) return fail(GTA_ERR_ARG, "aggregate: plan needs chunk and workspace");
@@ -3350,7 +3384,7 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
   bool ok = false;
   // lean path: one edge per instruction exactly filling the wave, SpMM form
   int gl = (wm == WM_HEAD) ? gsz / vw : 0;
-  const bool lean_shape = !bf && tuning().agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
+  const bool lean_shape = !bf && !y_bf16 && tuning().agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
                           !a.x_is_row && wm != WM_FULL && (wm == WM_NONE || gl == 4 || gl == 8 || gl == 16);
   if (lean_shape) {
     const int64_t blocks = (bound + kWavesPerBlock - 1) / kWavesPerBlock;
@@ -3382,7 +3416,7 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
     if (sb > 0) {
       const int64_t blocks = (sb + kWavesPerBlock - 1) / kWavesPerBlock;
       k_aggregate_combine<<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
-          a.plan, a.F, row_scale, y, ldy, accumulate, a.partial, xs, ldxs, bf ? 1 : 0, self_scale);
+          a.plan, a.F, row_scale, y, ldy, accumulate, a.partial, xs, ldxs, bf ? 1 : 0, self_scale, y_bf16);
       GTA_LAUNCHED("k_aggregate_combine");
     }
   }
@@ -3401,11 +3435,13 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
 
 int gta_aggregate_self(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int x_mode,
                        const void* x, int64_t ldx, int64_t F, int x_dtype, const float* w, int64_t ldw, int64_t heads,
-                       const float* row_scale, const void* x_self, int64_t ld_self, const float* self_scale, float* y,
-                       int64_t ldy, const void* plan, int64_t plan_chunk, void* workspace, void* stream) {
+                       const float* row_scale, const void* x_self, int64_t ld_self, const float* self_scale, void* y,
+                       int64_t ldy, int y_dtype, const void* plan, int64_t plan_chunk, void* workspace, void* stream) {
   if (!x_self) return fail(GTA_ERR_ARG, "aggregate_self: x_self is NULL");
-  return aggregate_impl(indptr, indices, n_rows, nnz, x_mode, x, ldx, F, x_dtype, w, ldw, heads, row_scale, y, ldy, 0,
-                        plan, plan_chunk, workspace, stream, x_self, ld_self, self_scale);
+  if (y_dtype != GTA_F32 && y_dtype != GTA_BF16) return fail(GTA_ERR_ARG, "aggregate_self: y_dtype must be F32 or BF16");
+  return aggregate_impl(indptr, indices, n_rows, nnz, x_mode, x, ldx, F, x_dtype, w, ldw, heads, row_scale,
+                        static_cast<float*>(y), ldy, 0, plan, plan_chunk, workspace, stream, x_self, ld_self, self_scale,
+                        y_dtype == GTA_BF16 ? 1 : 0);
 }
 
 int64_t gta_aggregate_blocked_plan_bytes(int64_t n_rows, int64_t nnz, int64_t blocks, int64_t item_edges) {
@@ -3978,7 +4014,7 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   return GTA_OK;
 }
 
-int gta_update_mlp(const float* x, int64_t ldx, int64_t M, int64_t K1, const void* w1t, int64_t ldw1, int64_t N1,
+int gta_update_mlp(const void* x, int64_t ldx, int64_t M, int64_t K1, const void* w1t, int64_t ldw1, int64_t N1,
                    int sf1, const void* w2t, int64_t ldw2, int64_t N2, int sf2, int dtype, float* out, int64_t ldo,
                    void* stream) {
   const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
@@ -3986,9 +4022,11 @@ int gta_update_mlp(const float* x, int64_t ldx, int64_t M, int64_t K1, const voi
     return fail(GTA_ERR_ARG, "update_mlp: bad sizes");
   if (M == 0) return GTA_OK;
   if (!x || !w1t || !w2t || !out) return fail(GTA_ERR_ARG, "update_mlp: bad arguments");
-  if (dtype != GTA_F32_BF16) return fail(GTA_ERR_UNSUPPORTED, "update_mlp: fp32 x with bf16 weights only");
+  if (dtype != GTA_F32_BF16 && dtype != GTA_BF16)
+    return fail(GTA_ERR_UNSUPPORTED, "update_mlp: fp32 or bf16 x with bf16 weights only");
   if (K1 > 128 || N1 > 128 || N2 > 128) return fail(GTA_ERR_UNSUPPORTED, "update_mlp: K1, N1, N2 <= 128");
-  if (K1 % 4 || ldx % 4 || !aligned(x, 16) || ldx > (1 << 20))
+  const bool xb = dtype == GTA_BF16;
+  if (K1 % 4 || ldx % (xb ? 8 : 4) || !aligned(x, 16) || ldx > (1 << 20))
     return fail(GTA_ERR_UNSUPPORTED, "update_mlp: x rows 16-B aligned with K1 % 4 == 0");
   const int64_t n_groups = (M + 15) / 16;
   const int64_t blocks = std::max<int64_t>(1, std::min<int64_t>((n_groups + kWavesPerBlock - 1) / kWavesPerBlock, 512));
@@ -3997,8 +4035,14 @@ int gta_update_mlp(const float* x, int64_t ldx, int64_t M, int64_t K1, const voi
   const uint16_t* w2 = static_cast<const uint16_t*>(w2t);
   const int k1 = static_cast<int>(K1), n1 = static_cast<int>(N1), n2 = static_cast<int>(N2);
   const bool c1 = sf1 == GTA_SF_NONE || sf1 == GTA_SF_RELU, c2 = sf2 == GTA_SF_NONE || sf2 == GTA_SF_RELU;
-#define GTA_MLP(A_, B_) \
-  k_mlp_bf<A_, B_><<<gr, dim3(kBlock), 0, S(stream)>>>(x, ldx, M, k1, w1, ldw1, n1, sf1, w2, ldw2, n2, sf2, out, ldo)
+#define GTA_MLP(A_, B_)                                                                                          \
+  do {                                                                                                           \
+    if (xb) k_mlp_bf<A_, B_, uint16_t><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const uint16_t*>(x), ldx, M,  \
+                                                                        k1, w1, ldw1, n1, sf1, w2, ldw2, n2, sf2, \
+                                                                        out, ldo);                                \
+    else k_mlp_bf<A_, B_, float><<<gr, dim3(kBlock), 0, S(stream)>>>(static_cast<const float*>(x), ldx, M, k1, w1,    \
+                                                                     ldw1, n1, sf1, w2, ldw2, n2, sf2, out, ldo); \
+  } while (0)
   if (c1 && c2) {
     if (sf1 == GTA_SF_RELU) { if (sf2 == GTA_SF_RELU) GTA_MLP(GTA_SF_RELU, GTA_SF_RELU); else GTA_MLP(GTA_SF_RELU, GTA_SF_NONE); }
     else { if (sf2 == GTA_SF_RELU) GTA_MLP(GTA_SF_NONE, GTA_SF_RELU); else GTA_MLP(GTA_SF_NONE, GTA_SF_NONE); }

@@ -163,6 +163,7 @@ class Executor:
         self.fuse_sf = True
         #   fuse_mlp: MM -> SF -> MM -> SF chains of node GEMMs (GIN's MLP) as one gta_update_mlp launch
         self.fuse_mlp = FUSE_MLP
+        self.mlp_bf16_sum = MLP_BF16_SUM
         # weighted/unweighted SpMM aggregates whose gathered table exceeds the chip's L2
         # run column-blocked (L2-resident slices) when the shape allows it
         self.blocked_min_table_bytes = 32 << 20
@@ -413,10 +414,11 @@ class Executor:
             return None
         return xs[0].t, rows[0][1]
 
-    def _eval_gather_acc(self, A):
+    def _eval_gather_acc(self, A, out_dtype=torch.float32):
         """A = ADD(G, T) as G's aggregate accumulated into T's buffer; None if G's form cannot
         accumulate (then A runs unfused).  When T = x * s (a scalar) and T was left unformed, the
-        aggregate forms it in its epilogue instead (no [N, F] T written and read back)."""
+        aggregate forms it in its epilogue instead (no [N, F] T written and read back); only that
+        form takes out_dtype bf16 (A stored rounded, for the fused MLP that reads it)."""
         G, slot_t, T = self.gacc[A.idx]
         raw = self.values.get(G)
         if not (isinstance(raw, Lazy) and raw.v is None):
@@ -424,9 +426,11 @@ class Executor:
         tv = self.values.get(T)
         if isinstance(tv, Lazy) and tv.v is None:
             st = self._self_term(self.g.ops[T])
-            y = self._eval_gather(self.g.ops[G], self_term=st) if st is not None else None
+            y = self._eval_gather(self.g.ops[G], self_term=st, out_dtype=out_dtype) if st is not None else None
             if y is not None:
                 return y  # T stays unformed: recomputed by its own kernel if something reads it
+        if out_dtype != torch.float32:
+            return None
         t = self._source(A, slot_t)
         if not isinstance(t, NodeT) or t.t.dtype != torch.float32 or not t.t.is_contiguous():
             return None
@@ -713,8 +717,9 @@ class Executor:
             x = x.float()
         return x, W
 
-    def _eval_gather(self, op, acc=None, self_term=None):
-        """self_term (x, s): y = x * s + the aggregate, or None if this gather's form cannot take it."""
+    def _eval_gather(self, op, acc=None, self_term=None, out_dtype=torch.float32):
+        """self_term (x, s): y = x * s + the aggregate, or None if this gather's form cannot take it;
+        out_dtype (self_term only): y's storage dtype."""
         if op.order != "R":
             raise NotImplementedError("gather ORDER C (to source) is not emitted by genGraphOP")
         src = self.g.inputs[op.idx][0]
@@ -730,13 +735,13 @@ class Executor:
                     pins = pins + ([self._wrap_ext(extra)] if extra is not None else [])
                 if len(pins) != 2:
                     return None
-                y = self._weighted_aggregate(pins[0], pins[1], self_term=self_term)
+                y = self._weighted_aggregate(pins[0], pins[1], self_term=self_term, out_dtype=out_dtype)
                 return None if y is None else NodeT(y)
             if isinstance(v, Scat):
-                y = self._spmm(v.t, v.mode, None, self_term=self_term)
+                y = self._spmm(v.t, v.mode, None, self_term=self_term, out_dtype=out_dtype)
                 if y is not None:
                     n, E = self.graph.n_rows, self.graph.nnz
-                    self._count(E * (4 + v.t.shape[1] * v.t.element_size()) + n * (8 + v.t.shape[1] * 4))
+                    self._count(E * (4 + v.t.shape[1] * v.t.element_size()) + n * (8 + v.t.shape[1] * y.element_size()))
                     return NodeT(y)
             return None
         if self.fuse_attention and src.kind == "op" and src.op in self.attn:
@@ -782,7 +787,7 @@ class Executor:
     def _plan(self):
         return self.plan_chunk if self.plan_chunk else None
 
-    def _weighted_aggregate(self, u, v, acc=None, self_term=None):
+    def _weighted_aggregate(self, u, v, acc=None, self_term=None, out_dtype=torch.float32):
         """sum_e u(e) (.) v(e): the wider operand is the feature row, the narrower the (head) weight.
         self_term: see _eval_gather (None back if this form cannot take it)."""
         n, E = self.graph.n_rows, self.graph.nnz
@@ -805,13 +810,13 @@ class Executor:
             xt, mode = self._to_edge_tensor(x), "edge"
         if xt.shape[1] % wt.shape[1]:
             raise ValueError(f"weighted aggregate: weight width {wt.shape[1]} does not divide {xt.shape[1]}")
-        y = self._spmm(xt, mode, wt, acc, self_term)
+        y = self._spmm(xt, mode, wt, acc, self_term, out_dtype)
         if y is None:
             return None
-        self._count(E * (4 + 4 * wt.shape[1] + xt.element_size() * xt.shape[1]) + n * (8 + 4 * xt.shape[1]))
+        self._count(E * (4 + 4 * wt.shape[1] + xt.element_size() * xt.shape[1]) + n * (8 + y.element_size() * xt.shape[1]))
         return y
 
-    def _spmm(self, xt, mode, wt, acc=None, self_term=None):
+    def _spmm(self, xt, mode, wt, acc=None, self_term=None, out_dtype=torch.float32):
         """SpMM-form aggregate: column-blocked when the gathered table outgrows L2, else row-chunked.
         self_term (x, s): y = x * s + the aggregate in one launch (row-chunked form; None back when
         x's dtype is not the gathered table's, or when the column-blocked form is the better one:
@@ -821,7 +826,7 @@ class Executor:
             xs, sc = self_term
             if B or xs.dtype != xt.dtype or xs.shape[1] != xt.shape[1] or xs.shape[0] < self.graph.n_rows:
                 return None
-            return ops.aggregate(self.graph, xt, mode, wt, plan=self._plan(), self_term=(xs, sc))
+            return ops.aggregate(self.graph, xt, mode, wt, plan=self._plan(), self_term=(xs, sc), out_dtype=out_dtype)
         if B:
             return ops.aggregate_blocked(self.graph, xt, wt, out=acc, accumulate=acc is not None, blocks=B)
         return ops.aggregate(self.graph, xt, mode, wt, out=acc, accumulate=acc is not None, plan=self._plan())
@@ -926,7 +931,7 @@ class Executor:
             c = fused_into.get(op.idx)
             if c is not None and self.g.ops[c].type == "gather" and op.comp in ("MUL", "MM"):
                 return Deferred(op.idx)
-        if self.fuse_mlp and op.type == "applynode" and op.comp == "MM":
+        if op.type == "applynode" and op.comp == "MM":
             v = self._eval_mlp(op)
             if v is not None:
                 return v
@@ -949,6 +954,8 @@ class Executor:
                 return v
             return self._gather_value(op)
         if op.type == "applynode":
+            if self.mlp_bf16_sum and self.gather_acc and op.idx in self.gacc and self._mlp_input(op) is not None:
+                return Lazy(lambda: self._eval_applynode(op))  # the MLP it feeds may take it in bf16
             if self.gather_acc and op.idx in self.gacc_t and self._self_term(op) is not None:
                 return Lazy(lambda: self._eval_applynode(op))  # its ADD consumer's aggregate may form it
             return self._eval_applynode(op)
@@ -987,28 +994,53 @@ class Executor:
             return None
         return c
 
-    def _eval_mlp(self, a):
-        """Two chained node GEMMs a -> [SF b] -> MM c -> [SF d] (GIN's MLP, genGraphOP.py:103-108),
-        each intermediate read only by the next op, as one gta_update_mlp launch when the shapes
-        allow it (fp32 x, bf16 weights, widths <= 128).  The chain's last value is set; a, b and c
-        stay available, recomputed unfused if something reads them (the tests read them all).
-        None when the chain or its operands do not fit."""
+    def _mlp_chain(self, a):
+        """(b, c, d) of a chain a -> [SF b] -> MM c -> [SF d] of node GEMMs, each intermediate read
+        only by the next op, with weights gta_update_mlp takes; else None."""
+        if not (self.fuse_mlp and a.type == "applynode" and a.comp == "MM" and len(self.g.inputs[a.idx]) == 1):
+            return None
         b = self._only_consumer(a, "SF") if self.fuse_sf else None
         c = self._only_consumer(b if b is not None else a, "MM")
         if c is None:
             return None
         d = self._only_consumer(c, "SF") if self.fuse_sf else None
-        ins = self._inputs(a)
-        if len(ins) != 1:
-            return None
-        x = self._node(ins[0])
         w1, w2 = self.tensors[f"w:{a.idx}"], self.tensors[f"w:{c.idx}"]
-        if not ops.update_mlp_supported(x, w1, w2):
+        return (b, c, d) if ops.update_mlp_weights_ok(w1.shape[0], w1, w2) else None
+
+    def _mlp_input(self, A):
+        """The MLP head a when node op A's only consumer heads a fusable MLP chain, else None."""
+        a = self._only_consumer(A, "MM")
+        return a if a is not None and self._mlp_chain(a) is not None else None
+
+    def _eval_mlp(self, a):
+        """Two chained node GEMMs a -> [SF b] -> MM c -> [SF d] (GIN's MLP, genGraphOP.py:103-108)
+        as one gta_update_mlp launch when the shapes allow it (fp32 or bf16 x, bf16 weights, widths
+        <= 128).  When a's input is the still-unformed GIN sum A = (1 + eps) x + aggregate, the
+        aggregate stores A in bf16 (ABI 10): the MLP rounds an fp32 x to bf16 anyway, so the bits
+        are unchanged and A's [N, F] write and read halve.  The chain's last value is set; A, a, b
+        and c stay available, recomputed unfused (fp32) if something reads them (the tests read
+        them all).  None when the chain or its operands do not fit."""
+        chain = self._mlp_chain(a)
+        if chain is None:
             return None
+        b, c, d = chain
+        w1, w2 = self.tensors[f"w:{a.idx}"], self.tensors[f"w:{c.idx}"]
+        x = None
+        src = self.g.inputs[a.idx][0]
+        if self.mlp_bf16_sum and self.gather_acc and src.kind == "op" and src.op in self.gacc:
+            raw = self.values.get(src.op)
+            if isinstance(raw, Lazy) and raw.v is None:
+                y = self._eval_gather_acc(self.g.ops[src.op], out_dtype=torch.bfloat16)
+                if y is not None and ops.update_mlp_supported(y.t, w1, w2):
+                    x = y.t
+        if x is None:
+            x = self._node(self._inputs(a)[0])
+            if not ops.update_mlp_supported(x, w1, w2):
+                return None
         sf1 = self.sem.sf_of(b) if b is not None else None
         sf2 = self.sem.sf_of(d) if d is not None else None
         out = ops.update_mlp(x, w1, w2, sf1=sf1, sf2=sf2)
-        self._count(x.shape[0] * (x.shape[1] * 4 + w2.shape[1] * 4) + w1.numel() * 2 + w2.numel() * 2)
+        self._count(x.shape[0] * (x.shape[1] * x.element_size() + w2.shape[1] * 4) + w1.numel() * 2 + w2.numel() * 2)
         self.values[(d if d is not None else c).idx] = NodeT(out)
         if d is not None:
             self.values[c.idx] = Lazy(lambda: self._eval_applynode(c))
@@ -1176,6 +1208,7 @@ def aggregate_trace(events):
 # shape, stride), the calling thread's libgta knob state (ops.knob_state) and stays eager on a stream with an attached
 # knob set; weights changed in place are re-transposed into the graph's W^T before the replay.
 FUSE_MLP = True  # default of Executor.fuse_mlp (layer benches A/B it)
+MLP_BF16_SUM = True  # default of Executor.mlp_bf16_sum: GIN's sum stored in bf16 for the fused MLP (ABI 10)
 AUTO_GRAPH = True
 AUTO_GRAPH_MAX_EDGES = 1 << 40  # every graph (round 3: 1 << 23, launch-bound layers only)
 AUTO_GRAPH_MAX_ENTRIES = 32

@@ -95,13 +95,17 @@ class AggregatePlan:
         return int(self.buf[8:16].view(torch.int64).item())
 
 
-def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumulate=False, plan=None, self_term=None):
+def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumulate=False, plan=None, self_term=None,
+              out_dtype=torch.float32):
     """y[i] (+)= row_scale[i] * sum_{e in row i} w(e) * x[idx(e)]  (K6/K7/K2).
 
     self_term: None, or (x_self, s): y[i] = x_self[i] * s + row_scale[i] * sum (gta_aggregate_self,
     no accumulate; x_self [>= N, F] of x's dtype, s a one-element float32 device tensor) -- without
     row_scale bitwise apply_node("MUL", x_self, s) followed by the accumulating aggregate (GIN ops
     3-4); with row_scale the scaled sum is rounded before the add.
+    out_dtype: torch.bfloat16 (self_term only, ABI 10) stores y rounded to bf16 (round to nearest
+    even, the rounding the fused MLP applies to an fp32 x); a fresh out is then a [N, F] view of
+    [N, ceil8(F)] rows (16-B aligned, what gta_update_mlp reads).
 
     x_mode: "src" (x is [N_src, F], fused scatter C), "dst" (fused scatter R),
             "edge" (x is an edge tensor [E, F]).  x float32, or bfloat16 for "src" / "dst" with
@@ -132,9 +136,14 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
     if row_scale is not None and (row_scale.dtype != torch.float32 or row_scale.numel() < graph.n_rows
                                   or not row_scale.is_contiguous()):
         raise ValueError("row_scale must be contiguous float32 [N]")
+    if out_dtype not in (torch.float32, torch.bfloat16) or out_dtype == torch.bfloat16 and self_term is None:
+        raise ValueError("aggregate: a bfloat16 out is written by the self-term form only")
     if out is None:
-        out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=x.device)
-    ldy = _rows(out, "out")
+        if out_dtype == torch.bfloat16:
+            out = torch.empty(graph.n_rows, (F + 7) // 8 * 8, dtype=out_dtype, device=x.device)[:, :F]
+        else:
+            out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=x.device)
+    ldy = _rows(out, "out", out_dtype)
     if out.shape[0] < graph.n_rows or out.shape[1] != F:
         raise ValueError("out must be [N, F]")
     if graph.n_rows == 0:
@@ -159,7 +168,9 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
         ldxs = _rows(xs, "x_self", xs.dtype)
         check(_L().gta_aggregate_self(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz, _MODES[x_mode],
                                       _ptr(x), ldx, F, x_dt, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(xs), ldxs,
-                                      _ptr(sc.contiguous()), _ptr(out), ldy, _ptr(pbuf), chunk, _ptr(ws),
+                                      _ptr(sc.contiguous()), _ptr(out), ldy,
+                                      _lib.GTA_BF16 if out_dtype == torch.bfloat16 else _lib.GTA_F32,
+                                      _ptr(pbuf), chunk, _ptr(ws),
                                       _stream(x.device)), "aggregate_self")
         return out
     check(_L().gta_aggregate(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz, _MODES[x_mode],
@@ -277,9 +288,14 @@ def aggregate_blocked(graph, x, w=None, row_scale=None, out=None, accumulate=Fal
         plan = graph.blocked_plan(blocks)
     if not plan.sorted:
         raise ValueError("aggregate_blocked needs every CSR row's columns sorted")
+    if out_dtype not in (torch.float32, torch.bfloat16) or out_dtype == torch.bfloat16 and self_term is None:
+        raise ValueError("aggregate: a bfloat16 out is written by the self-term form only")
     if out is None:
-        out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=x.device)
-    ldy = _rows(out, "out")
+        if out_dtype == torch.bfloat16:
+            out = torch.empty(graph.n_rows, (F + 7) // 8 * 8, dtype=out_dtype, device=x.device)[:, :F]
+        else:
+            out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=x.device)
+    ldy = _rows(out, "out", out_dtype)
     ws = plan.workspace(F) if single_launch else None
     check(_L().gta_aggregate_blocked(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols, graph.nnz,
                                      _ptr(x), ldx, F, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy,
@@ -485,22 +501,31 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
     return out
 
 
+def update_mlp_weights_ok(K1, w1, w2):
+    """The weight half of update_mlp_supported: bf16 W1 [K1, N1] and W2 [N1, N2], K1 % 4 == 0,
+    K1, N1, N2 <= 128."""
+    return (w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16 and w1.dim() == 2 and w2.dim() == 2
+            and K1 == w1.shape[0] and w1.shape[1] == w2.shape[0] and K1 % 4 == 0
+            and max(K1, w1.shape[1], w2.shape[1]) <= 128)
+
+
 def update_mlp_supported(x, w1, w2):
-    """Shapes gta_update_mlp takes: fp32 x [M, K1] with unit column stride and 16-B aligned rows,
-    K1 % 4 == 0, bf16 W1 [K1, N1] and W2 [N1, N2], K1, N1, N2 <= 128."""
-    return (x.dtype == torch.float32 and x.dim() == 2 and w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16
-            and w1.dim() == 2 and w2.dim() == 2 and x.shape[1] == w1.shape[0] and w1.shape[1] == w2.shape[0]
-            and max(w1.shape[0], w1.shape[1], w2.shape[1]) <= 128 and (x.shape[0] <= 1 or x.stride(1) == 1)
-            and x.shape[1] % 4 == 0 and (x.shape[0] <= 1 or x.stride(0) % 4 == 0) and x.data_ptr() % 16 == 0)
+    """Shapes gta_update_mlp takes: fp32 or bf16 x [M, K1] with unit column stride and 16-B aligned
+    rows, K1 % 4 == 0, bf16 W1 [K1, N1] and W2 [N1, N2], K1, N1, N2 <= 128."""
+    row_elems = 8 if x.dtype == torch.bfloat16 else 4
+    return (x.dtype in (torch.float32, torch.bfloat16) and x.dim() == 2 and update_mlp_weights_ok(x.shape[1], w1, w2)
+            and (x.shape[0] <= 1 or x.stride(1) == 1) and (x.shape[0] <= 1 or x.stride(0) % row_elems == 0)
+            and x.data_ptr() % 16 == 0)
 
 
 def update_mlp(x, w1, w2, sf1=None, sf2=None, out=None):
     """out = sf2(bf16(sf1(x W1)) W2) in one launch (gta_update_mlp: GIN's MM -> SF -> MM -> SF,
     genGraphOP.py:103-108), bitwise equal to update_mm(update_mm(x, w1, sf=sf1), w2, sf=sf2) with
-    fp32 x and bf16 weights, without the [M, N1] intermediate in HBM."""
+    fp32 x and bf16 weights, without the [M, N1] intermediate in HBM.  A bf16 x (ABI 10) gives the
+    same bits as the fp32 x it was rounded from: the kernel rounds an fp32 x to bf16 on load."""
     _need_gpu(x, w1, w2, out)
     if not update_mlp_supported(x, w1, w2):
-        raise ValueError("update_mlp: fp32 x [M, K1], bf16 W1 [K1, N1], bf16 W2 [N1, N2], K1, N1, N2 <= 128")
+        raise ValueError("update_mlp: fp32 / bf16 x [M, K1], bf16 W1 [K1, N1], bf16 W2 [N1, N2], K1, N1, N2 <= 128")
     M, K1 = x.shape
     N1, N2 = w1.shape[1], w2.shape[1]
     w1t, w2t = _transposed(w1), _transposed(w2)
@@ -508,8 +533,9 @@ def update_mlp(x, w1, w2, sf1=None, sf2=None, out=None):
         out = torch.empty(M, N2, dtype=torch.float32, device=x.device)
     if out.shape[0] < M or out.shape[1] != N2:
         raise ValueError("update_mlp: out must be [M, N2]")
-    check(_L().gta_update_mlp(_ptr(x), _rows(x, "x"), M, K1, _ptr(w1t), _rows(w1t, "w1^T", torch.bfloat16), N1, _sf(sf1),
-                              _ptr(w2t), _rows(w2t, "w2^T", torch.bfloat16), N2, _sf(sf2), _lib.GTA_F32_BF16,
+    xb = x.dtype == torch.bfloat16
+    check(_L().gta_update_mlp(_ptr(x), _rows(x, "x", x.dtype), M, K1, _ptr(w1t), _rows(w1t, "w1^T", torch.bfloat16), N1, _sf(sf1),
+                              _ptr(w2t), _rows(w2t, "w2^T", torch.bfloat16), N2, _sf(sf2), _lib.GTA_BF16 if xb else _lib.GTA_F32_BF16,
                               _ptr(out), _rows(out, "out"), _stream(x.device)), "update_mlp")
     return out
 

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 9  /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+#define GTA_ABI_VERSION 10 /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
                               hooks; 4: knob sets attached to streams (gta_tuning_*); 5: every UPDATE
                               on hand-written kernels (no vendor library), gta_update_mm_t_splits,
                               the blocked workspace is the slab rows alone and required, bf16
@@ -45,7 +45,8 @@ extern "C" {
                               6: gta_gat_aggregate_blocked's sf_out (an SF applied to y); 7:
                               gta_aggregate_self (the aggregate with a scaled self term); 8:
                               gta_update_mm_t_splits takes the stream (its attached knob set); 9:
-                              gta_update_mlp (two chained node GEMMs in one pass) */
+                              gta_update_mlp (two chained node GEMMs in one pass); 10: bf16 y of
+                              gta_aggregate_self, bf16 x of gta_update_mlp */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -144,11 +145,14 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
  * (no fma contraction): with row_scale NULL, bitwise equal to gta_apply_node(MUL, x_self, s) into y
  * then gta_aggregate accumulating into y; with row_scale, the scaled sum is rounded before the add
  * (the unfused scaled aggregate, then ADD).  GIN ops 3-4
- * (genGraphOP.py:99-103): agg + (1 + eps) x with no [N, F] intermediate. */
+ * (genGraphOP.py:99-103): agg + (1 + eps) x with no [N, F] intermediate.
+ * y_dtype (ABI 10): GTA_F32, or GTA_BF16 -- y holds the RNE bf16 rounding of the fp32 value (ldy in
+ * bf16 elements), for a consumer that rounds its input to bf16 anyway (gta_update_mlp: GIN's MLP
+ * after ops 3-4), so half the bytes are written and read and the value it sees is unchanged. */
 int gta_aggregate_self(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int x_mode,
                        const void* x, int64_t ldx, int64_t F, int x_dtype, const float* w, int64_t ldw, int64_t heads,
-                       const float* row_scale, const void* x_self, int64_t ld_self, const float* self_scale, float* y,
-                       int64_t ldy, const void* plan, int64_t plan_chunk, void* workspace, void* stream);
+                       const float* row_scale, const void* x_self, int64_t ld_self, const float* self_scale, void* y,
+                       int64_t ldy, int y_dtype, const void* plan, int64_t plan_chunk, void* workspace, void* stream);
 
 /* plan/workspace sizing: chunk must be a positive multiple of 64 */
 int64_t gta_aggregate_plan_bytes(int64_t n_rows, int64_t nnz, int64_t chunk);
@@ -295,11 +299,13 @@ int64_t gta_update_mm_t_split_workspace_bytes(int64_t M, int64_t K, int64_t N, i
  * MM -> SF -> MM -> SF; replaces two gta_update_mm_t calls and the [M, N1] intermediate they pass
  * through HBM): out = sf2(bf16(sf1(x W1)) W2).  x fp32 [M, K1] (rounded to bf16, RNE, as
  * GTA_F32_BF16 rounds it; rows 16-B aligned, K1 % 4 == 0), w1t = W1^T bf16 [N1][ldw1], w2t = W2^T bf16
- * [N2][ldw2]; K1, N1, N2 <= 128; dtype must be GTA_F32_BF16 (GTA_ERR_UNSUPPORTED otherwise).  The intermediate is rounded to bf16 (RNE) exactly as the second
+ * [N2][ldw2]; K1, N1, N2 <= 128; dtype GTA_F32_BF16, or (ABI 10) GTA_BF16 for a bf16 x (ldx % 8 == 0,
+ * 16-B aligned rows): then x is used as it is, and a bf16 x equal to the RNE rounding of an fp32 x
+ * gives bitwise the fp32 call's result.  Other dtypes: GTA_ERR_UNSUPPORTED.  The intermediate is rounded to bf16 (RNE) exactly as the second
  * unfused GEMM's staging rounds its fp32 input, and both products run the unfused kernels' k order:
  * bitwise equal to gta_update_mm_t(x, W1, sf1) followed by gta_update_mm_t(z, W2, sf2).
  * Reference: the two COMP_MM of interpreter.py's lowering (code/interpreter.py:335-343). */
-int gta_update_mlp(const float* x, int64_t ldx, int64_t M, int64_t K1, const void* w1t, int64_t ldw1, int64_t N1,
+int gta_update_mlp(const void* x, int64_t ldx, int64_t M, int64_t K1, const void* w1t, int64_t ldw1, int64_t N1,
                    int sf1, const void* w2t, int64_t ldw2, int64_t N2, int sf2, int dtype, float* out, int64_t ldo,
                    void* stream);
 int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M, int64_t K, const void* wt,

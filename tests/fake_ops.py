@@ -18,15 +18,27 @@ def _t(a):
 
 
 SELF_TERM_CALLS = [0]  # aggregates that formed a self term (the executor's GIN ops 3-4 fusion)
+BF16_OUT_CALLS = [0]   # of those, the ones that stored y in bf16 (the handoff to the fused MLP)
+# bf16 aggregate outputs -> the unrounded values: the real fused MLP rounds an fp32 x to bf16 on
+# load, so MLP(bf16(y)) is bitwise MLP(y); the fp64 stand-in models it by reading y itself
+_BF16_EXACT = {}
 
 
-def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumulate=False, plan=None, self_term=None):
+def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumulate=False, plan=None, self_term=None,
+              out_dtype=torch.float32):
     ip, ix = graph.numpy()
     y = isa_ref.aggregate(ip, ix, _np(x), x_mode, _np(w), _np(row_scale))
     if self_term is not None:
         SELF_TERM_CALLS[0] += 1
         xs, sc = self_term
         y = _np(xs)[:graph.n_rows] * float(_np(sc).reshape(-1)[0]) + y
+        if out_dtype == torch.bfloat16:
+            BF16_OUT_CALLS[0] += 1
+            yb = _t(y).to(torch.bfloat16)
+            _BF16_EXACT[yb.data_ptr()] = (yb, _t(y))
+            return yb
+    elif out_dtype != torch.float32:
+        raise ValueError("aggregate: a bfloat16 out is written by the self-term form only")
     if out is not None:
         y = y + (_np(out) if accumulate else 0)
         out.copy_(_t(y))
@@ -101,15 +113,21 @@ def update_mm(x, w, row_idx=None, sf=None, out=None, m=None):
 MLP_CALLS = [0]  # fused MM -> SF -> MM -> SF launches (the executor's GIN MLP fusion)
 
 
-def update_mlp_supported(x, w1, w2):
-    return (x.dtype == torch.float32 and w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16
+def update_mlp_weights_ok(K1, w1, w2):
+    return (w1.dtype == torch.bfloat16 and w2.dtype == torch.bfloat16 and K1 == w1.shape[0]
             and max(w1.shape[0], w1.shape[1], w2.shape[1]) <= 128)
+
+
+def update_mlp_supported(x, w1, w2):
+    return x.dtype in (torch.float32, torch.bfloat16) and update_mlp_weights_ok(x.shape[1], w1, w2)
 
 
 def update_mlp(x, w1, w2, sf1=None, sf2=None, out=None):
     """The two products in fp64, as this module's update_mm computes each (the bf16 rounding of the
     real kernel is the GPU tests' business)."""
     MLP_CALLS[0] += 1
+    if x.dtype == torch.bfloat16:
+        x = _BF16_EXACT[x.data_ptr()][1]
     return _t(isa_ref.mm(isa_ref.mm(_np(x), _np(w1), None, sf1), _np(w2), None, sf2))
 
 

@@ -392,6 +392,49 @@ def test_gin_bf16_model_input_on_gpu(golden_dir, manifest, cora, dev):
     assert SampledChecker(ex, ip, ix).check(n_samples=400, seed=3)
 
 
+@pytest.mark.parametrize("layer", ["layer2", "layer3"])
+@pytest.mark.parametrize("dtype_x", [torch.float32, torch.bfloat16])
+def test_gin_sum_reaches_fused_mlp_in_bf16(golden_dir, manifest, cora, dev, monkeypatch, layer, dtype_x):
+    """ABI 10: GIN's sum (1 + eps) x + aggregate, formed in one launch, is stored in bf16 when its only
+    reader is the fused MLP; the layer output is bitwise the unfused run's (the MLP's first GEMM
+    rounds an fp32 x to bf16 on load either way), and the sum itself, read afterwards, is the fp32
+    value (recomputed)."""
+    rec = [s for s in _all_streams(manifest) if s["network"] == "GIN" and not s["reorder"] and s["dataset"] == "cora"
+           and layer in s["file"]][0]
+    sem = Semantics.for_network("GIN", False)
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    ip, ix = cora
+    gd = G.from_numpy(ip, ix, device=dev)
+    tc = workloads.make_tensors(og, G.from_numpy(ip, ix), "GIN", seed=11, dtype_w=torch.bfloat16, dtype_x=dtype_x)
+    tensors = {k: v.to(dev) for k, v in tc.items()}
+    seen = []
+    real = executor.ops.aggregate
+
+    def spy(*a, **k):
+        y = real(*a, **k)
+        seen.append(y.dtype)
+        return y
+
+    monkeypatch.setattr(executor.ops, "aggregate", spy)
+    outs = {}
+    for fuse in (True, False):
+        seen.clear()
+        ex = executor.Executor(og, st, gd, tensors, sem)
+        ex.fuse_mlp = fuse
+        outs[fuse] = {k: v.clone() for k, v in ex.run().items()}
+        assert (torch.bfloat16 in seen) == fuse, seen
+        sums = {i: ex.tensor_of(i) for i in ex.gacc}
+        assert all(t.dtype == torch.float32 for t in sums.values())
+        if fuse:
+            fused_sums = sums
+        else:
+            for i, t in sums.items():
+                assert torch.equal(t, fused_sums[i]), i
+    for k in outs[False]:
+        assert torch.equal(outs[True][k], outs[False][k]), k
+
+
 def test_bf16_source_table_takes_the_row_chunked_aggregate(golden_dir, manifest, cora, dev):
     """a bf16 source table of a width the blocked kernels take (F = 128), above the
     blocked-form size gate, runs the bf16 row-chunked aggregate (the blocked kernels are fp32-only),

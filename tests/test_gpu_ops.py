@@ -1117,6 +1117,58 @@ def test_aggregate_self_term(dev, dt, F, heads, plan):
     assert torch.equal(got, want)
 
 
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("F,heads", [(100, 0), (128, 8), (36, 1)])
+@pytest.mark.parametrize("plan", [None, 64])
+def test_aggregate_self_term_bf16_out(dev, dt, F, heads, plan):
+    """ABI 10 bf16 y of gta_aggregate_self (the GIN sum handed to the fused MLP) == the fp32 y rounded
+    to nearest even, bitwise: per-row and split rows (the combine kernel's store), empty rows, F
+    not a multiple of 8 (the fresh [N, ceil8(F)] rows); the columns past F are never written."""
+    n, e = 500, 9000
+    g, ip, ix = _graph(n, e, seed=F + heads + 7, heavy_row=900, empty_rows=5, dev=dev)
+    rng = np.random.default_rng(F + 1)
+    tdt = torch.bfloat16 if dt == "bf16" else torch.float32
+    x = torch.from_numpy(rng.standard_normal((n, F)).astype(np.float32)).to(tdt).to(dev)
+    w = torch.from_numpy(rng.random((g.nnz, heads)).astype(np.float32)).to(dev) if heads else None
+    s = torch.tensor([[1.1]], device=dev)
+    want = ops.aggregate(g, x, "src", w, plan=plan, self_term=(x, s))
+    got = ops.aggregate(g, x, "src", w, plan=plan, self_term=(x, s), out_dtype=torch.bfloat16)
+    assert got.dtype == torch.bfloat16 and got.shape == (n, F) and got.stride(0) % 8 == 0
+    pad = torch.full((n, 48), 7.0, dtype=torch.bfloat16, device=dev)  # a caller's out with a guard band
+    got2 = ops.aggregate(g, x, "src", w, plan=plan, self_term=(x, s), out_dtype=torch.bfloat16,
+                         out=pad[:, :F] if F <= 40 else None)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want.to(torch.bfloat16))
+    assert torch.equal(got2, got)
+    if F <= 40:
+        assert bool((pad[:, F:] == 7.0).all())
+    with pytest.raises(ValueError):
+        ops.aggregate(g, x, "src", w, plan=plan, out_dtype=torch.bfloat16)  # no self term: fp32 only
+
+
+@pytest.mark.parametrize("M,K1,N1,N2,sf1,sf2", [(20000, 100, 128, 128, "RELU", "RELU"), (4099, 36, 64, 20, None, "ELU"),
+                                                (33, 128, 20, 8, "SIGMOID", None)])
+def test_update_mlp_bf16_x(dev, M, K1, N1, N2, sf1, sf2):
+    """ABI 10 bf16 x of gta_update_mlp (the aggregate's bf16 GIN sum) gives the bits of the fp32 x it
+    was rounded from (the kernel rounds an fp32 x to bf16 on load): one 16-B piece per step, the K
+    tail of a 36-wide row masked by 4-column pairs, rows padded to a multiple of 8."""
+    rng = np.random.default_rng(M + K1)
+    x = torch.from_numpy(rng.standard_normal((M, K1)).astype(np.float32)).to(dev)
+    w1 = torch.from_numpy((rng.standard_normal((K1, N1)) / np.sqrt(K1)).astype(np.float32)).to(torch.bfloat16).to(dev)
+    w2 = torch.from_numpy((rng.standard_normal((N1, N2)) / np.sqrt(N1)).astype(np.float32)).to(torch.bfloat16).to(dev)
+    ld = (K1 + 7) // 8 * 8
+    xbuf = torch.full((M, ld), float("nan"), dtype=torch.bfloat16, device=dev)  # NaN past K1: must not be read
+    xb = xbuf[:, :K1]
+    xb.copy_(x.to(torch.bfloat16))
+    assert ops.update_mlp_supported(xb, w1, w2)
+    want = ops.update_mlp(x, w1, w2, sf1=sf1, sf2=sf2)
+    got = ops.update_mlp(xb, w1, w2, sf1=sf1, sf2=sf2)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+    if K1 % 8:
+        assert not ops.update_mlp_supported(torch.empty(M, K1, dtype=torch.bfloat16, device=dev)[1:], w1, w2)
+
+
 @pytest.mark.parametrize("M,K1,N1,N2,sf1,sf2", [(20000, 100, 128, 128, "RELU", "RELU"), (4099, 128, 128, 128, None, "ELU"),
                                                 (3001, 64, 96, 48, "SIGMOID", None), (777, 100, 128, 100, "RELU", None),
                                                 (33, 36, 20, 8, "EXP", "RELU"), (5, 128, 128, 128, "RELU", "RELU")])

@@ -341,9 +341,13 @@ def test_mlp_chain_fusion_cpu(golden_dir, manifest, monkeypatch, layer):
     tensors = workloads.make_tensors(og, gc, "GIN", seed=9, dtype_w=torch.bfloat16)
     ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
     for fuse in (True, False):
-        calls = fake_ops.MLP_CALLS[0]
+        calls, st_calls, bf_calls = fake_ops.MLP_CALLS[0], fake_ops.SELF_TERM_CALLS[0], fake_ops.BF16_OUT_CALLS[0]
         ex = executor.Executor(og, st, gc, tensors, sem)
         ex.fuse_mlp = fuse
         ex.run()
         assert fake_ops.MLP_CALLS[0] == calls + (1 if fuse else 0)
+        # ABI 10: with the fusion, the GIN sum (op 4, formed with its self term) reaches the MLP
+        # in bf16 and no fp32 copy of it is made during the run; without it, no bf16 aggregate
+        n_self, n_bf = fake_ops.SELF_TERM_CALLS[0] - st_calls, fake_ops.BF16_OUT_CALLS[0] - bf_calls
+        assert n_bf == (n_self if fuse else 0) and (not fuse or n_self == 1), (fuse, n_self, n_bf)
         compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
