@@ -288,14 +288,9 @@ def aggregate_blocked(graph, x, w=None, row_scale=None, out=None, accumulate=Fal
         plan = graph.blocked_plan(blocks)
     if not plan.sorted:
         raise ValueError("aggregate_blocked needs every CSR row's columns sorted")
-    if out_dtype not in (torch.float32, torch.bfloat16) or out_dtype == torch.bfloat16 and self_term is None:
-        raise ValueError("aggregate: a bfloat16 out is written by the self-term form only")
     if out is None:
-        if out_dtype == torch.bfloat16:
-            out = torch.empty(graph.n_rows, (F + 7) // 8 * 8, dtype=out_dtype, device=x.device)[:, :F]
-        else:
-            out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=x.device)
-    ldy = _rows(out, "out", out_dtype)
+        out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=x.device)
+    ldy = _rows(out, "out")
     ws = plan.workspace(F) if single_launch else None
     check(_L().gta_aggregate_blocked(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols, graph.nnz,
                                      _ptr(x), ldx, F, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy,
