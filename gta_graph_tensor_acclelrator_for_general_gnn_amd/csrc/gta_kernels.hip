@@ -2202,6 +2202,61 @@ k_mm_rows(const TA* __restrict__ x, int64_t ldx, const int32_t* __restrict__ row
   }
 }
 
+// The accumulator tile of a (16 FR) x (16 NT) wave tile out as k_mm_rows / k_mm_ring store it:
+// the SF applied, then quad-transposed 16-B row stores (two DPP swaps per quad turn the lane's 4
+// rows of one column into 4 columns of one row) when out rows are 16-B aligned, else per element.
+template <int FR, int NT>
+__device__ __forceinline__ void store_tile(f32x4 (&acc)[FR][NT], int sf, float* __restrict__ out, int64_t ldo,
+                                           int64_t M, int N, int64_t mw, int n0, int lane, bool vstore) {
+  const int g = lane >> 4, r16 = lane & 15;
+  sf_tile(sf, acc);
+  if (vstore) {
+    const int p = r16 & 3, q = r16 >> 2;
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+      for (int c = 0; c < NT; ++c) {
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][c][r];
+#pragma unroll
+        for (int m2 = 0; m2 < 2; ++m2) {
+          const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
+          const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2 + 1]), 0xB1, 0xF, 0xF, false));
+          if (p & 1) v[2 * m2] = sb; else v[2 * m2 + 1] = sa;
+        }
+#pragma unroll
+        for (int m2 = 0; m2 < 2; ++m2) {
+          const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2]), 0x4E, 0xF, 0xF, false));
+          const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2 + 2]), 0x4E, 0xF, 0xF, false));
+          if (p & 2) v[m2] = sb; else v[m2 + 2] = sa;
+        }
+        const int64_t m = mw + 16 * i + 4 * g + p;
+        const int n = n0 + 16 * c + 4 * q;
+        if (m < M) {
+          if (n + 3 < N) {
+            *reinterpret_cast<float4*>(out + m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              if (n + r < N) out[m * ldo + n + r] = v[r];
+          }
+        }
+      }
+  } else {
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+      for (int c = 0; c < NT; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int64_t m = mw + 16 * i + 4 * g + r;
+          const int n = n0 + 16 * c + r16;
+          if (m < M && n < N) out[m * ldo + n] = acc[i][c][r];
+        }
+  }
+}
+
 // fp32 UPDATE on MFMA with an LDS-DMA ring (the plain fp32 GEMM of GCN/GAT/SAGE layers,
 // `template/ISA_defination.yaml:1-31` j,ij->i; LOAD_W `code/interpreter.py:335-343`).
 // Why not k_mm_rows: there each K chunk of W is staged synchronously (stage, barrier, compute)
@@ -2379,53 +2434,7 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   };
   const bool vstore = ldo % 4 == 0 && aligned(out, 16);
   auto epilogue = [&](int64_t j) __attribute__((always_inline)) {
-    const int64_t mw = (grp0 + j * gstep) * GR + wv * (16 * FR);
-    sf_tile(sf, acc);
-    if (vstore) {  // quad-transposed 16-B row stores (k_mm_rows' epilogue)
-      const int p = r16 & 3, q = r16 >> 2;
-#pragma unroll
-      for (int i = 0; i < FR; ++i)
-#pragma unroll
-        for (int c = 0; c < NT; ++c) {
-          float v[4];
-#pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = acc[i][c][r];
-#pragma unroll
-          for (int m2 = 0; m2 < 2; ++m2) {
-            const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
-            const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2 + 1]), 0xB1, 0xF, 0xF, false));
-            if (p & 1) v[2 * m2] = sb; else v[2 * m2 + 1] = sa;
-          }
-#pragma unroll
-          for (int m2 = 0; m2 < 2; ++m2) {
-            const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2]), 0x4E, 0xF, 0xF, false));
-            const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2 + 2]), 0x4E, 0xF, 0xF, false));
-            if (p & 2) v[m2] = sb; else v[m2 + 2] = sa;
-          }
-          const int64_t m = mw + 16 * i + 4 * g + p;
-          const int n = n0 + 16 * c + 4 * q;
-          if (m < M) {
-            if (n + 3 < N) {
-              *reinterpret_cast<float4*>(out + m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
-            } else {
-#pragma unroll
-              for (int r = 0; r < 4; ++r)
-                if (n + r < N) out[m * ldo + n + r] = v[r];
-            }
-          }
-        }
-    } else {
-#pragma unroll
-      for (int i = 0; i < FR; ++i)
-#pragma unroll
-        for (int c = 0; c < NT; ++c)
-#pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            const int64_t m = mw + 16 * i + 4 * g + r;
-            const int n = n0 + 16 * c + r16;
-            if (m < M && n < N) out[m * ldo + n] = acc[i][c][r];
-          }
-    }
+    store_tile(acc, sf, out, ldo, M, N, (grp0 + j * gstep) * GR + wv * (16 * FR), n0, lane, vstore);
   };
   auto tail = [&](int64_t j) __attribute__((always_inline)) {  // the K tail from registers, 16 k per step:
     for (int kt = S * KS; kt < K; kt += 16) {                     // k = kt + 4g + jj < K, zeros past it
@@ -2505,6 +2514,121 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   // the counted waits above assume only ring DMA is outstanding; stores may retire out of order
   // with the loads, so drain them here (the next group's first stages have had a step to land)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+}
+
+// fp32 UPDATE with one independent wave per block and no LDS (knob mm_wave): the same product as
+// k_mm_ring -- `template/ISA_defination.yaml:1-31` j,ij->i, LOAD_W `code/interpreter.py:335-343` --
+// without its per-stage block barrier.  A wave owns a (16 FR) x (16 NT) output tile and streams
+// both operands straight into registers: per 16-k stage, lane L = 16g + r loads x[row r][k0 + 4g ..
+// +3] of each of its FR row fragments and W^T[col r][k0 + 4g .. +3] of each of its NT column
+// fragments (16-B buffer loads; the stage offset k0 * 4 is the scalar soffset), exactly its MFMA
+// fragments, so nothing is staged or shuffled.  Step t issues W^T of stage t + 1, then x of stage
+// t + 3, waits until stage t has landed and runs FR x NT x 4 v_mfma_f32_16x16x4_f32 on it: x (HBM)
+// gets three stages of MFMA time to arrive, W^T (L2-resident) one.  The loads and the counted waits
+// are inline asm in a fixed order -- with the intrinsics, the compiler sank every load to one stage
+// ahead of its use (the registers it saved were not the bound), which left ~2 us of HBM latency
+// exposed per 1.7 us stage.  The K tail is one more stage whose lanes past K are zeroed (loads past
+// the tensor read 0 through the buffer bounds); stages past the last re-read it.  Same
+// per-accumulator k order and fma chain as k_mm_rows / k_mm_ring: bitwise equal to them.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4_t buf_desc(const void* p, uint32_t bytes) {  // raw buffer: stride 0, bounds = bytes
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  return i32x4_t{static_cast<int>(a & 0xffffffffu), static_cast<int>((a >> 32) & 0xffffu), static_cast<int>(bytes),
+                 0x00020000};
+}
+__device__ __forceinline__ void buf_load16(f32x4& v, uint32_t voff, const i32x4_t& rs, int soff) {
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(v) : "v"(voff), "s"(rs), "s"(soff) : "memory");
+}
+template <int NT, int FR, int WPS>
+__global__ void __launch_bounds__(kWave, WPS)
+k_mm_wave(const float* __restrict__ x, int64_t ldx, int64_t M, int K, const float* __restrict__ wt, int64_t ldwt, int N,
+          int sf, float* __restrict__ out, int64_t ldo, uint32_t x_bytes, uint32_t w_bytes) {
+  constexpr int GR = 16 * FR, BN = 16 * NT;
+  const int lane = threadIdx.x;
+  const int g = lane >> 4, r16 = lane & 15;
+  const int ncb = (N + BN - 1) / BN;
+  const int64_t n_units = (M + GR - 1) / GR * ncb;
+  const i32x4_t rx = buf_desc(x, x_bytes), rw = buf_desc(wt, w_bytes);
+  const int SF = (K + 15) / 16;  // stages, the K tail included
+  const bool tail = (K & 15) != 0;
+  const bool vstore = ldo % 4 == 0 && aligned(out, 16);
+  for (int64_t u = blockIdx.x; u < n_units; u += gridDim.x) {
+    const int n0 = static_cast<int>(u % ncb) * BN;
+    const int64_t mw = u / ncb * GR;
+    uint32_t ao[FR], bo[NT];
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+      ao[i] = static_cast<uint32_t>((min<int64_t>(mw + 16 * i + r16, M - 1) * ldx + 4 * g) * 4);
+#pragma unroll
+    for (int c = 0; c < NT; ++c) bo[c] = static_cast<uint32_t>((static_cast<int64_t>(min(n0 + 16 * c + r16, N - 1)) * ldwt + 4 * g) * 4);
+    f32x4 acc[FR][NT];
+#pragma unroll
+    for (int i = 0; i < FR; ++i)
+#pragma unroll
+      for (int c = 0; c < NT; ++c) acc[i][c] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 a0[FR], a1[FR], a2[FR], a3[FR], b0[NT], b1[NT];
+    auto load_a = [&](f32x4 (&a)[FR], int s) __attribute__((always_inline)) {
+      const int so = min(s, SF - 1) * 64;
+#pragma unroll
+      for (int i = 0; i < FR; ++i) buf_load16(a[i], ao[i], rx, so);
+    };
+    auto load_b = [&](f32x4 (&b)[NT], int s) __attribute__((always_inline)) {
+      const int so = min(s, SF - 1) * 64;
+#pragma unroll
+      for (int c = 0; c < NT; ++c) buf_load16(b[c], bo[c], rw, so);
+    };
+    // step t: W^T of t + 1 into bn, x of t + 3 into an; then stage t (ac, bc) has landed once at most
+    // the loads issued after B(t) -- x of t + 2 (the step before), bn and an -- are outstanding
+    auto step = [&](f32x4 (&ac)[FR], f32x4 (&bc)[NT], f32x4 (&bn)[NT], f32x4 (&an)[FR], int t)
+        __attribute__((always_inline)) {
+      load_b(bn, t + 1);
+      load_a(an, t + 3);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * FR + NT) : "memory");
+#pragma unroll
+      for (int i = 0; i < FR; ++i) asm volatile("" : "+v"(ac[i]));
+#pragma unroll
+      for (int c = 0; c < NT; ++c) asm volatile("" : "+v"(bc[c]));
+      if (tail && t == SF - 1) {  // k = 16 t + 4 g + e past K: zero (as k_mm_rows' masked loads)
+        const int k0 = 16 * t + 4 * g;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const bool past = k0 + e >= K;
+#pragma unroll
+          for (int i = 0; i < FR; ++i) ac[i][e] = past ? 0.f : ac[i][e];
+#pragma unroll
+          for (int c = 0; c < NT; ++c) bc[c][e] = past ? 0.f : bc[c][e];
+        }
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+#pragma unroll
+        for (int c = 0; c < NT; ++c)
+#pragma unroll
+          for (int i = 0; i < FR; ++i)
+            acc[i][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(ac[i][jj], bc[c][jj], acc[i][c], 0, 0, 0);
+    };
+    // issue order A(0), A(1), B(0), A(2): after B(t) come A(t + 2), B(t + 1), A(t + 3) for every t
+    load_a(a0, 0);
+    load_a(a1, 1);
+    load_b(b0, 0);
+    load_a(a2, 2);
+    int t = 0;  // a0..a2 hold stages t..t + 2, b0 stage t
+    for (; t + 4 <= SF; t += 4) {
+      step(a0, b0, b1, a3, t);
+      step(a1, b1, b0, a0, t + 1);
+      step(a2, b0, b1, a1, t + 2);
+      step(a3, b1, b0, a2, t + 3);
+    }
+    const int rem = SF - t;
+    if (rem >= 1) step(a0, b0, b1, a3, t);
+    if (rem >= 2) step(a1, b1, b0, a0, t + 1);
+    if (rem >= 3) step(a2, b0, b1, a1, t + 2);
+    // the loads issued past the last stage, and the stores below, drained before the next unit
+    // counts its own loads
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    store_tile(acc, sf, out, ldo, M, N, mw, n0, lane, vstore);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 }
 
@@ -2822,30 +2946,47 @@ k_mlp_bf(const TA* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint16_
   // bf16 x: one (held in xa[st][0]), its 4-B pairs past K1 zeroed by a select
   constexpr bool XB = sizeof(TA) == 2;
   const uint32_t row_bytes = static_cast<uint32_t>(ldx) * static_cast<uint32_t>(sizeof(TA));
-  auto load_x = [&](int64_t gi, float4 (&xa)[SB][2]) __attribute__((always_inline)) {
+  // The loads are inline asm in program order (with the intrinsics the compiler sank them next to
+  // their use and drained every load in flight at each group); x_wait() below counts them.
+  constexpr int LPG = XB ? SB : 2 * SB;  // loads per group
+  auto load_x = [&](int64_t gi, f32x4 (&xa)[SB][2]) __attribute__((always_inline)) {
     const int64_t row0 = gi * 16;
     const int64_t rows = max<int64_t>(0, min<int64_t>(16, M - row0));  // 0 past the last group: all zeros
-    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-        const_cast<TA*>(x + row0 * ldx), 0, static_cast<int>(rows * row_bytes), 0x00020000);
+    const i32x4_t rs = buf_desc(x + row0 * ldx, static_cast<uint32_t>(rows * row_bytes));
     const uint32_t roff = static_cast<uint32_t>(r16) * row_bytes;
 #pragma unroll
     for (int st = 0; st < SB; ++st) {
       if constexpr (XB) {
         const int k = 32 * st + 8 * g;
-        const uint32_t off = k < K1 ? roff + static_cast<uint32_t>(k) * 2u : 0x80000000u;
-        uint4 v = __builtin_bit_cast(uint4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
-        v.x = k < K1 ? v.x : 0u;  // (K1 is even: a pair is wholly inside or past K1)
-        v.y = k + 2 < K1 ? v.y : 0u;
-        v.z = k + 4 < K1 ? v.z : 0u;
-        v.w = k + 6 < K1 ? v.w : 0u;
-        xa[st][0] = __builtin_bit_cast(float4, v);
+        buf_load16(xa[st][0], k < K1 ? roff + static_cast<uint32_t>(k) * 2u : 0x80000000u, rs, 0);
       } else {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int k = 32 * st + 8 * g + 4 * h;
-          const uint32_t off = k < K1 ? roff + static_cast<uint32_t>(k) * 4u : 0x80000000u;
-          xa[st][h] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, off, 0, 0));
+          buf_load16(xa[st][h], k < K1 ? roff + static_cast<uint32_t>(k) * 4u : 0x80000000u, rs, 0);
         }
+      }
+    }
+  };
+  // a group's x landed: at most the two later groups' loads are outstanding (stores are not counted:
+  // they may retire out of order with the loads, and an outstanding one only makes the wait longer)
+  auto x_wait = [&](f32x4 (&xa)[SB][2]) __attribute__((always_inline)) {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * LPG) : "memory");
+#pragma unroll
+    for (int st = 0; st < SB; ++st) {
+      asm volatile("" : "+v"(xa[st][0]));
+      if constexpr (!XB) asm volatile("" : "+v"(xa[st][1]));
+    }
+    if constexpr (XB) {
+#pragma unroll
+      for (int st = 0; st < SB; ++st) {  // 4-B pairs past K1 zeroed (K1 is even: a pair is wholly in or past)
+        const int k = 32 * st + 8 * g;
+        uint4 v = __builtin_bit_cast(uint4, xa[st][0]);
+        v.x = k < K1 ? v.x : 0u;
+        v.y = k + 2 < K1 ? v.y : 0u;
+        v.z = k + 4 < K1 ? v.z : 0u;
+        v.w = k + 6 < K1 ? v.w : 0u;
+        xa[st][0] = __builtin_bit_cast(f32x4, v);
       }
     }
   };
@@ -2865,7 +3006,7 @@ k_mlp_bf(const TA* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint16_
   const bool vstore = ldo % 4 == 0 && aligned(out, 16);
   const int p = r16 & 3, qq = r16 >> 2;
   // one 16-row group: GEMM 1, the z image, GEMM 2, the stores
-  auto compute = [&](const float4 (&xa)[SB][2], int64_t grp) __attribute__((always_inline)) {
+  auto compute = [&](const f32x4 (&xa)[SB][2], int64_t grp) __attribute__((always_inline)) {
     f32x4 acc[1][NT];
 #pragma unroll
     for (int c = 0; c < NT; ++c) acc[0][c] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -2877,14 +3018,8 @@ k_mlp_bf(const TA* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint16_
       if constexpr (XB) {
         a8 = __builtin_bit_cast(bf16x8, xa[st][0]);
       } else {
-      a8[0] = static_cast<short>(to_bf16_bits(xa[st][0].x));
-      a8[1] = static_cast<short>(to_bf16_bits(xa[st][0].y));
-      a8[2] = static_cast<short>(to_bf16_bits(xa[st][0].z));
-      a8[3] = static_cast<short>(to_bf16_bits(xa[st][0].w));
-      a8[4] = static_cast<short>(to_bf16_bits(xa[st][1].x));
-      a8[5] = static_cast<short>(to_bf16_bits(xa[st][1].y));
-      a8[6] = static_cast<short>(to_bf16_bits(xa[st][1].z));
-      a8[7] = static_cast<short>(to_bf16_bits(xa[st][1].w));
+#pragma unroll
+      for (int q = 0; q < 8; ++q) a8[q] = static_cast<short>(to_bf16_bits(xa[st][q >> 2][q & 3]));
       }
       f32x4 b4[NT];
 #pragma unroll
@@ -2996,19 +3131,23 @@ k_mlp_bf(const TA* __restrict__ x, int64_t ldx, int64_t M, int K1, const uint16_
   // group past the last reads zeros (empty descriptor) and stores nothing (rows past M are masked).
   const int64_t mine = grp < n_groups ? (n_groups - grp + gstep - 1) / gstep : 0;
   const int64_t rounds = (mine + 2) / 3;
-  float4 xa[SB][2], xb[SB][2], xc[SB][2];
+  f32x4 xa[SB][2], xb[SB][2], xc[SB][2];
   if (rounds > 0) {
     load_x(grp, xa);
     load_x(grp + gstep, xb);
   }
   for (int64_t t = 0; t < rounds; ++t, grp += 3 * gstep) {
     load_x(grp + 2 * gstep, xc);
+    x_wait(xa);
     compute(xa, grp);
     load_x(grp + 3 * gstep, xa);
+    x_wait(xb);
     compute(xb, grp + gstep);
     load_x(grp + 4 * gstep, xb);
+    x_wait(xc);
     compute(xc, grp + 2 * gstep);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the loads issued past the last group
 }
 
 // out[m, n] = sf(sum_s ws[s][m][n]) in slice order (split-K UPDATE; ws slices are [M, N] dense).
@@ -3155,6 +3294,8 @@ struct Tuning {
   int mm_ring_depth = 0;   // k_mm_ring stages: 0 = auto (by blocks per CU), else 3, 4 or 8
   int mm_prefetch = 1;     // k_mm_rows A prefetch: 1 auto, 2 always, 0 never
   int64_t mm_split = -1;   // UPDATE K slices: -1 auto, 0 = never split, n = n slices
+  int mm_wave = 1;         // fp32 UPDATE on k_mm_wave (one wave per block, operands in registers): 0 never, 1 auto, 2 always
+  int mm_wave_fr = 0;      // k_mm_wave row fragments per wave: 2, 3 or 4 (0 = auto: the best CU balance)
 };
 
 Tuning& thread_tuning() {  // gta_debug_set / gta_debug_get: the calling thread's knobs
@@ -3213,6 +3354,8 @@ const Knob* find_knob(const char* key) {
       {"mm_ring_depth", &Tuning::mm_ring_depth, nullptr},
       {"mm_prefetch", &Tuning::mm_prefetch, nullptr},
       {"mm_split", nullptr, &Tuning::mm_split},
+      {"mm_wave", &Tuning::mm_wave, nullptr},
+      {"mm_wave_fr", &Tuning::mm_wave_fr, nullptr},
   };
   const std::string k(key ? key : "");
   for (const Knob& kb : knobs)
@@ -3881,6 +4024,90 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
 namespace {
 // k_mm_ring launch: NT (4: N <= 64, 8: wider), ring depth D (3 / 4 / 8: blocks per CU the grid
 // needs), FR (A fragments per wave); kslice > 0: the split-K form (grid.y = K slices)
+// waves per SIMD k_mm_wave<NT, FR> is built for (its __launch_bounds__): what its registers allow
+constexpr int wave_wps(int NT, int FR) { return NT == 4 || FR <= 2 ? 2 : 1; }
+
+// k_mm_wave unit cost model, in FR = 4 units (64 rows) of one wave alone on a SIMD, per unit of
+// each FR (profiles/r04/mm_wave_ab.log, K = 500 / 602): FR 3 (48 rows) 0.81, FR 2 (32 rows) 0.56 alone
+// and 1.3 per pair sharing a SIMD (its 2-waves-per-SIMD build).  A launch takes as many rounds of
+// its units as the most loaded SIMD holds: units spread over the 1024 SIMDs, FR 2 two deep.
+double wave_cost(int fr, int64_t units) {
+  if (fr == 2) return units <= 1024 ? 0.56 : static_cast<double>((units + 2047) / 2048) * 1.3;
+  return static_cast<double>((units + 1023) / 1024) * (fr == 3 ? 0.81 : 1.0);
+}
+
+struct WavePlan {
+  int fr = 4;          // FR of the first launch
+  int64_t rows = 0;    // rows of the first launch (all of M when there is no second)
+  int fr2 = 0;         // FR of the second launch over the remaining rows (0: none)
+  double cost = 0.0;
+};
+
+// the cheapest single launch, or whole FR = 4 rounds (every SIMD the same number of units) and the
+// remainder rows as a second launch with its own cheapest FR -- a partial last round of 64-row
+// units leaves SIMDs idle (232,965 x 602: 3.56 rounds)
+WavePlan wave_plan(int64_t M, int64_t ncb) {
+  WavePlan best;
+  best.cost = 1e30;
+  for (int f = 4; f >= 2; --f) {
+    const double c = wave_cost(f, (M + 16 * f - 1) / (16 * f) * ncb);
+    if (c < best.cost - 1e-9) { best.cost = c; best.fr = f; best.rows = M; best.fr2 = 0; }
+  }
+  const int64_t rounds = M / 64 * ncb / 1024;  // whole FR 4 rounds
+  if (rounds >= 1) {
+    const int64_t rows = rounds * 1024 / ncb * 64, rem = M - rows;
+    if (rem > 0 && rows > 0) {
+      for (int f = 4; f >= 2; --f) {
+        const double c = static_cast<double>(rounds) + wave_cost(f, (rem + 16 * f - 1) / (16 * f) * ncb) + 0.05;
+        if (c < best.cost - 1e-9) { best.cost = c; best.fr = 4; best.rows = rows; best.fr2 = f; }
+      }
+    }
+  }
+  return best;
+}
+
+int64_t wave_units(int64_t M, int64_t ncb, int fr) { return (M + 16 * fr - 1) / (16 * fr) * ncb; }
+
+// one k_mm_wave launch over rows [0, M) of x / out
+void launch_wave_rows(int nt, int fr, hipStream_t s, const float* x, int64_t ldx, int64_t M, int K, const float* wt,
+                      int64_t ldwt, int N, int sf, float* out, int64_t ldo) {
+  const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
+  const dim3 gr(static_cast<unsigned>(std::min<int64_t>(wave_units(M, ncb, fr), 1024LL * wave_wps(nt, fr))));
+  const uint32_t xbu = static_cast<uint32_t>(((M - 1) * ldx + K) * 4);
+  const uint32_t wbu = static_cast<uint32_t>((static_cast<int64_t>(N - 1) * ldwt + K) * 4);
+#define GTA_WAVE(NT_, FR_) \
+  k_mm_wave<NT_, FR_, wave_wps(NT_, FR_)><<<gr, dim3(kWave), 0, s>>>(x, ldx, M, K, wt, ldwt, N, sf, out, ldo, xbu, wbu)
+  if (nt == 8) { if (fr == 2) GTA_WAVE(8, 2); else if (fr == 3) GTA_WAVE(8, 3); else GTA_WAVE(8, 4); }
+  else { if (fr == 2) GTA_WAVE(4, 2); else if (fr == 3) GTA_WAVE(4, 3); else GTA_WAVE(4, 4); }
+#undef GTA_WAVE
+}
+
+// k_mm_wave over the whole output when it is the better form (knob mm_wave: 0 never, 1 auto, 2
+// whenever the shape allows; mm_wave_fr 2 / 3 / 4 forces one launch of that FR).  Auto: N > 64
+// (NT = 8), K >= 256 and enough units to occupy most SIMDs; elsewhere k_mm_ring measured as fast
+// or faster (profiles/r04/mm_wave_ab*.log).  Rows are independent, so the two-launch split is
+// bitwise the one-launch result.  False: not taken (the caller runs k_mm_ring).
+bool launch_wave(int nt, hipStream_t s, const float* x, int64_t ldx, int64_t M, int K, const float* wt, int64_t ldwt,
+                 int N, int sf, float* out, int64_t ldo) {
+  const int mode = tuning().mm_wave;
+  const int64_t xb = ((M - 1) * ldx + K) * 4, wb = (static_cast<int64_t>(N - 1) * ldwt + K) * 4;
+  if (mode == 0 || xb > 0xFFFFFFFFLL || wb > 0xFFFFFFFFLL || (nt != 4 && nt != 8) || K < 16) return false;
+  const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
+  const int frk = tuning().mm_wave_fr;
+  WavePlan pl;
+  if (frk == 2 || frk == 3 || frk == 4) {
+    pl.fr = frk;
+    pl.rows = M;
+  } else {
+    pl = wave_plan(M, ncb);
+  }
+  if (mode == 1 && (nt != 8 || K < 256 || wave_units(pl.rows, ncb, pl.fr) < 768)) return false;
+  launch_wave_rows(nt, pl.fr, s, x, ldx, pl.rows, K, wt, ldwt, N, sf, out, ldo);
+  if (pl.fr2 && pl.rows < M)
+    launch_wave_rows(nt, pl.fr2, s, x + pl.rows * ldx, ldx, M - pl.rows, K, wt, ldwt, N, sf, out + pl.rows * ldo, ldo);
+  return true;
+}
+
 void launch_ring(int nt, int D, int fr, dim3 gr, hipStream_t s, const float* x, int64_t ldx, const int32_t* row_idx,
                  int64_t M, int K, const float* wt, int64_t ldwt, int N, int sf, float* out, int64_t ldo, int kslice,
                  int64_t slice_stride) {
@@ -3935,6 +4162,14 @@ int gta_update_mm_t(const void* x, int64_t ldx, const int32_t* row_idx, int64_t 
   const int nt = mm_nt(N);
   const int64_t groups = (M + 127) / 128;
   const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
+  // (mm_ring = 0 selects k_mm_rows, and a forced ring shape (mm_ring_fr / mm_ring_depth) the ring)
+  if (dtype == GTA_F32 && tuning().mm_wave && tuning().mm_ring && !tuning().mm_ring_fr && !tuning().mm_ring_depth &&
+      !row_idx && K >= 16 &&
+      launch_wave(nt, S(stream), static_cast<const float*>(x), ldx, M, static_cast<int>(K), static_cast<const float*>(wt),
+                  ldwt, static_cast<int>(N), sf, out, ldo)) {
+    GTA_LAUNCHED("k_mm_wave");
+    return GTA_OK;
+  }
   if (K >= 32 && ring_ok(dtype, nt, x, wt, ldwt)) {
     // 64-row groups (one A fragment per wave, twice the work units for the per-CU balance) when
     // 128-row groups load the CUs unevenly on a short K, where per-group start-up and epilogue weigh

@@ -1036,6 +1036,45 @@ def _ring_vs_rows(dev, x, w, what):
     return y_ring
 
 
+@pytest.mark.parametrize("M,K,N,sf,ldo_pad,x_off", [
+    (40000, 602, 128, None, 0, 0), (232965, 602, 128, "RELU", 0, 0), (29000, 602, 256, None, 0, 0),
+    (44625, 500, 128, "ELU", 0, 0), (20011, 37, 200, None, 0, 0), (3001, 61, 66, "RELU", 1, 0),
+    (5000, 16, 72, None, 3, 0), (20000, 600, 128, None, 0, 1), (777, 1433, 100, "SIGMOID", 0, 3)])
+def test_update_mm_wave_bitwise(dev, M, K, N, sf, ldo_pad, x_off):
+    """k_mm_wave (fp32 UPDATE, one independent wave per block, both operands straight to registers;
+    the default for N > 64, K >= 256 on enough rows) == k_mm_rows bitwise at every row-fragment
+    count (FR 2 / 3 / 4 forced), the automatic plan (232,965 x 602: whole 64-row rounds, then the
+    remainder rows as a second launch) and mm_wave = 2 (every shape): K tails of every class as the
+    last register stage (37, 61, 600, 1433), K = 16 (one stage), columns past N (66, 72, 100, 200),
+    unaligned output rows (ldo = N + 1 / + 3: element stores), x rows only 4-B aligned (a column
+    window of a wider table), SF epilogues.  Within the fp64 bound."""
+    rng = np.random.default_rng(M + K + N)
+    big = torch.from_numpy(rng.standard_normal((M, K + x_off + (4 if x_off else 0))).astype(np.float32))
+    x = big[:, x_off:x_off + K]
+    w = torch.from_numpy((rng.standard_normal((K, N)) / np.sqrt(K)).astype(np.float32))
+    xd, wd = big.to(dev)[:, x_off:x_off + K], w.to(dev)
+    outs = []
+    try:
+        ops.set_debug("mm_split", 0)
+        for mode, fr in ((0, 0), (2, 2), (2, 3), (2, 4), (2, 0), (1, 0)):
+            ops.set_debug("mm_ring", 0 if mode == 0 else 1)
+            ops.set_debug("mm_wave", max(mode, 0))
+            ops.set_debug("mm_wave_fr", fr)
+            o = torch.full((M, N + ldo_pad), float("nan"), device=dev)[:, :N]
+            outs.append(ops.update_mm(xd, wd, sf=sf, out=o))
+    finally:
+        for k, v in (("mm_split", -1), ("mm_ring", 1), ("mm_wave", 1), ("mm_wave_fr", 0)):
+            ops.set_debug(k, v)
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs[1:]):
+        assert torch.equal(outs[0], o), i
+    rows = np.arange(0, M, max(1, M // 2000))
+    xs = x.numpy()[rows]
+    ref = isa_ref.mm(xs, w.numpy(), sf_kind=sf)
+    _check(outs[1][torch.from_numpy(rows).to(dev)], ref,
+           np.abs(xs).astype(np.float64) @ np.abs(w.numpy()).astype(np.float64), "k_mm_wave")
+
+
 @pytest.mark.parametrize("K", list(range(32, 65)))
 def test_update_mm_ring_every_k_tail(dev, K):
     """Every K tail class of the fp32 ring (K % 16 = 0..15; K % 4 = 0 runs the tail as one more
