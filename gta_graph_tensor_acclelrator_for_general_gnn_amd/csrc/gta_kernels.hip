@@ -2434,7 +2434,53 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
   };
   const bool vstore = ldo % 4 == 0 && aligned(out, 16);
   auto epilogue = [&](int64_t j) __attribute__((always_inline)) {
-    store_tile(acc, sf, out, ldo, M, N, (grp0 + j * gstep) * GR + wv * (16 * FR), n0, lane, vstore);
+    const int64_t mw = (grp0 + j * gstep) * GR + wv * (16 * FR);
+    sf_tile(sf, acc);
+    if (vstore) {  // quad-transposed 16-B row stores (k_mm_rows' epilogue)
+      const int p = r16 & 3, q = r16 >> 2;
+#pragma unroll
+      for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int c = 0; c < NT; ++c) {
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = acc[i][c][r];
+#pragma unroll
+          for (int m2 = 0; m2 < 2; ++m2) {
+            const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2]), 0xB1, 0xF, 0xF, false));
+            const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[2 * m2 + 1]), 0xB1, 0xF, 0xF, false));
+            if (p & 1) v[2 * m2] = sb; else v[2 * m2 + 1] = sa;
+          }
+#pragma unroll
+          for (int m2 = 0; m2 < 2; ++m2) {
+            const float sa = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2]), 0x4E, 0xF, 0xF, false));
+            const float sb = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v[m2 + 2]), 0x4E, 0xF, 0xF, false));
+            if (p & 2) v[m2] = sb; else v[m2 + 2] = sa;
+          }
+          const int64_t m = mw + 16 * i + 4 * g + p;
+          const int n = n0 + 16 * c + 4 * q;
+          if (m < M) {
+            if (n + 3 < N) {
+              *reinterpret_cast<float4*>(out + m * ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                if (n + r < N) out[m * ldo + n + r] = v[r];
+            }
+          }
+        }
+    } else {
+#pragma unroll
+      for (int i = 0; i < FR; ++i)
+#pragma unroll
+        for (int c = 0; c < NT; ++c)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int64_t m = mw + 16 * i + 4 * g + r;
+            const int n = n0 + 16 * c + r16;
+            if (m < M && n < N) out[m * ldo + n] = acc[i][c][r];
+          }
+    }
   };
   auto tail = [&](int64_t j) __attribute__((always_inline)) {  // the K tail from registers, 16 k per step:
     for (int kt = S * KS; kt < K; kt += 16) {                     // k = kt + 4g + jj < K, zeros past it
