@@ -4104,7 +4104,7 @@ WavePlan wave_plan(int64_t M, int64_t ncb) {
     const int64_t rows = rounds * 1024 / ncb * 64, rem = M - rows;
     if (rem > 0 && rows > 0) {
       for (int f = 4; f >= 2; --f) {
-        const double c = static_cast<double>(rounds) + wave_cost(f, (rem + 16 * f - 1) / (16 * f) * ncb) + 0.05;
+        const double c = static_cast<double>(rounds) + wave_cost(f, (rem + 16 * f - 1) / (16 * f) * ncb) + 0.1;
         if (c < best.cost - 1e-9) { best.cost = c; best.fr = 4; best.rows = rows; best.fr2 = f; }
       }
     }
