@@ -17,6 +17,9 @@ GROUPS = {
     "sq_insts": ["SQ_INSTS_VALU", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_SALU", "SQ_INSTS_LDS",
                  "SQ_ACTIVE_INST_LDS", "SQ_INSTS_SMEM", "GRBM_GUI_ACTIVE"],
     "l2": ["TCC_HIT_sum", "TCC_MISS_sum", "TCP_TCC_READ_REQ_sum"],
+    # the texture path (round 4): TA / TD busy and stall cycles, L1 -> L2 read latency
+    "tex": ["TA_TA_BUSY_sum", "TA_ADDR_STALLED_BY_TC_CYCLES_sum", "TD_TD_BUSY_sum", "TD_TC_STALL_sum",
+            "TCP_TCC_READ_REQ_LATENCY_sum", "TCP_TCC_READ_REQ_sum", "TCP_PENDING_STALL_CYCLES_sum", "GRBM_GUI_ACTIVE"],
 }
 KERNELS = ("k_agg_h32", "k_seg_reduce")
 
