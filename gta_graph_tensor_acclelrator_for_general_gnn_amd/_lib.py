@@ -10,7 +10,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgta.so")
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 # enum mirrors of include/gta.h
 GTA_F32, GTA_BF16, GTA_F32_BF16 = 0, 1, 2
@@ -42,7 +42,9 @@ SIGNATURES = {
     "gta_gat_aggregate_blocked_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64, _i64, _i64]),
     "gta_gat_aggregate_blocked": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _i32,
                                          _i32, _i32, _vp, _i64, _vp, _vp, _i64, _i64, _vp, _vp]),
-    "gta_gather_add": (_i32, [_vp, _i64, _i64, _vp, _i64, _i64, _vp, _i64, _i32, _vp]),
+    "gta_gather_add": (_i32, [_i32, _vp, _i64, _i64, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i32, _vp]),
+    "gta_csc_workspace_bytes": (_i64, [_i64, _i64]),
+    "gta_csc_build": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _vp, _vp, _vp, _i64, _vp]),
     "gta_apply_edge": (_i32, [_i32, _i32, _vp, _vp, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp,
                               _i64, _vp]),
     "gta_edge_softmax": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp]),

@@ -25,8 +25,17 @@ The cycle loop here skips runs of cycles in which nothing can start or finish
 the result is identical, and a Cora layer takes ~1 s instead of ~20 s.
 tile nnz data = calculate_sparsity(SR, 1) of the graph flattened row-major (:425-426),
 from ops.tile_nnz (GPU) or a CPU restatement.
+
+Per instruction (per_instruction): the bytes every instruction appends to simulate()'s rw_record
+(:282-309; aggregated per TYPE by aggregate_rw_record, :107-125) and the unit-busy cycles of its
+iterations (the durations update_timeline records, :329-330), in closed form over the tile-nnz
+array with NumPy -- no cycle loop, so it runs at Reddit scale (the metric block's 106 M-iteration
+instructions) in seconds.  The cycle loop (simulate_stream(..., record=True)) adds each
+instruction's first start and last end; timeline_info restates aggregate_timeline (:127-146).
 """
 import math
+
+import numpy as np
 
 BW = 128 * (1024 ** 3) * (10 ** (-9))
 UNITS = ["Memory_Access_Unit", "VEC_ALU", "SF_ALU", "MM", "Virtual_Loader"]
@@ -42,12 +51,13 @@ def _find(blocks, typ, ident):
 
 
 class _Sim:
-    def __init__(self, node_num, tiles_for, sinput=False, sparsity=1.0):
+    def __init__(self, node_num, tiles_for, sinput=False, sparsity=1.0, record=False):
         self.N = node_num
         self.tiles_for = tiles_for  # SR -> flat list of tile nnz (row-major [ceil(N/SR)][N])
         self.sinput = sinput
         self.sparsity = sparsity
         self.rw = 0
+        self.spans = {} if record else None  # (block, index) -> [first start, its cost, last end]
 
     def cost(self, inst, remain, data):
         t = inst["TYPE"]
@@ -91,6 +101,10 @@ class _Sim:
         for b, blk in enumerate(blocks):
             if b == 0 or tile_sizes[b][0] != tile_sizes[b - 1][0]:
                 data = self.tiles_for(tile_sizes[b][0])
+                if isinstance(data, TileCounts):
+                    data = data.dense()
+                if isinstance(data, np.ndarray):
+                    data = data.tolist()
             n = len(blk)
             credit = [[0] * n for _ in range(n)]
             for j, inst in enumerate(blk):
@@ -124,6 +138,9 @@ class _Sim:
                         unit_busy[unit_of[j]] = True
                         state[j] = 1
                         remain_cycle[j] = self.cost(blk[j], remain_times[j], data)
+                        if self.spans is not None:
+                            sp = self.spans.setdefault((b, j), [cycle, remain_cycle[j], 0])
+                            sp[2] = cycle + remain_cycle[j]
                         busy_change = True
                     elif st == 1:
                         unfinished = True
@@ -155,9 +172,13 @@ class _Sim:
         return cycle - 1, self.rw
 
 
-def simulate_stream(blocks, tile_size_list, node_num, tiles_for, sinput=False, sparsity=1.0):
-    """(cycles, rw) exactly as code/simulator.py:370-502 computes them for this stream."""
-    return _Sim(node_num, tiles_for, sinput, sparsity).run(blocks, tile_size_list)
+def simulate_stream(blocks, tile_size_list, node_num, tiles_for, sinput=False, sparsity=1.0, record=False):
+    """(cycles, rw) exactly as code/simulator.py:370-502 computes them for this stream.  record=True:
+    (cycles, rw, spans) with spans[(block, index)] = [first start cycle, that iteration's cost, last
+    end cycle] per instruction -- the first and last entries update_timeline (:329-330) records."""
+    sim = _Sim(node_num, tiles_for, sinput, sparsity, record)
+    cycles, rw = sim.run(blocks, tile_size_list)
+    return (cycles, rw, sim.spans) if record else (cycles, rw)
 
 
 def model_rw(blocks, node_num, edges_in_tiles):
@@ -175,3 +196,157 @@ def model_rw(blocks, node_num, edges_in_tiles):
             elif t == "LOAD_W":
                 rw += tt * math.ceil(ts * fl)
     return rw
+
+
+class TileCounts:
+    """calculate_sparsity(T, 1)'s flat [ceil(N/T) * n_cols] list without its zeros: the nonzero
+    tile counts (any order), the list's length and its first entry (tile (0, 0)) -- all the
+    per-instruction model needs when an instruction sweeps every tile (Tile_Times == length, which
+    interpret()'s TR*TC is), at the size of the edge list rather than the tile grid (ogbn-products'
+    dense grid at T = 512 would hold 1.2e10 entries).  dense() rebuilds the list (small graphs)."""
+    __slots__ = ("length", "values", "first", "_dense")
+
+    def __init__(self, length, values, first, dense=None):
+        self.length, self.values, self.first, self._dense = int(length), np.asarray(values, np.int64), int(first), dense
+
+    def __len__(self):
+        return self.length
+
+    def dense(self):
+        if self._dense is None:
+            raise ValueError("TileCounts: no dense form available")
+        return np.asarray(self._dense(), dtype=np.int64)
+
+
+def _first(data, tt):
+    """data[len(data) - tt]: the tile of an instruction's first iteration."""
+    if isinstance(data, TileCounts):
+        if tt == data.length:
+            return data.first
+        data = data.dense()
+    return int(_data_slice(data, tt)[0])
+
+
+def _data_slice(data, tt):
+    """data[len(data) - remain] for remain = tt .. 1 (the iteration order of :282 and :324), as an
+    array; Python's negative-index wrap for remain > len(data) kept."""
+    n = len(data)
+    if tt <= n:
+        return data[n - tt:]
+    idx = n - np.arange(tt, 0, -1, dtype=np.int64)
+    return data[np.where(idx < 0, idx + n, idx)]
+
+
+def _edge_sums(cache, data, tt, fl):
+    """(sum nnz, sum ceil(nnz/8), sum ceil(nnz*fl/BW)) over the instruction's iterations, cached per
+    (tt, fl): the metric block's three edge instructions share one 106 M-entry pass each."""
+    key = (id(data), tt)
+    if key not in cache:
+        if isinstance(data, TileCounts):
+            d = data.values if tt == data.length else _data_slice(data.dense(), tt)  # zeros add nothing
+        else:
+            d = _data_slice(data, tt)
+        cache[key] = {"nnz": int(d.sum()), "c8": int(((d + 7) // 8).sum()), "d": d}
+    ent = cache[key]
+    if fl not in ent:
+        ent[fl] = int(np.ceil((ent["d"] * fl) / BW).sum())
+    return ent["nnz"], ent["c8"], ent[fl]
+
+
+def per_instruction(blocks, tile_size_list, node_num, tiles_for, sinput=False, sparsity=1.0):
+    """Closed-form per-instruction model of simulate() (code/simulator.py:272-327) for a stream.
+
+    Returns one dict per instruction, in stream order:
+      block, index, TYPE, ID, unit   -- where it is and which modelled unit runs it
+      starts                          -- iterations (= Tile_Times = timeline entries)
+      rw_bytes                        -- its contribution to simulate()'s rw
+      record_bytes, records, nnz      -- what it appends to rw_record: summed bytes, count, and the
+                                         summed edge-tile nnz of its LOAD_E/STORE_E records
+      busy                            -- summed unit-busy cycles of its iterations (timeline durations)
+      first_cost                      -- the cost of its first iteration
+    Equal to the records simulate() keeps, bit for bit (tests/golden/simulate_records.json)."""
+    out = []
+    cache = {}
+    data = None
+    for b, blk in enumerate(blocks):
+        if b == 0 or tile_size_list[b][0] != tile_size_list[b - 1][0]:
+            data = tiles_for(tile_size_list[b][0])
+            if not isinstance(data, TileCounts):
+                data = np.asarray(data, dtype=np.int64)
+        for j, inst in enumerate(blk):
+            t, fl, tt, ts, unit = (inst["TYPE"], inst["Feature_Length"], inst["Tile_Times"], inst["Tile_Size"],
+                                   inst["Hardware_Unit"])
+            r = {"block": b, "index": j, "TYPE": t, "ID": inst["ID"], "unit": unit, "starts": tt, "rw_bytes": 0,
+                 "record_bytes": 0, "records": 0, "nnz": 0, "busy": 0, "first_cost": 0}
+            if tt <= 0:
+                out.append(r)
+                continue
+            if t in ("LOAD_E", "STORE_E"):
+                nnz, _, cyc = _edge_sums(cache, data, tt, fl)
+                d0 = _first(data, tt)
+                r.update(rw_bytes=nnz * fl, record_bytes=nnz * fl, records=tt, nnz=nnz, busy=cyc,
+                         first_cost=math.ceil(d0 * fl / BW))
+            elif t in ("LOAD_W", "LOAD_N", "STORE_N"):
+                sp = (t == "LOAD_N" and "0_applynode" in inst["ID"] and sinput and any(
+                    d["TYPE"] == "COMP_MM" and d["ID"].split("_")[0] == inst["ID"].split("_")[0]
+                    for d in inst["Dependency"]["WAR"]))
+                if sp:  # the sparse-input path adds to rw but records nothing (:292-295)
+                    v = math.ceil(ts * fl * sparsity)
+                    c = math.ceil(ts * fl * sparsity / BW)
+                    r.update(rw_bytes=tt * v, busy=tt * c, first_cost=c)
+                else:
+                    full = ts * fl
+                    last = full
+                    if t != "LOAD_W":
+                        blk_rows = node_num - math.floor(node_num / ts) * ts
+                        last = (blk_rows if blk_rows else ts) * fl
+                    cf, cl = math.ceil(full / BW), math.ceil(last / BW)
+                    tot = (tt - 1) * math.ceil(full) + math.ceil(last)
+                    r.update(rw_bytes=tot, record_bytes=(tt - 1) * full + last, records=tt,
+                             busy=(tt - 1) * cf + cl, first_cost=cl if tt == 1 else cf)
+            else:
+                perf = PERF[unit]
+                if t == "COMP_MM":
+                    if "0_applynode" in inst["ID"] and sinput:
+                        c = math.ceil(ts * sparsity / PERF["VEC_ALU"][0]) * math.ceil(fl / PERF["VEC_ALU"][1])
+                    else:
+                        c = math.ceil(math.ceil(fl / perf[1]) * math.ceil((inst["Weight_Size"] / fl) / perf[0]))
+                    r.update(busy=tt * c, first_cost=c)
+                elif "applyedge" in inst["ID"] or "gather" in inst["ID"]:
+                    _, c8, _ = _edge_sums(cache, data, tt, fl)
+                    f16 = math.ceil(fl / perf[1])
+                    d0 = _first(data, tt)
+                    r.update(busy=c8 * f16, first_cost=math.ceil(d0 / perf[0]) * f16)
+                else:
+                    c = math.ceil(ts / perf[0]) * math.ceil(fl / perf[1])
+                    r.update(busy=tt * c, first_cost=c)
+            out.append(r)
+    return out
+
+
+def rw_info(insts):
+    """aggregate_rw_record (code/simulator.py:107-125): ({TYPE: summed bytes}, {TYPE: records})."""
+    val, cnt = {}, {}
+    for r in insts:
+        if r["records"]:
+            val[r["TYPE"]] = val.get(r["TYPE"], 0) + r["record_bytes"]
+            cnt[r["TYPE"]] = cnt.get(r["TYPE"], 0) + r["records"]
+    return val, cnt
+
+
+def timeline_info(insts, spans):
+    """aggregate_timeline (code/simulator.py:127-146): ({TYPE: entries}, {TYPE: summed durations}).
+    Restated with its quirk: a type's first entry met (blocks in order, units in UNITS order, then
+    time order) initialises the total with its duration and is then added again."""
+    count, total = {}, {}
+    order = sorted(insts, key=lambda r: (r["block"], UNITS.index(r["unit"]), spans[(r["block"], r["index"])][0]))
+    for r in order:
+        if r["starts"] <= 0:
+            continue
+        t = r["TYPE"]
+        if t not in count:
+            count[t] = 0
+            total[t] = r["first_cost"]
+        count[t] += r["starts"]
+        total[t] += r["busy"]
+    return count, total

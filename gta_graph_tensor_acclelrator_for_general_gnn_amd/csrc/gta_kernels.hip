@@ -3870,11 +3870,207 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
   return GTA_OK;
 }
 
-int gta_gather_add(const int64_t* indptr, int64_t n_rows, int64_t nnz, const float* xe, int64_t ldxe, int64_t F,
-                   float* y, int64_t ldy, int accumulate, void* stream) {
+}  // extern "C"
+
+// ---------------------------------------------------------------------------
+// CSC view of the CSR (ABI 11): the edge permutation that orders edges by SOURCE column, for the
+// ISA gather with DIRECTION src (template/ISA_defination.yaml:46-48, "from edges to src
+// (column-wise)"; lowered with ORDER C, code/interpreter.py:108-121).  A stable LSD radix sort of
+// (source column, edge id) with 8-bit digits: per pass a per-tile digit histogram, one exclusive
+// scan over [digit][tile], and a stable scatter in which every element's place is fixed by its
+// position in the CSR (ranks inside a wave from 8 ballots, across waves and rounds from LDS
+// counters) -- no atomics decide an order, so perm is a pure function of the graph: within a
+// column, edges keep CSR order (increasing destination row, then CSR position).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kRadixItems = 16;                    // elements per thread per tile
+constexpr int64_t kRadixTile = int64_t{kBlock} * kRadixItems;
+
+__global__ void __launch_bounds__(kBlock) k_radix_hist(const uint32_t* __restrict__ keys, int64_t n, int shift,
+                                                       int32_t* __restrict__ hist, int64_t nb) {
+  __shared__ uint32_t cnt[256];
+  const int t = threadIdx.x;
+  cnt[t] = 0;
+  __syncthreads();
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kRadixTile;
+#pragma unroll 4
+  for (int r = 0; r < kRadixItems; ++r) {
+    const int64_t i = base + r * kBlock + t;
+    if (i < n) atomicAdd(&cnt[(keys[i] >> shift) & 255u], 1u);  // a count: order-independent
+  }
+  __syncthreads();
+  hist[static_cast<int64_t>(t) * nb + blockIdx.x] = static_cast<int32_t>(cnt[t]);
+}
+
+// vals_in == nullptr: the value of element i is i (the edge id, first pass)
+__global__ void __launch_bounds__(kBlock) k_radix_scatter(const uint32_t* __restrict__ keys_in,
+                                                          const uint32_t* __restrict__ vals_in, int64_t n, int shift,
+                                                          const int32_t* __restrict__ offs, int64_t nb,
+                                                          uint32_t* __restrict__ keys_out,
+                                                          uint32_t* __restrict__ vals_out) {
+  __shared__ uint32_t run[256];
+  __shared__ uint32_t wcnt[kWavesPerBlock][256];
+  const int t = threadIdx.x, lane = t & (kWave - 1), w = t / kWave;
+  run[t] = static_cast<uint32_t>(offs[static_cast<int64_t>(t) * nb + blockIdx.x]);
+#pragma unroll
+  for (int q = 0; q < kWavesPerBlock; ++q) wcnt[q][t] = 0;
+  __syncthreads();
+  const uint64_t below = lane ? (~0ull >> (kWave - lane)) : 0ull;
+  const int64_t base = static_cast<int64_t>(blockIdx.x) * kRadixTile;
+  for (int r = 0; r < kRadixItems; ++r) {  // round r: elements base + r*256 + t, in thread order
+    const int64_t i = base + r * kBlock + t;
+    const bool valid = i < n;
+    const uint32_t k = valid ? keys_in[i] : 0u;
+    const uint32_t v = valid ? (vals_in ? vals_in[i] : static_cast<uint32_t>(i)) : 0u;
+    const uint32_t d = (k >> shift) & 255u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const uint64_t m = __ballot(bit);
+      peers &= bit ? m : ~m;
+    }
+    const uint32_t rank = static_cast<uint32_t>(__popcll(peers & below));
+    const uint32_t cnt = static_cast<uint32_t>(__popcll(peers));
+    if (valid && rank + 1 == cnt) wcnt[w][d] = cnt;  // the wave's last lane of this digit
+    __syncthreads();
+    if (valid) {
+      uint32_t pos = run[d] + rank;
+      for (int q = 0; q < w; ++q) pos += wcnt[q][d];
+      if (keys_out) keys_out[pos] = k;
+      vals_out[pos] = v;
+    }
+    __syncthreads();
+    uint32_t add = 0;
+#pragma unroll
+    for (int q = 0; q < kWavesPerBlock; ++q) {
+      add += wcnt[q][t];
+      wcnt[q][t] = 0;
+    }
+    run[t] += add;
+    __syncthreads();
+  }
+}
+
+// colptr[j] = first position of column j in the sorted keys (lower bound), j in [0, n_cols]
+__global__ void __launch_bounds__(kBlock) k_csc_colptr(const uint32_t* __restrict__ sorted, int64_t n, int64_t n_cols,
+                                                       int64_t* __restrict__ colptr) {
+  const int64_t j = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (j > n_cols) return;
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (static_cast<int64_t>(sorted[mid]) < j) lo = mid + 1; else hi = mid;
+  }
+  colptr[j] = lo;
+}
+
+// rows[k] = destination row of edge perm[k] (the last row whose indptr start is <= perm[k])
+__global__ void __launch_bounds__(kBlock) k_csc_rows(const int64_t* __restrict__ indptr, int64_t n_rows,
+                                                     const int32_t* __restrict__ perm, int64_t n,
+                                                     int32_t* __restrict__ rows) {
+  const int64_t k = static_cast<int64_t>(blockIdx.x) * kBlock + threadIdx.x;
+  if (k >= n) return;
+  const int64_t e = perm[k];
+  int64_t lo = 0, hi = n_rows;  // invariant: indptr[lo] <= e < indptr[hi]
+  while (hi - lo > 1) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (indptr[mid] <= e) lo = mid; else hi = mid;
+  }
+  rows[k] = static_cast<int32_t>(lo);
+}
+
+struct CscWork {
+  uint32_t* keys[2];
+  uint32_t* vals;
+  int32_t* hist;
+  int64_t* scan;
+  int64_t nb;
+};
+
+inline int64_t round256(int64_t b) { return (b + 255) / 256 * 256; }
+
+int64_t csc_layout(int64_t nnz, char* p, CscWork* w) {
+  const int64_t nb = (nnz + kRadixTile - 1) / kRadixTile;
+  const int64_t kb = round256(nnz * 4), hb = round256((256 * nb + 1) * 4), sb = round256((kScanMaxTiles + 1) * 8);
+  if (w) {
+    w->keys[0] = reinterpret_cast<uint32_t*>(p);
+    w->keys[1] = reinterpret_cast<uint32_t*>(p + kb);
+    w->vals = reinterpret_cast<uint32_t*>(p + 2 * kb);
+    w->hist = reinterpret_cast<int32_t*>(p + 3 * kb);
+    w->scan = reinterpret_cast<int64_t*>(p + 3 * kb + hb);
+    w->nb = nb;
+  }
+  return 3 * kb + hb + sb;
+}
+}  // namespace
+
+extern "C" {
+
+int64_t gta_csc_workspace_bytes(int64_t n_cols, int64_t nnz) {
+  if (n_cols < 0 || nnz < 0) return -1;
+  return csc_layout(nnz, nullptr, nullptr);
+}
+
+int gta_csc_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols, int64_t nnz,
+                  int64_t* colptr, int32_t* perm, int32_t* rows, void* workspace, int64_t workspace_bytes,
+                  void* stream) {
   const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
-  return gta_aggregate(indptr, nullptr, n_rows, nnz, GTA_IDX_EDGE, xe, ldxe, F, GTA_F32, nullptr, 0, 0, nullptr, y,
-                       ldy, accumulate, nullptr, 0, nullptr, stream);
+  if (n_rows < 0 || n_cols < 0 || nnz < 0 || !colptr) return fail(GTA_ERR_ARG, "csc_build: bad arguments");
+  if (nnz > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "csc_build: more than 2^31 - 1 edges");
+  if (n_cols > (int64_t{1} << 32)) return fail(GTA_ERR_UNSUPPORTED, "csc_build: more than 2^32 columns");
+  hipStream_t s = S(stream);
+  if (nnz == 0) {
+    GTA_HIP(hipMemsetAsync(colptr, 0, (n_cols + 1) * sizeof(int64_t), s));
+    return GTA_OK;
+  }
+  if (!indptr || !indices || !perm || n_rows == 0 || n_cols == 0) return fail(GTA_ERR_ARG, "csc_build: bad arguments");
+  if (!workspace || workspace_bytes < csc_layout(nnz, nullptr, nullptr))
+    return fail(GTA_ERR_ARG, "csc_build: workspace smaller than gta_csc_workspace_bytes");
+  CscWork w;
+  csc_layout(nnz, static_cast<char*>(workspace), &w);
+  int bits = 0;
+  for (uint64_t m = static_cast<uint64_t>(n_cols - 1); m; m >>= 1) ++bits;
+  const int passes = bits > 8 ? (bits + 7) / 8 : 1;
+  const dim3 grid(static_cast<unsigned>(w.nb)), blk(kBlock);
+  const uint32_t* kin = reinterpret_cast<const uint32_t*>(indices);
+  const uint32_t* vin = nullptr;
+  for (int p = 0; p < passes; ++p) {
+    uint32_t* kout = w.keys[p & 1];
+    uint32_t* vout = ((passes - 1 - p) % 2 == 0) ? reinterpret_cast<uint32_t*>(perm) : w.vals;  // last pass -> perm
+    k_radix_hist<<<grid, blk, 0, s>>>(kin, nnz, 8 * p, w.hist, w.nb);
+    GTA_LAUNCHED("k_radix_hist");
+    scan_excl<int32_t>(w.hist, 256 * w.nb, 0, nullptr, w.scan, s);
+    GTA_LAUNCHED("scan_excl");
+    k_radix_scatter<<<grid, blk, 0, s>>>(kin, vin, nnz, 8 * p, w.hist, w.nb, kout, vout);
+    GTA_LAUNCHED("k_radix_scatter");
+    kin = kout;
+    vin = vout;
+  }
+  k_csc_colptr<<<dim3(static_cast<unsigned>((n_cols + 1 + kBlock - 1) / kBlock)), blk, 0, s>>>(kin, nnz, n_cols, colptr);
+  GTA_LAUNCHED("k_csc_colptr");
+  if (rows) {
+    k_csc_rows<<<dim3(static_cast<unsigned>((nnz + kBlock - 1) / kBlock)), blk, 0, s>>>(indptr, n_rows, perm, nnz, rows);
+    GTA_LAUNCHED("k_csc_rows");
+  }
+  return GTA_OK;
+}
+
+int gta_gather_add(int dir, const int64_t* indptr, int64_t n_rows, int64_t nnz, const int64_t* colptr,
+                   const int32_t* perm, int64_t n_cols, const float* xe, int64_t ldxe, int64_t F, float* y,
+                   int64_t ldy, int accumulate, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
+  if (dir == GTA_DIR_R)
+    return gta_aggregate(indptr, nullptr, n_rows, nnz, GTA_IDX_EDGE, xe, ldxe, F, GTA_F32, nullptr, 0, 0, nullptr, y,
+                         ldy, accumulate, nullptr, 0, nullptr, stream);
+  if (dir != GTA_DIR_C) return fail(GTA_ERR_ARG, "gather_add: bad dir");
+  if (n_cols < 0) return fail(GTA_ERR_ARG, "gather_add: bad n_cols");
+  if (nnz > 0 && (!colptr || !perm)) return fail(GTA_ERR_ARG, "gather_add C needs the CSC view (gta_csc_build)");
+  if (nnz == 0 && n_cols > 0 && !colptr) return fail(GTA_ERR_ARG, "gather_add C needs colptr");
+  // y[j] = sum over column j's edges, in CSC order, of xe[perm[k]]: the edge tensor read as a table
+  // of nnz rows gathered by index -- the same ordered row kernel as direction R, no atomics
+  return gta_aggregate(colptr, perm, n_cols, nnz, GTA_IDX_SRC, xe, ldxe, F, GTA_F32, nullptr, 0, 0, nullptr, y, ldy,
+                       accumulate, nullptr, 0, nullptr, stream);
 }
 
 int gta_scatter(int dir, const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, const void* x,

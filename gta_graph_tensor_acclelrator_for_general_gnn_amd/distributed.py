@@ -246,6 +246,24 @@ class Comm:
         dist.all_reduce(y, group=self.group)  # gloo: no reduce-scatter
         return y[s.rank * s.m: s.rank * s.m + s.n_local]
 
+    def reduce_cols(self, y):
+        """A gather to the SOURCE (ISA gather DIRECTION src, ORDER C) over this rank's CSR, [n_cols, F]
+        -> this rank's summed node block [n_p, F].  Column shards own their sources' every edge, so
+        their sums are complete; a row shard's columns are the padded [world*m] table layout and each
+        rank holds partial sums of every block: reduce-scattered like reduce_rows."""
+        s = self.s
+        if not self.local_rows:
+            return y[:s.n_local]
+        if not self.on:
+            return y[s.rank * s.m: s.rank * s.m + s.n_local]
+        self.bytes += y.numel() * y.element_size()
+        if self.nccl:
+            out = torch.empty(s.m, y.shape[1], dtype=y.dtype, device=y.device)
+            dist.reduce_scatter_tensor(out, y.contiguous(), group=self.group)
+            return out[:s.n_local]
+        dist.all_reduce(y, group=self.group)  # gloo: no reduce-scatter
+        return y[s.rank * s.m: s.rank * s.m + s.n_local]
+
     def gather_rows(self, x):
         """Dst-side scatter table: column shards all-gather the blocks; row shards own the rows."""
         return x if self.local_rows else self._all_blocks(x)

@@ -24,6 +24,7 @@ import os
 import time
 import weakref
 
+import numpy as np
 import torch
 
 from . import ir, ops
@@ -123,6 +124,9 @@ class ExecResult:
         self.model_cycles = None  # simulate()'s first result (code/simulator.py:502), if requested
         self.model_rw = None      # simulate()'s second result: modelled DRAM bytes
         self.trace = None         # Chrome trace events when execute(..., trace=...) asked for them
+        self.model_insts = None   # per-instruction model (costmodel.per_instruction), when a model was asked for
+        self.model_spans = None   # model="full": (block, index) -> [first start, first cost, last end] cycles
+        self.model_arch = None    # (architecture_name, flexible) of a vTCAD-style call
 
     def simulate_tuple(self):
         """(cycles, rw) in the shape the reference's simulate() returns."""
@@ -519,7 +523,9 @@ class Executor:
 
     def _gather_value(self, op):
         v = self._eval_gather(op)
-        return NodeT(self.dist.reduce_rows(v.t)) if self.dist is not None else v
+        if self.dist is None:
+            return v
+        return NodeT(self.dist.reduce_cols(v.t) if op.order == "C" else self.dist.reduce_rows(v.t))
 
     def _eval_mm_first(self, G, M):
         """Sets M's value to aggregate(x W) and returns G's value lazily; None if the operands
@@ -720,8 +726,10 @@ class Executor:
     def _eval_gather(self, op, acc=None, self_term=None, out_dtype=torch.float32):
         """self_term (x, s): y = x * s + the aggregate, or None if this gather's form cannot take it;
         out_dtype (self_term only): y's storage dtype."""
-        if op.order != "R":
-            raise NotImplementedError("gather ORDER C (to source) is not emitted by genGraphOP")
+        if op.order == "C":
+            if acc is not None or self_term is not None:
+                return None
+            return self._eval_gather_c(op)
         src = self.g.inputs[op.idx][0]
         if self_term is not None:
             v = self._source(op, 0) if not (self.fuse_attention and src.kind == "op" and src.op in self.attn) else None
@@ -786,6 +794,73 @@ class Executor:
 
     def _plan(self):
         return self.plan_chunk if self.plan_chunk else None
+
+    def _eval_gather_c(self, op):
+        """ISA gather with DIRECTION src (ORDER C, template/ISA_defination.yaml:46-48): y[j] = sum of
+        the edge value over the edges whose SOURCE is j, y [n_cols, F].  Runs the ordered row kernels
+        over the graph's stable CSC view (ops.CSC, gta_csc_build): a column's edges are summed in CSR
+        order, deterministic, no atomics.  A fused producer stays virtual as in direction R: a scatter
+        operand is gathered by index (its CSC view: "dst" rows for scatter R, the column itself for
+        scatter C), a MUL by an edge weight runs as one weighted aggregate (the weight read in CSC
+        order through one permuting copy); anything else is materialised as an edge tensor and summed
+        by CSC position (gta_gather_add's direction C)."""
+        c = ops.csc(self.graph)
+        E, nc = self.graph.nnz, self.graph.n_cols
+        v = self._source(op, 0)
+        if isinstance(v, Deferred):
+            p = self.g.ops[v.op]
+            if p.comp != "MM" and self._binary(p) == "MUL":
+                pins = self._inputs(p)
+                if len(pins) == 1:
+                    extra = self._ext(p, 1)
+                    pins = pins + ([self._wrap_ext(extra)] if extra is not None else [])
+                if len(pins) == 2:
+                    y = self._weighted_c(c, pins[0], pins[1])
+                    if y is not None:
+                        return NodeT(y)
+            v = self._materialize_deferred(v)
+        if isinstance(v, Scat):
+            view = c.view("dst" if v.mode == "dst" else "src")
+            y = ops.aggregate(view, v.t, "src", None, plan=self._plan())
+            self._count(E * (4 + v.t.shape[1] * v.t.element_size()) + nc * (8 + v.t.shape[1] * 4))
+            return NodeT(y)
+        xe = self._to_edge_tensor(v)
+        y = ops.aggregate(c.view("edge"), xe, "src", None, plan=self._plan())
+        self._count(E * (4 + xe.shape[1] * 4) + nc * (8 + xe.shape[1] * 4))
+        return NodeT(y)
+
+    def _weighted_c(self, c, u, v):
+        """sum over a source column's edges of u(e) (.) v(e) (direction C form of _weighted_aggregate):
+        the narrower operand is the (head) weight, permuted once into CSC order; None when neither
+        operand is an edge/scatter tensor of a width the aggregate takes."""
+        def width(z):
+            if isinstance(z, tuple):
+                return z[1].shape[1]
+            return z.t.shape[1] if not isinstance(z, Deferred) else 0
+
+        x, w = (u, v) if width(u) >= width(v) else (v, u)
+        if isinstance(x, tuple) or isinstance(x, Deferred) or isinstance(w, Deferred):
+            return None
+        E, nc = self.graph.nnz, self.graph.n_cols
+        if isinstance(w, tuple) and w[0] == "row":  # a constant row weight: aggregate then scale (linear)
+            if isinstance(x, Scat):
+                y = ops.aggregate(c.view("dst" if x.mode == "dst" else "src"), x.t, "src", None, plan=self._plan())
+            else:
+                y = ops.aggregate(c.view("edge"), self._to_edge_tensor(x), "src", None, plan=self._plan())
+            self._count(E * (4 + 4 * y.shape[1]) + nc * (8 + 4 * y.shape[1]))
+            return ops.apply_node("MUL", None, y, w[1], b_broadcast_row=True)
+        wt = self._to_edge_tensor(w)
+        if wt.dtype != torch.float32 or width(x) % wt.shape[1]:
+            return None
+        wc = ops.apply_edge(c.view("edge"), None, None, wt, "src")  # wc[k] = wt[perm[k]]: CSC order
+        if isinstance(x, Scat):
+            view, table = c.view("dst" if x.mode == "dst" else "src"), x.t
+        else:
+            view, table = c.view("edge"), self._to_edge_tensor(x)
+        y = ops.aggregate(view, table, "src", wc, plan=self._plan())
+        F, H = table.shape[1], wc.shape[1]
+        self._count(E * 8 * H + E * (4 + 4 * H + table.element_size() * F) + nc * (8 + 4 * F))
+        return y
 
     def _weighted_aggregate(self, u, v, acc=None, self_term=None, out_dtype=torch.float32):
         """sum_e u(e) (.) v(e): the wider operand is the feature row, the narrower the (head) weight.
@@ -1310,33 +1385,85 @@ def run_stream(opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, 
     return ExecResult(ex.values, outputs, dt, ex.alg_bytes, ex.launches), ex
 
 
-SPARSITY = {"cora": 0.012, "pubmed": 0.1, "flickr": 0.46, "reddit": 1}  # code/simulator.py:381-392
+def _tiles_for(graph, sparse=True):
+    """T -> the tile counts of graph for the cost model, cached on the graph object like its plans:
+    sparse (tiles.sparse_counts, O(E)) for the closed-form per-instruction model, or the dense flat
+    list (gta_tile_nnz on the GPU, row-major [ceil(N/T)][n_cols]) the cycle loop walks.  Like the
+    reference's dense adjacency they count a repeated (dst, src) once when rows are column-sorted."""
+    from . import tiles
+    cache = graph.__dict__.setdefault("_tile_nnz_cache", {})
+
+    def tiles_for(T):
+        key = (T, sparse)
+        if key not in cache:
+            cache[key] = (tiles.sparse_counts(graph, int(T)) if sparse
+                          else ops.tile_nnz(graph, int(T)).flatten().cpu().numpy().astype(np.int64))
+        return cache[key]
+    return tiles_for
 
 
 def attach_model(res, stream_records, tile_size_list, graph, model="rw", isSinput=False, dataset=None):
-    """Fill res.model_rw (closed form) and, for model == "full", res.model_cycles via the exact
-    cost-model restatement (costmodel.py).  Tile nnz come from the GPU (gta_tile_nnz); like the
-    reference's dense adjacency they count a repeated (dst, src) once when rows are column-sorted."""
+    """The reference's modelled numbers for the stream just executed (simulate(), code/simulator.py:370-502):
+      "rw"   res.model_rw, the closed form (one tile-count pass at T = N);
+      "inst" also res.model_insts, the per-instruction model (costmodel.per_instruction: each
+             instruction's rw_record bytes and unit-busy cycles, closed form over sparse tile counts:
+             runs at Reddit / products scale), res.model_rw its sum;
+      "full" also res.model_cycles and res.model_spans via the exact cycle-loop restatement
+             (costmodel.simulate_stream with each instruction's first start / last end; Python
+             speed: Cora / Flickr-sized graphs)."""
     from . import costmodel
     if model is None:
         return res
     n = graph.n_rows
-    # tile counts are a property of the CSR: kept on the graph object like its plans, so a
-    # repeated call computes (and synchronises for) them once
-    cache = graph.__dict__.setdefault("_tile_nnz_cache", {})
-
-    def tiles_for(T):
-        if T not in cache:
-            cache[T] = ops.tile_nnz(graph, int(T)).flatten().cpu().tolist()
-        return cache[T]
-    if model == "full":
-        res.model_cycles, res.model_rw = costmodel.simulate_stream(
-            stream_records, tile_size_list, n, tiles_for, isSinput, SPARSITY.get(dataset, 1))
-    else:
+    sp = SPARSITY.get(dataset, 1)
+    if model == "rw":
+        cache = graph.__dict__.setdefault("_tile_nnz_cache", {})
         if ("sum", n) not in cache:
             cache[("sum", n)] = int(ops.tile_nnz(graph, n).sum().item())
         res.model_rw = costmodel.model_rw(stream_records, n, cache[("sum", n)])
+        return res
+    res.model_insts = costmodel.per_instruction(stream_records, tile_size_list, n, _tiles_for(graph), isSinput, sp)
+    res.model_rw = sum(r["rw_bytes"] for r in res.model_insts)
+    if model == "full":
+        res.model_cycles, rw, res.model_spans = costmodel.simulate_stream(
+            stream_records, tile_size_list, n, _tiles_for(graph, sparse=False), isSinput, sp, record=True)
+        assert rw == res.model_rw, (rw, res.model_rw)
     return res
+
+
+def model_trace(res, events=None):
+    """The modelled numbers beside the measured Chrome trace.  Every measured op event gets, in
+    args.model, the stream instructions that execute it (by the op ids in their IDs) with their
+    modelled bytes (rw_record) and unit-busy cycles / µs at the reference's 1 GHz clock
+    (code/start.py:56 reports cycles/1e9 s).  With model="full" the modelled timeline is added as
+    its own tracks: one event per instruction from its first start to its last end, pid
+    "GTA model", tid = the reference's hardware unit (vTCAD/code/simulator.py:360-382 schema)."""
+    insts = getattr(res, "model_insts", None) or []
+    by_op = {}
+    for r in insts:
+        for op in {p[0] for p in ir.parse_id(r["ID"])}:
+            by_op.setdefault(op, []).append({"TYPE": r["TYPE"], "ID": r["ID"], "bytes": r["record_bytes"],
+                                             "busy_cycles": r["busy"], "model_us": r["busy"] / 1e3,
+                                             "iterations": r["starts"]})
+    out = []
+    for e in events or []:
+        e = dict(e, args=dict(e["args"]))
+        e["args"]["model"] = by_op.get(e["args"]["op"], [])
+        out.append(e)
+    spans = getattr(res, "model_spans", None)
+    if spans:
+        for r in insts:
+            sp = spans.get((r["block"], r["index"]))
+            if sp is None:
+                continue
+            out.append({"name": r["TYPE"], "cat": r["ID"], "ph": "X", "ts": sp[0] / 1e3, "dur": (sp[2] - sp[0]) / 1e3,
+                        "pid": "GTA model", "tid": r["unit"],
+                        "args": {"bytes": r["record_bytes"], "busy_cycles": r["busy"], "iterations": r["starts"],
+                                 "block": r["block"]}})
+    return out
+
+
+SPARSITY = {"cora": 0.012, "pubmed": 0.1, "flickr": 0.46, "reddit": 1}  # code/simulator.py:381-392
 
 
 _LOADED = {}
@@ -1360,32 +1487,66 @@ def _load(network, reorder, semantics, op_path, inst_path):
     return hit[1:]
 
 
-def execute(tile_size_list, dataset, network, layer, isReorder, isSinput=False, *, graph, tensors,
-            inst_root="Results/Insts", op_root="Network", inst_path=None, op_path=None, semantics=None,
-            plan_chunk=512, model="rw", trace=None):
+ARCHITECTURES = ("GTA", "HyGCN", "GCNAX", "OPU")  # vTCAD/code/simulator.py:489-509
+
+
+def execute(tile_size_list, dataset, network, layer, isReorder, isSinput=False, isFlexibleHardware=False,
+            architecture_name="GTA", *, graph, tensors, inst_root="Results/Insts", op_root="Network", inst_path=None,
+            op_path=None, semantics=None, plan_chunk=512, model="rw", trace=None):
     """Drop-in for simulate(tile_size_list, dataset, network, layer, isReorder, isSinput)
     (code/simulator.py:370): same leading arguments, same files, real execution.
 
     Returns ExecResult: the sink ops' device tensors, measured elapsed_s, and the
-    reference's modelled numbers for the same stream: model_rw (always, closed
-    form) and model_cycles (model="full"; exact restatement of the cycle loop,
-    Python-speed, meant for Cora/Flickr-sized graphs).  `res.simulate_tuple()`
-    is what simulate() would have returned.  trace: True (events in res.trace) or a path for a
-    Chrome trace JSON of the measured per-op device time, as the reference's chrome_timeline.json.
+    reference's modelled numbers for the same stream (attach_model): model_rw (always, closed
+    form), model_insts (model="inst" or "full": per instruction, the bytes simulate() records in
+    rw_record and the unit-busy cycles, closed form at any graph size) and model_cycles /
+    model_spans (model="full"; exact restatement of the cycle loop, Python-speed, meant for
+    Cora/Flickr-sized graphs).  `res.simulate_tuple()` is what simulate() would have returned.
+    trace: True (events in res.trace) or a path for a Chrome trace JSON of the measured per-op
+    device time, as the reference's chrome_timeline.json, each op event carrying its
+    instructions' modelled bytes and cycles (model_trace; model="full" adds the modelled timeline).
+
+    Also takes vTCAD's call, simulate(tile_size_list, dataset, network, layer, isReorder, isSinput,
+    isFlexibleHardware, architecture_name) (vTCAD/code/simulator.py:423, called positionally at
+    vTCAD/code/test.py:15; bind() gives a callable that takes exactly that line).  The names are
+    checked as vTCAD checks them (:489-510: an unknown architecture is an error -- vTCAD returns -1,
+    this raises) and kept in res.model_arch.  They select the modelled ASIC, not the execution: the
+    GPU runs the same kernels for every architecture, and the modelled numbers restate
+    code/simulator.py's fixed-hardware GTA model; vTCAD's other presets and its per-block search
+    over flexible unit counts are ASIC design-space models outside the hot path.
 
     From the second call with the same stream, CSR and input tensor objects on (graphs of at most
     AUTO_GRAPH_MAX_EDGES edges: every graph by default), the execution replays a captured HIP graph: the outputs are then
     the graph's own tensors and the next such call overwrites them -- clone what must outlive it
     (AUTO_GRAPH = False keeps every call eager, with fresh outputs)."""
+    if architecture_name not in ARCHITECTURES:
+        raise ValueError(f"architecture_name {architecture_name!r}: vTCAD knows {', '.join(ARCHITECTURES)} "
+                         "(vTCAD/code/simulator.py:489-510)")
+    if not isinstance(isFlexibleHardware, (bool, int)):
+        raise TypeError("isFlexibleHardware must be a bool")
     op_path = op_path or ir.op_yaml_path(network, dataset, layer, isReorder, op_root)
     inst_path = inst_path or ir.inst_path(network, dataset, layer, isReorder, inst_root)
     sem, g, records, s = _load(network, isReorder, semantics, op_path, inst_path)
     res, ex = run_stream(g, s, graph, tensors, sem, plan_chunk, trace=trace is not None)
+    # a trace carries the per-instruction model beside the measured ops
+    attach_model(res, records, tile_size_list, graph, "inst" if (trace is not None and model == "rw") else model,
+                 isSinput, dataset)
     if trace is not None:
-        res.trace = ex.trace_events
+        res.trace = model_trace(res, ex.trace_events)
         if isinstance(trace, str):
-            save_chrome_trace(ex.trace_events, trace)
-    return attach_model(res, records, tile_size_list, graph, model, isSinput, dataset)
+            save_chrome_trace(res.trace, trace)
+    # vTCAD turns flexible hardware off for every preset but GTA (:493-507)
+    res.model_arch = (architecture_name, bool(isFlexibleHardware) and architecture_name == "GTA")
+    return res
+
+
+def bind(graph, tensors, **kw):
+    """A simulate()-shaped callable over one graph and its tensors: bind(g, t)(tile_size_list,
+    dataset, network, layer, isReorder, isSinput[, isFlexibleHardware, architecture_name]) -- the
+    reference callers' lines (code/start.py:51, code/genetic_algorithm.py:603, vTCAD/code/test.py:15)
+    unchanged once `simulate` names it."""
+    import functools
+    return functools.partial(execute, graph=graph, tensors=tensors, **kw)
 
 
 class GraphedRun:

@@ -62,6 +62,13 @@ class Graph:
             self._row_of_edge = torch.repeat_interleave(rows, self.degrees())
         return self._row_of_edge
 
+    def csc(self):
+        """Cached CSC view (ops.CSC: edges ordered by source column, built on the device once)."""
+        if "csc" not in self._plans:
+            from . import ops
+            self._plans["csc"] = ops.CSC(self)
+        return self._plans["csc"]
+
     def plan(self, chunk=512):
         """Cached device-side aggregate plan (row chunks of <= chunk edges)."""
         if chunk not in self._plans:

@@ -105,6 +105,7 @@ class OpGraph:
     """
 
     def __init__(self, records, patches=None):
+        self.records = records  # the YAML list as read (the oracle resolves its own data flow from it)
         self.ops = [Op(i, r) for i, r in enumerate(records)]
         self.patches = dict(patches or {})
         self.inputs = [self._resolve(op) for op in self.ops]

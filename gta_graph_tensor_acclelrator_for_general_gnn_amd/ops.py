@@ -2,7 +2,7 @@
 
 One function per ISA op / fused pattern of the GTA stream:
   scatter      ISA `scatter`  (template/ISA_defination.yaml:33-44)        -> gta_scatter
-  gather_add   ISA `gather`   (template/ISA_defination.yaml:46-61)        -> gta_gather_add
+  gather_add   ISA `gather` R/C (template/ISA_defination.yaml:46-61)      -> gta_gather_add (+ gta_csc_build for C)
   aggregate    fused applyedge MUL -> gather ADD (+ removed scatter FETCH)
                (hardware_info.yaml Inst_fused :35-38, code/interpreter.py:575-636, 764-802) -> gta_aggregate
   apply_edge   applyedge ADD/MUL/SF (genGraphOP.py:36, 55-60)              -> gta_apply_edge
@@ -338,17 +338,79 @@ def gat_aggregate_blocked(graph, x, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize
     return out, sums
 
 
-def gather_add(graph, xe, out=None, accumulate=False):
-    """y[i] (+)= sum_{e in row i} xe[e]   (gather R, ADD)."""
+class CSC:
+    """The CSR's edges ordered by SOURCE column (gta_csc_build, ABI 11): colptr int64 [n_cols + 1],
+    perm int32 [E] (CSR edge id at each position), rows int32 [E] (that edge's destination row).
+    Stable: a column's edges keep CSR order, so every sum over them has a fixed order.  Built once
+    per graph on the device (Graph.csc()).  The ISA's DIRECTION src (ORDER C) for gather
+    (template/ISA_defination.yaml:46-48) runs the ordered row kernels over these transposed views."""
+
+    def __init__(self, graph):
+        _need_gpu(graph.indptr)
+        L = _L()
+        dev = graph.device
+        self.graph = graph
+        self.colptr = torch.empty(graph.n_cols + 1, dtype=torch.int64, device=dev)
+        self.perm = torch.empty(graph.nnz, dtype=torch.int32, device=dev)
+        self.rows = torch.empty(graph.nnz, dtype=torch.int32, device=dev)
+        nb = check(L.gta_csc_workspace_bytes(graph.n_cols, graph.nnz), "csc_workspace_bytes")
+        ws = torch.empty(int(nb), dtype=torch.uint8, device=dev)
+        check(L.gta_csc_build(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.n_cols, graph.nnz,
+                              _ptr(self.colptr), _ptr(self.perm), _ptr(self.rows), _ptr(ws), int(nb),
+                              _stream(dev)), "csc_build")
+        self._views = {}
+
+    def view(self, kind):
+        """A Graph over the n_cols source nodes whose row j lists column j's edges in CSC order, with
+        "indices" = what an operand of those edges is read by: "edge" -> the CSR edge id (an edge
+        tensor read as a table of E rows), "dst" -> the destination row (a scatter R operand),
+        "src" -> j itself (a scatter C operand)."""
+        if kind not in self._views:
+            from . import graph as G
+            g = self.graph
+            if kind == "edge":
+                v = G.Graph(self.colptr, self.perm, n_cols=g.nnz)
+            elif kind == "dst":
+                v = G.Graph(self.colptr, self.rows, n_cols=g.n_rows)
+            elif kind == "src":
+                cols = torch.arange(g.n_cols, device=g.device, dtype=torch.int32)
+                v = G.Graph(self.colptr, torch.repeat_interleave(cols, self.colptr[1:] - self.colptr[:-1]),
+                            n_cols=g.n_cols)
+            else:
+                raise ValueError(kind)
+            self._views[kind] = v
+        return self._views[kind]
+
+
+def csc(graph):
+    """graph's cached CSC view (Graph.csc())."""
+    return graph.csc()
+
+
+def gather_add(graph, xe, out=None, accumulate=False, direction="R"):
+    """ISA gather ADD of an edge tensor xe [E, F] (CSR order), both DIRECTIONs (ABI 11):
+    "R": y[i] (+)= sum_{e in row i} xe[e]            (to the destination; y [n_rows, F])
+    "C": y[j] (+)= sum_{e : src(e) = j} xe[e]         (to the source; y [n_cols, F]), summed in the
+         stable CSC order of graph.csc() -- deterministic, no atomics."""
     _need_gpu(xe, out, graph.indptr)
+    if direction not in ("R", "C"):
+        raise ValueError("gather_add: direction must be 'R' or 'C'")
     ldx = _rows(xe, "xe")
     F = xe.shape[1]
     if xe.shape[0] < graph.nnz:
         raise ValueError("xe must be [E, F]")
+    n_out = graph.n_rows if direction == "R" else graph.n_cols
     if out is None:
-        out = (torch.zeros if accumulate else torch.empty)(graph.n_rows, F, dtype=torch.float32, device=xe.device)
+        out = (torch.zeros if accumulate else torch.empty)(n_out, F, dtype=torch.float32, device=xe.device)
     ldy = _rows(out, "out")
-    check(_L().gta_gather_add(_ptr(graph.indptr), graph.n_rows, graph.nnz, _ptr(xe), ldx, F, _ptr(out), ldy,
+    if out.shape[0] < n_out or out.shape[1] != F:
+        raise ValueError(f"out must be [{n_out}, {F}]")
+    colptr = perm = None
+    if direction == "C":
+        c = graph.csc()
+        colptr, perm = c.colptr, c.perm
+    check(_L().gta_gather_add(_lib.DIR_R if direction == "R" else _lib.DIR_C, _ptr(graph.indptr), graph.n_rows,
+                              graph.nnz, _ptr(colptr), _ptr(perm), graph.n_cols, _ptr(xe), ldx, F, _ptr(out), ldy,
                               int(bool(accumulate)), _stream(xe.device)), "gather_add")
     return out
 

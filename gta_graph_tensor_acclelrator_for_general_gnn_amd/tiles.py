@@ -54,6 +54,38 @@ def max_tile(graph, T, dense_limit_bytes=2 << 30):
     return m
 
 
+def sparse_counts(graph, T):
+    """calculate_sparsity(T, 1) of the CSR as costmodel.TileCounts: the nonzero (T-row block, source
+    column) counts with the same rule as gta_tile_nnz (self loops dropped, a column that repeats
+    its row's previous entry counted once), from one sort of the edges' tile keys -- O(E) memory
+    instead of the [ceil(N/T), n_cols] grid.  dense() falls back to gta_tile_nnz (GPU) or a scatter
+    of these counts (CPU)."""
+    from .costmodel import TileCounts
+    nt = -(-graph.n_rows // T)
+    length = nt * graph.n_cols
+    if graph.nnz == 0:
+        return TileCounts(length, np.zeros(0, np.int64), 0, lambda: np.zeros(length, np.int64))
+    rows = graph.row_of_edge().long()
+    cols = graph.indices.long()
+    keep = rows != cols
+    if graph.nnz > 1:  # the previous entry of the same row repeats this column: counted once
+        keep[1:] &= ~((rows[1:] == rows[:-1]) & (cols[1:] == cols[:-1]))
+    keys = (rows[keep] // T) * graph.n_cols + cols[keep]
+    del rows, cols, keep
+    uk, counts = torch.unique(keys, return_counts=True)
+    del keys
+    uk, counts = uk.cpu().numpy(), counts.cpu().numpy().astype(np.int64)
+    first = int(counts[0]) if uk.size and uk[0] == 0 else 0
+
+    def dense():
+        if graph.device.type == "cuda":
+            return ops.tile_nnz(graph, T).flatten().cpu().numpy()
+        d = np.zeros(length, np.int64)
+        d[uk] = counts
+        return d
+    return TileCounts(length, counts, first, dense)
+
+
 def metadata(graph, start=64, end=None):
     """(sizelist, maxlist) as preprocessing.py writes them for compile()."""
     end = graph.n_rows if end is None else end

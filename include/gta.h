@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 10 /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+#define GTA_ABI_VERSION 11 /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
                               hooks; 4: knob sets attached to streams (gta_tuning_*); 5: every UPDATE
                               on hand-written kernels (no vendor library), gta_update_mm_t_splits,
                               the blocked workspace is the slab rows alone and required, bf16
@@ -46,7 +46,8 @@ extern "C" {
                               gta_aggregate_self (the aggregate with a scaled self term); 8:
                               gta_update_mm_t_splits takes the stream (its attached knob set); 9:
                               gta_update_mlp (two chained node GEMMs in one pass); 10: bf16 y of
-                              gta_aggregate_self, bf16 x of gta_update_mlp */
+                              gta_aggregate_self, bf16 x of gta_update_mlp; 11: gta_gather_add takes the ISA
+                              DIRECTION (dir R / C) and the CSC view of gta_csc_build */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -216,12 +217,34 @@ int gta_gat_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int
                               float* y, int64_t ldy, float* sums, const void* plan, int64_t blocks, int64_t item_edges,
                               void* workspace, void* stream);
 
-/* ---- K2 GATHER ADD (edge -> node) ---------------------------------------
- * y[i, :] (+)= sum_{e in row i} xe[e, :]    == gta_aggregate(x_mode=EDGE, w=NULL)
- * Reference: gather ISA template/ISA_defination.yaml:46-61; LOAD_E + Virtual
- * LOAD_N + COMP_ADD + STORE_N, code/interpreter.py:329-334, 373-375. */
-int gta_gather_add(const int64_t* indptr, int64_t n_rows, int64_t nnz, const float* xe, int64_t ldxe,
-                   int64_t F, float* y, int64_t ldy, int accumulate, void* stream);
+/* ---- CSC view of the CSR (ABI 11) -----------------------------------------
+ * The edges ordered by SOURCE column, for the ISA gather / scatter with DIRECTION src
+ * ("column-wise", template/ISA_defination.yaml:35, :48; ORDER C in the op YAML, lowered by
+ * code/interpreter.py:55-129): colptr int64 [n_cols+1] (column j's edges are positions
+ * colptr[j] .. colptr[j+1]-1), perm int32 [nnz] = the CSR edge id at each position, and
+ * optionally rows int32 [nnz] = that edge's destination row (NULL: not written).  Stable:
+ * within a column, edges keep their CSR order (increasing destination row), so the result is a
+ * pure function of the CSR and every consumer's sum order is fixed.  A device LSD radix sort
+ * (8-bit digits, ceil(log2(n_cols)/8) passes, no order decided by atomics); built once per graph.
+ * indices must lie in [0, n_cols) (colptr[n_cols] == nnz then); nnz < 2^31.
+ * workspace >= gta_csc_workspace_bytes(n_cols, nnz). */
+int64_t gta_csc_workspace_bytes(int64_t n_cols, int64_t nnz);
+int gta_csc_build(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols, int64_t nnz,
+                  int64_t* colptr, int32_t* perm, int32_t* rows, void* workspace, int64_t workspace_bytes,
+                  void* stream);
+
+/* ---- K2 GATHER ADD (edge -> node), both ISA directions (ABI 11) -----------
+ * dir GTA_DIR_R: y[i, :] (+)= sum_{e in row i} xe[e, :]          (to the destination, y [n_rows])
+ *                == gta_aggregate(x_mode=EDGE, w=NULL); colptr / perm unused (may be NULL).
+ * dir GTA_DIR_C: y[j, :] (+)= sum_{e : src(e) = j} xe[e, :]      (to the source, y [n_cols])
+ *                summed in CSC order (colptr / perm of gta_csc_build): deterministic, no atomics.
+ * xe is an edge tensor [nnz, F] in CSR order.
+ * Reference: gather ISA DIRECTION dst/src template/ISA_defination.yaml:46-61; LOAD_E + Virtual
+ * LOAD_N + COMP_ADD + STORE_N, code/interpreter.py:329-334, 373-375; tile counts per ORDER,
+ * code/interpreter.py:55-129 (STORE_N of ORDER C: TR*TC x SC). */
+int gta_gather_add(int dir, const int64_t* indptr, int64_t n_rows, int64_t nnz, const int64_t* colptr,
+                   const int32_t* perm, int64_t n_cols, const float* xe, int64_t ldxe, int64_t F, float* y,
+                   int64_t ldy, int accumulate, void* stream);
 
 /* ---- K3' fused GAT edge-softmax (ops 6-10 of the GAT op graph) ------------
  * v(e, h)     = sf( a_dst[dst(e), h] + b_src[src(e), h] )       (ops 6 ADD, 7 SF)

@@ -2,13 +2,22 @@
 
 Ignores blocks and fusion entirely: every op is evaluated unfused, in the op
 graph's data-flow order, with the ISA semantics of oracle/isa_ref.py.  The
-data flow (which op feeds which slot) and the per-network semantic choices
-are the spec objects ir.OpGraph / semantics.Semantics; all arithmetic here is
-independent of the product code.
+data flow (which op feeds which slot) is resolved here from the raw YAML records
+(opgraph.records) by oracle/opgraph_ref.py, not taken from the product's
+ir.OpGraph resolution; the per-network choices the YAML leaves open (which SF,
+GAT op 9's "/", GAT op 10's input patch) come from semantics.Semantics, the
+written spec.  All arithmetic here is independent of the product code.
 """
 import numpy as np
 
-from . import isa_ref
+from . import isa_ref, opgraph_ref
+
+
+class _OpView:  # what Semantics.sf_of / bin_of read: position and COMP_TYPE
+    __slots__ = ("idx", "comp")
+
+    def __init__(self, idx, comp):
+        self.idx, self.comp = idx, comp
 
 
 def _as_operand(t, n, e):
@@ -31,14 +40,18 @@ def execute_ref(opgraph, sem, indptr, indices, tensors):
     ip, ix = np.asarray(indptr, np.int64), np.asarray(indices, np.int64)
     vals = {}
 
+    recs = opgraph.records
+    patches = getattr(opgraph, "patches", None) or {}
+    flow = opgraph_ref.dataflow(recs, patches)
+
     def src(op, slot):
-        s = opgraph.inputs[op.idx][slot]
-        if s.kind == "op":
-            return vals[s.op]
+        kind, ref = flow[op.idx][slot]
+        if kind == "op":
+            return vals[ref]
         key = f"ext:{op.idx}:{slot}"
         if key in tensors:
             return _as_operand(tensors[key], n, e)
-        if s.kind == "ext":
+        if kind == "ext":
             raise KeyError(key)
         if op.type == "applyedge":
             return ("edge", np.asarray(tensors["x_edge"], np.float64))
@@ -60,13 +73,18 @@ def execute_ref(opgraph, sem, indptr, indices, tensors):
             return np.broadcast_to(t, (n, t.shape[1]))
         raise TypeError("edge value used as a node operand")
 
-    for i in opgraph.topo():
-        op = opgraph.ops[i]
-        nin = len(opgraph.inputs[i])
+    class _Rec:
+        __slots__ = ("idx", "type", "comp", "order")
+
+    for i in opgraph_ref.topo(recs, patches):
+        r = recs[i]
+        op = _Rec()
+        op.idx, op.type, op.comp, op.order = i, r["TYPE"], r.get("COMP_TYPE", "NONE"), r.get("ORDER", "R")
+        nin = len(flow[i])
         if op.type == "scatter":
             vals[i] = ("edge", isa_ref.scatter(ip, ix, node_rows(src(op, 0)), "R" if op.order == "R" else "C"))
         elif op.type == "gather":
-            vals[i] = ("node", isa_ref.gather_add(ip, edge_rows(src(op, 0))))
+            vals[i] = ("node", isa_ref.gather_add(ip, edge_rows(src(op, 0)), "C" if op.order == "C" else "R", ix))
         else:
             edge = op.type == "applyedge"
             rows = edge_rows if edge else node_rows
@@ -78,9 +96,9 @@ def execute_ref(opgraph, sem, indptr, indices, tensors):
                     W = W.astype(np.float64)
                 vals[i] = (kind, X @ W)
             elif op.comp == "SF":
-                vals[i] = (kind, isa_ref.sf(sem.sf_of(op), rows(src(op, 0))))
+                vals[i] = (kind, isa_ref.sf(sem.sf_of(_OpView(i, op.comp)), rows(src(op, 0))))
             else:
-                b = sem.bin_of(op)
+                b = sem.bin_of(_OpView(i, op.comp))
                 ins = [src(op, s) for s in range(nin)]
                 if len(ins) == 1 and f"ext:{i}:1" in tensors:
                     ins.append(_as_operand(tensors[f"ext:{i}:1"], n, e))

@@ -36,11 +36,19 @@ def scatter(indptr, indices, x, direction):
     return edge_operand(indptr, indices, x, "dst" if direction == "R" else "src").copy()
 
 
-def gather_add(indptr, xe):
-    """ISA `gather` R with COMPUTE mul: add (template/ISA_defination.yaml:46-61)."""
-    n = len(indptr) - 1
+def gather_add(indptr, xe, direction="R", indices=None, n_cols=None):
+    """ISA `gather` with COMPUTE mul: add (template/ISA_defination.yaml:46-61), DIRECTION dst/src
+    (:48): "R" sums each edge row into its destination row (y [N]), "C" into its source column
+    (y [n_cols], "from edges to src (column-wise)"; needs indices, n_cols defaults to N)."""
+    if direction == "R":
+        out = np.zeros((len(indptr) - 1, xe.shape[1]), dtype=np.float64)
+        np.add.at(out, row_of_edge(indptr), xe.astype(np.float64))
+        return out
+    if direction != "C" or indices is None:
+        raise ValueError("gather_add: direction 'R', or 'C' with indices")
+    n = len(indptr) - 1 if n_cols is None else n_cols
     out = np.zeros((n, xe.shape[1]), dtype=np.float64)
-    np.add.at(out, row_of_edge(indptr), xe.astype(np.float64))
+    np.add.at(out, np.asarray(indices, dtype=np.int64), xe.astype(np.float64))
     return out
 
 
@@ -78,7 +86,8 @@ def binop(kind, a, b):
     if kind == "MUL":
         return a * b
     if kind == "DIV":
-        return a / b
+        with np.errstate(divide="ignore", invalid="ignore"):  # 0/0 at isolated nodes (GAT-trans op 11) is expected
+            return a / b
     if kind == "SUB":
         return a - b
     raise ValueError(kind)

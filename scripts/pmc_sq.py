@@ -1,7 +1,10 @@
-"""SQ / TCC counters of the metric launches (k_agg_h32 + k_seg_reduce), one rocprofv3 --pmc pass
-per counter group (each within the per-block slot limits), over `bench.py --pmc-child` (the bench's
-own inputs and launches).  Per-kernel means over the launches after the first (cold) one.
-Usage: python scripts/pmc_sq.py OUT_DIR  -> OUT_DIR/<group>/... CSVs and OUT_DIR/summary.json"""
+"""SQ / TA / TD / TCC counters of a hot launch, one rocprofv3 --pmc pass per counter group (each
+within the per-block slot limits).  Targets (PMC_TARGET):
+  metric (default) -- `bench.py --pmc-child`: the bench's own inputs and launches (k_agg_h32 + k_seg_reduce)
+  gin              -- `scripts/gin_pmc.py --child --no-calib`: GIN products' aggregate exactly as the
+                      layer launches it (k_aggregate<..., ushort> of gta_aggregate_self, bf16 y)
+Per-kernel means over the launches after the first (cold) one.
+Usage: python scripts/pmc_sq.py OUT_DIR [bench args]  -> OUT_DIR/<group>/... CSVs and OUT_DIR/summary.json"""
 import csv
 import glob
 import json
@@ -21,7 +24,17 @@ GROUPS = {
     "tex": ["TA_TA_BUSY_sum", "TA_ADDR_STALLED_BY_TC_CYCLES_sum", "TD_TD_BUSY_sum", "TD_TC_STALL_sum",
             "TCP_TCC_READ_REQ_LATENCY_sum", "TCP_TCC_READ_REQ_sum", "TCP_PENDING_STALL_CYCLES_sum", "GRBM_GUI_ACTIVE"],
 }
-KERNELS = ("k_agg_h32", "k_seg_reduce")
+TARGETS = {
+    "metric": (["bench.py", "--pmc-child", "--steps", "4"], ("k_agg_h32", "k_seg_reduce")),
+    "gin": (["scripts/gin_pmc.py", "--child", "--no-calib"], ("k_aggregate",)),
+}
+TARGET = os.environ.get("PMC_TARGET", "metric")
+KERNELS = TARGETS[TARGET][1]
+
+
+def _kernel(name):
+    """The KERNELS entry a dispatch belongs to (a combine / reduce helper only when named)."""
+    return next((k for k in KERNELS if k in name and ("combine" in k or "combine" not in name)), None)
 
 
 def summarize(d):
@@ -29,7 +42,7 @@ def summarize(d):
     for f in glob.glob(os.path.join(d, "**", "*counter_collection*.csv"), recursive=True):
         for row in csv.DictReader(open(f)):
             name = row.get("Kernel_Name", "")
-            k = next((k for k in KERNELS if k in name), None)
+            k = _kernel(name)
             if k is None:
                 continue
             did = int(row.get("Dispatch_Id") or row.get("Correlation_Id") or 0)
@@ -47,14 +60,15 @@ EXTRA = []  # bench.py arguments after OUT_DIR (e.g. --blocks 16 --knobs seg_lea
 
 def main(out_dir):
     os.makedirs(out_dir, exist_ok=True)
-    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"))
+    env = dict(os.environ, TMPDIR=os.environ.get("TMPDIR", "/tmp"), GIN_PMC_META=os.path.join(out_dir, "meta.json"))
+    script = TARGETS[TARGET][0]
     summary = {}
     for gname, counters in GROUPS.items():
         d = os.path.join(out_dir, gname)
         shutil.rmtree(d, ignore_errors=True)
         cmd = ["timeout", "-s", "KILL", "120", shutil.which("rocprofv3") or "rocprofv3", "--kernel-trace", "--pmc",
                *counters, "--output-format", "csv", "-d", d, "-o", "run", "--", sys.executable,
-               os.path.join(ROOT, "bench.py"), "--pmc-child", "--steps", "4", *EXTRA]
+               os.path.join(ROOT, script[0]), *script[1:], *EXTRA]
         p = subprocess.run(cmd, env=env, cwd=ROOT, capture_output=True, text=True)
         print(gname, "rc", p.returncode, p.stderr[-300:] if p.returncode else "", flush=True)
         if p.returncode != 0:

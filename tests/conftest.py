@@ -19,11 +19,22 @@ def golden_dir():
     return GOLDEN
 
 
+_MANIFEST = []
+
+
+def load_manifest():
+    """tests/golden/manifest.json, read once: test modules parametrize over its entries at
+    collection time (one test per golden stream / candidate list, no placeholder skips)."""
+    if not _MANIFEST:
+        import json
+        with open(os.path.join(GOLDEN, "manifest.json")) as f:
+            _MANIFEST.append(json.load(f))
+    return _MANIFEST[0]
+
+
 @pytest.fixture(scope="session")
 def manifest():
-    import json
-    with open(os.path.join(GOLDEN, "manifest.json")) as f:
-        return json.load(f)
+    return load_manifest()
 
 
 @pytest.fixture(scope="session")

@@ -46,8 +46,43 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
     return _t(y)
 
 
-def gather_add(graph, xe, out=None, accumulate=False):
+def gather_add(graph, xe, out=None, accumulate=False, direction="R"):
+    if direction == "C":
+        ip, ix = graph.numpy()
+        y = isa_ref.gather_add(ip, _np(xe), "C", ix, graph.n_cols)
+        if out is not None:
+            out.copy_(_t(y + (_np(out) if accumulate else 0)))
+            return out
+        return _t(y)
     return aggregate(graph, xe, "edge", None, out=out, accumulate=accumulate)
+
+
+class _CSC:
+    """CPU stand-in of ops.CSC: numpy's stable argsort by source column (the same permutation the
+    device radix sort builds)."""
+
+    def __init__(self, graph):
+        from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G
+        ip, ix = graph.numpy()
+        perm = np.argsort(ix, kind="stable")
+        colptr = np.zeros(graph.n_cols + 1, np.int64)
+        np.cumsum(np.bincount(ix, minlength=graph.n_cols), out=colptr[1:])
+        rows = isa_ref.row_of_edge(ip)[perm]
+        cols = np.sort(ix, kind="stable")
+        self.colptr, self.perm, self.rows = colptr, perm, rows
+        self._views = {"edge": G.from_numpy(colptr, perm, n_cols=graph.nnz),
+                       "dst": G.from_numpy(colptr, rows, n_cols=graph.n_rows),
+                       "src": G.from_numpy(colptr, cols, n_cols=graph.n_cols)}
+
+    def view(self, kind):
+        return self._views[kind]
+
+
+def csc(graph):
+    c = graph._plans.get("fake_csc")
+    if c is None:
+        c = graph._plans["fake_csc"] = _CSC(graph)
+    return c
 
 
 def scatter(graph, x, direction, out=None):

@@ -26,7 +26,8 @@ def lib():
 def test_header_declares_the_boundary():
     syms = declared_symbols()
     for s in ("gta_abi_version", "gta_last_error", "gta_scatter", "gta_gather_add", "gta_aggregate",
-              "gta_apply_edge", "gta_apply_node", "gta_update_mm", "gta_tile_nnz", "gta_aggregate_plan_build"):
+              "gta_apply_edge", "gta_apply_node", "gta_update_mm", "gta_tile_nnz", "gta_aggregate_plan_build",
+              "gta_csc_build", "gta_csc_workspace_bytes"):
         assert s in syms
 
 
@@ -45,6 +46,12 @@ def test_abi_version_and_error_path(lib):
     assert b"aggregate" in lib.gta_last_error()
     assert lib.gta_aggregate_plan_bytes(100, 1000, 64) > 0
     assert lib.gta_aggregate_plan_bytes(100, 1000, 0) < 0
+    # ABI 11: gather C without the CSC view, a CSC build without workspace, a bad direction
+    assert lib.gta_gather_add(1, None, 10, 10, None, None, 10, None, 0, 4, None, 0, 0, None) < 0
+    assert b"CSC" in lib.gta_last_error()
+    assert lib.gta_gather_add(7, None, 10, 10, None, None, 10, None, 0, 4, None, 0, 0, None) < 0
+    assert lib.gta_csc_workspace_bytes(100, 1000) > 0 and lib.gta_csc_workspace_bytes(-1, 0) < 0
+    assert lib.gta_csc_build(None, None, 10, 10, 100, None, None, None, None, 0, None) < 0
 
 
 def test_product_path_refuses_cpu_tensors():

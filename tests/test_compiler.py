@@ -5,17 +5,13 @@ import pytest
 
 from gta_graph_tensor_acclelrator_for_general_gnn_amd import compiler, ir
 
+from .conftest import load_manifest
 
-def _cases(manifest):
-    return sorted(manifest["compile"].items())
+CASES = sorted(load_manifest()["compile"].items())
 
 
-@pytest.mark.parametrize("idx", range(45))
-def test_candidates_match_reference(golden_dir, manifest, idx):
-    cases = _cases(manifest)
-    if idx >= len(cases):
-        pytest.skip("fewer cases")
-    key, gold = cases[idx]
+@pytest.mark.parametrize("key,gold", CASES, ids=[k.replace("/", "_") for k, _ in CASES])
+def test_candidates_match_reference(golden_dir, manifest, key, gold):
     sizes = manifest["tiles"]["gen_size_64_2708"]
     maxl = manifest["tiles"]["maxlist"]
     if "error" in gold:  # reference raised (GCN-trans: feature_number shorter than its inputs)

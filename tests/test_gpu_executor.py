@@ -15,6 +15,7 @@ from gta_graph_tensor_acclelrator_for_general_gnn_amd.semantics import Semantics
 from oracle import isa_ref
 from oracle.exec_ref import execute_ref
 
+from .conftest import load_manifest
 from .test_ir_executor_cpu import compare
 
 pytestmark = pytest.mark.gpu
@@ -45,12 +46,12 @@ def _run(golden_dir, rec, ip, ix, dev, seed, plan_chunk):
     return res
 
 
-@pytest.mark.parametrize("idx", range(0, 160))
+STREAMS = _all_streams(load_manifest())
+
+
+@pytest.mark.parametrize("idx", range(len(STREAMS)), ids=[r["file"][:-5] for r in STREAMS])
 def test_executor_golden_stream_on_gpu(golden_dir, manifest, cora, dev, idx):
-    streams = _all_streams(manifest)
-    if idx >= len(streams):
-        pytest.skip("fewer streams")
-    rec = streams[idx]
+    rec = STREAMS[idx]
     ip, ix = cora
     res = _run(golden_dir, rec, ip, ix, dev, seed=idx, plan_chunk=64 if idx % 2 else 512)
     assert res.launches > 0 and res.alg_bytes > 0

@@ -1236,3 +1236,86 @@ def test_update_mlp_bitwise(dev, M, K1, N1, N2, sf1, sf2):
     ref = isa_ref.mm(zg, w2.double().cpu().numpy(), sf_kind=sf2)
     _check(fused, ref, np.abs(zg) @ np.abs(w2.double().cpu().numpy()), "update_mlp")
     assert np.abs(zb - zg).max() <= 2 ** -7 * np.abs(zb).max() + 1e-6  # neighbouring bf16 values at most
+
+
+# ---- ABI 11: the CSC view and the ISA gather with DIRECTION src (ORDER C) ----------------------
+def _csc_cases():
+    """(name, indptr, indices, n_cols): lognormal rows, empty rows and columns, duplicate edges, self
+    loops, one heavy row, a rectangular CSR, n_cols needing 1, 2 and 3 radix passes, no edges."""
+    out = []
+    g = G.synthetic(3000, 40000, seed=1)
+    ip, ix = g.numpy()
+    out.append(("lognormal", ip, ix, 3000))
+    rng = np.random.default_rng(2)
+    deg = rng.integers(0, 6, 200)
+    deg[[3, 50, 199]] = 0
+    deg[100] = 9000  # one heavy row
+    ip2 = np.concatenate([[0], np.cumsum(deg)]).astype(np.int64)
+    ix2 = rng.integers(0, 200, int(ip2[-1])).astype(np.int32)  # duplicates and self loops
+    ix2[ip2[10]:ip2[11]] = 10
+    out.append(("dup_self_heavy", ip2, ix2, 200))
+    out.append(("rect_wide", ip2, rng.integers(0, 70000, int(ip2[-1])).astype(np.int32), 70000))  # 2 passes
+    out.append(("three_passes", ip2, rng.integers(0, 1 << 20, int(ip2[-1])).astype(np.int32), (1 << 20) + 3))
+    out.append(("one_col", ip2, np.zeros(int(ip2[-1]), np.int32), 1))
+    out.append(("no_edges", np.zeros(51, np.int64), np.zeros(0, np.int32), 50))
+    return out
+
+
+@pytest.mark.parametrize("case", range(6))
+def test_csc_build_is_the_stable_source_sort(dev, case):
+    """gta_csc_build == numpy's stable argsort by source column, bit-exact (perm, colptr, rows)."""
+    name, ip, ix, nc = _csc_cases()[case]
+    g = G.from_numpy(ip, ix, device=dev, n_cols=nc)
+    c = ops.CSC(g)
+    perm = np.argsort(ix, kind="stable")
+    colptr = np.concatenate([[0], np.cumsum(np.bincount(ix, minlength=nc))]).astype(np.int64)
+    assert np.array_equal(c.colptr.cpu().numpy(), colptr), name
+    assert np.array_equal(c.perm.cpu().numpy(), perm), name
+    assert np.array_equal(c.rows.cpu().numpy(), isa_ref.row_of_edge(ip)[perm]), name
+    c2 = ops.CSC(g)  # a pure function of the graph
+    assert torch.equal(c.perm, c2.perm) and torch.equal(c.colptr, c2.colptr)
+
+
+@pytest.mark.parametrize("case", [0, 1, 2, 4, 5])
+@pytest.mark.parametrize("F", [1, 16, 128, 130])
+def test_gather_add_direction_c(dev, case, F):
+    """gather C: y[j] = sum_{e: src(e) = j} xe[e] vs the fp64 oracle (per-element bound), repeat
+    runs bitwise equal, accumulate; empty columns are 0 (or keep y)."""
+    name, ip, ix, nc = _csc_cases()[case]
+    g = G.from_numpy(ip, ix, device=dev, n_cols=nc)
+    rng = np.random.default_rng(F)
+    xe = rng.standard_normal((len(ix), F)).astype(np.float32)
+    xd = torch.from_numpy(xe).to(dev)
+    y = ops.gather_add(g, xd, direction="C")
+    ref = isa_ref.gather_add(ip, xe, "C", ix, nc)
+    _check(y, ref, isa_ref.gather_add(ip, np.abs(xe), "C", ix, nc), f"gather C {name} F={F}")
+    assert torch.equal(y, ops.gather_add(g, xd, direction="C"))
+    y0 = rng.standard_normal((nc, F)).astype(np.float32)
+    yd = torch.from_numpy(y0).to(dev)
+    ops.gather_add(g, xd, out=yd, accumulate=True, direction="C")
+    _check(yd, y0 + ref, np.abs(y0) + isa_ref.gather_add(ip, np.abs(xe), "C", ix, nc), f"gather C acc {name}")
+    # direction R through the same entry point
+    if case != 5:
+        _check(ops.gather_add(g, xd, direction="R"), isa_ref.gather_add(ip, xe), isa_ref.gather_add(ip, np.abs(xe)),
+               f"gather R {name}")
+
+
+@pytest.mark.parametrize("kind", ["dst", "src", "edge"])
+def test_csc_views_aggregate(dev, kind):
+    """The transposed aggregate the executor runs for gather C of a fused producer: weighted sums
+    over a source column's edges of x[dst(e)] (scatter R), x[src(e)] (scatter C) or xe[e]."""
+    name, ip, ix, nc = _csc_cases()[1]
+    n = len(ip) - 1
+    g = G.from_numpy(ip, ix, device=dev, n_cols=nc)
+    c = ops.CSC(g)
+    rng = np.random.default_rng(3)
+    w = rng.random((len(ix), 4)).astype(np.float32)
+    wc = ops.apply_edge(c.view("edge"), None, None, torch.from_numpy(w).to(dev), "src")
+    assert torch.equal(wc.cpu(), torch.from_numpy(w[np.argsort(ix, kind="stable")]))  # a bit-exact permuting copy
+    rows = {"dst": n, "src": nc, "edge": len(ix)}[kind]
+    x = rng.standard_normal((rows, 32)).astype(np.float32)
+    y = ops.aggregate(c.view(kind), torch.from_numpy(x).to(dev), "src", wc, plan=64)
+    mode = {"dst": "dst", "src": "src", "edge": "edge"}[kind]
+    xe = isa_ref.edge_operand(ip, ix, x.astype(np.float64), mode) * np.repeat(w, 8, axis=1)
+    ref = isa_ref.gather_add(ip, xe, "C", ix, nc)
+    _check(y, ref, isa_ref.gather_add(ip, np.abs(xe), "C", ix, nc), f"csc view {kind}")

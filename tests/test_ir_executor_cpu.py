@@ -15,6 +15,7 @@ from gta_graph_tensor_acclelrator_for_general_gnn_amd.semantics import Semantics
 from oracle.exec_ref import execute_ref
 
 from . import fake_ops
+from .conftest import load_manifest
 
 
 def _streams(manifest, dataset="cora"):
@@ -76,12 +77,12 @@ def compare(values_ex, ref, ops_to_check, rtol=1e-4):
         assert err <= rtol, f"op {i}: normalised max err {err:.2e}"
 
 
-@pytest.mark.parametrize("idx", range(0, 160, 1))
+CORA_STREAMS = _streams(load_manifest())
+
+
+@pytest.mark.parametrize("idx", range(len(CORA_STREAMS)), ids=[r["file"][:-5] for r in CORA_STREAMS])
 def test_executor_plans_every_golden_stream(golden_dir, manifest, monkeypatch, idx):
-    streams = _streams(manifest)
-    if idx >= len(streams):
-        pytest.skip("fewer streams")
-    rec = streams[idx]
+    rec = CORA_STREAMS[idx]
     monkeypatch.setattr(executor, "ops", fake_ops)
     g, ip, ix = _cora_graph(golden_dir)
     sem = Semantics.for_network(rec["network"], rec["reorder"])
@@ -351,3 +352,66 @@ def test_mlp_chain_fusion_cpu(golden_dir, manifest, monkeypatch, layer):
         n_self, n_bf = fake_ops.SELF_TERM_CALLS[0] - st_calls, fake_ops.BF16_OUT_CALLS[0] - bf_calls
         assert n_bf == (n_self if fuse else 0) and (not fuse or n_self == 1), (fuse, n_self, n_bf)
         compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
+
+
+def _vtcad_case(golden_dir, manifest, tmp_path):
+    """vTCAD/code/test.py:6-14's set-up (GIN, cora, layer3, original order): the op YAML at the
+    reference path and the stream interpret() writes for the compiler's best candidate."""
+    import shutil
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import lowering
+    data_set, network, layer, isReorder = "cora", "GIN", "layer3", False
+    path = ir.op_yaml_path(network, data_set, layer, isReorder)
+    os.makedirs(os.path.dirname(path))
+    shutil.copy(os.path.join(golden_dir, "ops", "GIN-cora-layer3-original.yaml"), path)
+    best = manifest["compile"]["GIN-cora-layer3-original"]["top"][0]
+    op_array, tile_size_list = best[0], best[1]
+    lowering.interpret(data_set, network, isReorder, layer, op_array, tile_size_list)
+    return data_set, network, layer, isReorder, tile_size_list, path
+
+
+def test_vtcad_simulate_call_runs_unchanged(golden_dir, manifest, monkeypatch, tmp_path):
+    """vTCAD's eight-argument simulate() line (vTCAD/code/test.py:15, vTCAD/code/simulator.py:423)
+    runs against execute() as written once `simulate` is bound to a graph and its tensors; the
+    architecture name is checked as vTCAD checks it; outputs match the fp64 oracle."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    monkeypatch.chdir(tmp_path)
+    data_set, network, layer, isReorder, tile_size_list, path = _vtcad_case(golden_dir, manifest, tmp_path)
+    g, ip, ix = _cora_graph(golden_dir)
+    sem = Semantics.for_network(network, isReorder)
+    og = ir.OpGraph.load(path, sem.inputs)
+    tensors = workloads.make_tensors(og, g, network, seed=0)
+    simulate = executor.bind(g, tensors, model="full")
+    res = simulate(tile_size_list,data_set,network,layer,isReorder,False,True,'GTA')  # noqa: E231  (verbatim)
+    assert res.model_arch == ("GTA", True)
+    assert res.model_cycles > 0 and res.model_rw == sum(r["rw_bytes"] for r in res.model_insts)
+    ref = execute_ref(og, sem, ip, ix, {k: v.numpy() for k, v in tensors.items()})
+    for k, v in res.outputs.items():
+        compare({k: v}, ref, [k])
+    for arch in ("HyGCN", "GCNAX", "OPU"):
+        assert simulate(tile_size_list, data_set, network, layer, isReorder, False, True, arch).model_arch == (arch, False)
+    with pytest.raises(ValueError):
+        simulate(tile_size_list, data_set, network, layer, isReorder, False, True, "TPU")
+    # the six-argument call of code/simulator.py:370 (code/start.py:51) through the same binding
+    assert executor.bind(g, tensors)(tile_size_list, data_set, network, layer, isReorder, False).model_rw == res.model_rw
+
+
+def test_trace_carries_the_per_instruction_model(golden_dir, manifest, monkeypatch, tmp_path):
+    """execute(..., trace=...) puts each op's stream instructions, with their modelled bytes and
+    busy cycles, on the measured op event; model="full" adds the modelled timeline tracks."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    monkeypatch.chdir(tmp_path)
+    data_set, network, layer, isReorder, tile_size_list, path = _vtcad_case(golden_dir, manifest, tmp_path)
+    g, _, _ = _cora_graph(golden_dir)
+    sem = Semantics.for_network(network, isReorder)
+    tensors = workloads.make_tensors(ir.OpGraph.load(path, sem.inputs), g, network, seed=0)
+    res = executor.execute(tile_size_list, data_set, network, layer, isReorder, graph=g, tensors=tensors,
+                           trace=str(tmp_path / "trace.json"))
+    measured = [e for e in res.trace if e["pid"] == "MI355X"]
+    assert measured and all(e["args"]["model"] for e in measured)
+    assert sum(m["bytes"] for e in measured for m in e["args"]["model"]) > 0
+    assert sum(r["rw_bytes"] for r in res.model_insts) == res.model_rw
+    full = executor.execute(tile_size_list, data_set, network, layer, isReorder, graph=g, tensors=tensors,
+                            model="full", trace=True)
+    model_ev = [e for e in full.trace if e["pid"] == "GTA model"]
+    assert len(model_ev) == sum(1 for r in full.model_insts if r["starts"] > 0)
+    assert max(e["ts"] + e["dur"] for e in model_ev) * 1e3 <= full.model_cycles + 1

@@ -5,17 +5,17 @@ import pytest
 
 from gta_graph_tensor_acclelrator_for_general_gnn_amd import ir, lowering
 
+from .conftest import load_manifest
 
-def _recs(manifest):
-    return [s for s in manifest["streams"]]
+STREAMS = load_manifest()["streams"]
 
 
-@pytest.mark.parametrize("idx", range(170))
-def test_stream_bytes_match_reference(golden_dir, manifest, idx):
-    recs = _recs(manifest)
-    if idx >= len(recs):
-        pytest.skip("fewer streams")
-    rec = recs[idx]
+def _sid(rec):
+    return rec.get("file") or f"{rec['network']}-{rec['dataset']}-layer{rec['layer']}-err-{rec['op_array']}"
+
+
+@pytest.mark.parametrize("rec", STREAMS, ids=[_sid(r) for r in STREAMS])
+def test_stream_bytes_match_reference(golden_dir, manifest, rec):
     m = "trans" if rec["reorder"] else "original"
     op_file = f"{rec['network']}-{rec['dataset']}-layer{rec['layer']}-{m}.yaml"
     records = ir.read_yaml(os.path.join(golden_dir, "ops", op_file))
