@@ -133,7 +133,6 @@ class Aggregate:
 
     def step(self):
         g, works = self.s.grid, []
-        nccl = self.backend == "nccl"
         for c in range(len(self.parts)):
             self.launch(c)
             a, b, _ = self.parts[c]
@@ -142,23 +141,35 @@ class Aggregate:
             if self.mode == "edges" and self.pc > 1:
                 p0, p1 = g.part(c)
                 own = self.y_own[p0:p1]
-                if nccl:  # RCCL reduce-scatter among the pc ranks of this row group
-                    works.append(dist.reduce_scatter_tensor(own, self.y[a:b], group=self.group, async_op=True))
-                else:     # gloo (CPU / one-GPU rehearsal): no reduce-scatter
-                    part = self.y[a:b].clone()
-                    dist.all_reduce(part, group=self.group)
-                    own.copy_(part[g.j * (p1 - p0):(g.j + 1) * (p1 - p0)])
+                # reduce-scatter among the pc ranks of this row group (RCCL on the GPUs; the gloo
+                # rehearsals run the same call)
+                works.append(dist.reduce_scatter_tensor(own, self.y[a:b], group=self.group, async_op=True))
             elif self.mode == "rows" and self.world > 1:
                 w = self.world * g.mk
                 out = self.y_full[c * w:(c + 1) * w]
-                if nccl:
-                    works.append(dist.all_gather_into_tensor(out, self.y[a:b], async_op=True))
-                else:
-                    parts = [torch.empty_like(self.y[a:b]) for _ in range(self.world)]
-                    dist.all_gather(parts, self.y[a:b].contiguous())
-                    out.copy_(torch.cat(parts))
+                works.append(dist.all_gather_into_tensor(out, self.y[a:b], async_op=True))
         for wk in works:
             wk.wait()
+
+
+def layers_leg(names, world, record, say=print):
+    """The 'layers' records.  On one GPU a failing layer is reported in its record and the next one
+    runs.  With N > 1 ranks a failure propagates: a rank that caught its own error would
+    run on into the next layer's collectives while its peers still wait inside the failed layer's
+    exchange -- collectives paired across layers, or a hang until the watchdog; raising lets
+    torchrun tear every rank down at once."""
+    recs = []
+    for name in filter(None, (n.strip() for n in names)):
+        say(f"layer {name}")
+        if world > 1:
+            recs.append(record(name))
+        else:
+            try:
+                recs.append(record(name))
+            except Exception as exc:  # reported, not fatal: the metric line stands on its own
+                recs.append({"config": name, "n_gpus": world, "error": f"{type(exc).__name__}: {exc}"[:300]})
+        say(f"layer {name}: {json.dumps(recs[-1])[:200]}")
+    return recs
 
 
 def grid_of(args, world):
@@ -748,15 +759,10 @@ def main():
     if args.layers and args.layers != "none":
         del agg
         torch.cuda.empty_cache()
-        recs = []
-        for name in args.layers.split(","):
-            log(rank, f"layer {name}")
-            try:
-                recs.append(distributed.layer_record(name.strip(), dev, rank, world, reps=3, backend=backend))
-            except Exception as exc:  # reported, not fatal: the metric line above stands on its own
-                recs.append({"config": name, "n_gpus": world, "error": f"{type(exc).__name__}: {exc}"[:300]})
-            log(rank, f"layer {name}: {json.dumps(recs[-1])[:200]}")
-        result["layers"] = recs
+        result["layers"] = layers_leg(args.layers.split(","), world,
+                                      lambda name: distributed.layer_record(name, dev, rank, world, reps=3,
+                                                                            backend=backend),
+                                      lambda msg: log(rank, msg))
     if rank == 0 and not args.no_cpu_baseline:  # after the timed region; other ranks wait at the barrier
         log(rank, "cpu baseline")
         result["cpu_baseline"] = cpu_baseline(shard, target_s=args.cpu_baseline_s)

@@ -757,10 +757,25 @@ __device__ __forceinline__ float quad_bcast(float v) {  // lane (l & ~3) | SEL o
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), SEL * 0x55, 0xF, 0xF, false));
 }
 
+// lane l ^ 4: the neighbouring quad of a 16-lane row.  gfx9 DPP has no row_xmask, so two row
+// rotations (row_ror:n -- lane l reads lane (l - n) mod 16 of its row) and a pick by quad parity
+__device__ __forceinline__ float xmask4(float v, bool odd_quad) {
+  const float from_lo = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x124, 0xF, 0xF, false));
+  const float from_hi = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x12C, 0xF, 0xF, false));
+  return odd_quad ? from_lo : from_hi;
+}
+
 // W1 (WEIGHTED with one weight per edge, e.g. GCN / GraphSAGE-mean [E, 1]): the weights of a
 // 32-edge chunk arrive with its indices (lane l loads w[e + l]) and edge u's weight is broadcast
 // like its index (bcastG), instead of one load per edge per lane.
-template <bool WEIGHTED, int NT, bool W1 = false>
+// A1 (8 heads, ldw even, 8-B aligned weights): a full step's 8 x 8 weights arrive in ONE 8-B load
+// per lane instead of two 4-B loads: lane (h, q) loads heads 2(h/2), 2(h/2)+1 of edge 2q + h%2, so
+// the quad of head h holds head h's weights of edges 2k + h%2 (k = quad lane) and the neighbouring
+// quad (h ^ 1, two DPP row rotations away) those of edges 2k + (h^1)%2; each edge's weight then
+// reaches the head's lanes by the same quad broadcasts, picked per lane by head parity.  The same
+// weights enter the same fma chain: bitwise equal to the two-load form.  (the alpha
+// loads were ~19 % of the kernel's vector-memory instructions; the texture path is its bound.)
+template <bool WEIGHTED, int NT, bool W1 = false, bool A1 = false>
 __global__ void __launch_bounds__(kBlock)
 k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
           uint32_t row_bytes, const float* __restrict__ w, int64_t ldw, float* __restrict__ slabs,
@@ -783,7 +798,14 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
   const int ldw32 = static_cast<int>(ldw);
   // chunk cursors: advanced once per 32 edges, so no per-edge 64-bit offsets are live
   const int32_t* ic = indices + it.beg;
-  const float* wc = WEIGHTED ? w + it.beg * ldw + (W1 ? 0 : h) : nullptr;
+  const float* wc = (WEIGHTED && !A1) ? w + it.beg * ldw + (W1 ? 0 : h) : nullptr;
+  // A1: the weights as the uniform base w + a 32-bit byte offset (host: nnz * ldw * 4 < 2^32), like
+  // the rows -- with 64-bit per-lane pointers the compiler strength-reduced every (step, edge)
+  // weight address into its own 64-bit induction variable (134 VGPRs, 3 waves per SIMD)
+  const char* wbase = reinterpret_cast<const char*>(w);
+  uint32_t woff = A1 ? static_cast<uint32_t>((it.beg * ldw + h) * 4) : 0u;
+  const uint32_t wrow = static_cast<uint32_t>(ldw) * 4u;
+  auto wat = [&](uint32_t off) { return *reinterpret_cast<const float*>(wbase + off); };
   float acc[4] = {0.f, 0.f, 0.f, 0.f};
   // NT bit 0: non-temporal index loads, bit 2: non-temporal weight loads (both streams are read
   // once), bit 1: non-temporal slab stores
@@ -808,6 +830,21 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
         if (WEIGHTED && W1) {
 #pragma unroll
           for (int u = 0; u < U; ++u) wu[u] = __int_as_float(bcastG<G>(__float_as_int(wv), s + u));
+        } else if (WEIGHTED && A1) {
+          const float2 pr = *reinterpret_cast<const float2*>(
+              wbase + (woff + static_cast<uint32_t>((h & 1) + s + 2 * q) * wrow + static_cast<uint32_t>(2 * (h >> 1) - h) * 4u));
+          const bool odd = h & 1;
+          const float own = odd ? pr.y : pr.x, oth = xmask4(odd ? pr.x : pr.y, odd);
+          float a[4], b[4];
+          a[0] = quad_bcast<0>(own); b[0] = quad_bcast<0>(oth);
+          a[1] = quad_bcast<1>(own); b[1] = quad_bcast<1>(oth);
+          a[2] = quad_bcast<2>(own); b[2] = quad_bcast<2>(oth);
+          a[3] = quad_bcast<3>(own); b[3] = quad_bcast<3>(oth);
+#pragma unroll
+          for (int k2 = 0; k2 < 4; ++k2) {
+            wu[2 * k2] = odd ? b[k2] : a[k2];
+            wu[2 * k2 + 1] = odd ? a[k2] : b[k2];
+          }
         } else if (WEIGHTED) {
           const float* wp = wc + (s + 2 * q) * ldw32;
           const float w0 = ldw_(wp), w1 = ldw_(wp + ldw32);
@@ -823,7 +860,9 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
           const int src = bcastG<G>(idxv, s + u);
           if (u < rem) {
             xv[u] = row(src);
-            if (WEIGHTED) wu[u] = W1 ? __int_as_float(bcastG<G>(__float_as_int(wv), s + u)) : ldw_(wc + (s + u) * ldw32);
+            if (WEIGHTED)
+              wu[u] = W1 ? __int_as_float(bcastG<G>(__float_as_int(wv), s + u))
+                         : (A1 ? wat(woff + static_cast<uint32_t>(s + u) * wrow) : ldw_(wc + (s + u) * ldw32));
           } else {
             xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (WEIGHTED) wu[u] = 0.f;
@@ -845,7 +884,8 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
     idxv = idxn;
     if (W1) wv = wvn;
     ic += G;
-    if (WEIGHTED) wc += static_cast<int64_t>(G) * ldw;
+    if (WEIGHTED && A1) woff += static_cast<uint32_t>(G) * wrow;
+    else if (WEIGHTED) wc += static_cast<int64_t>(G) * ldw;
   }
   if (len > 0) {
     float* o = slabs + k * F + l32 * 4;
@@ -3329,6 +3369,7 @@ struct Tuning {
   int agg_lean = 1;        // k_agg_lean for F = 64*VW SpMM shapes (0: k_aggregate, the form of other shapes)
   int seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
   int seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
+  int seg_alpha1 = 1;      // k_agg_h32 with 8 heads: one 8-B weight load per lane and step (A1) instead of two 4-B
   int seg_phase = 0;       // blocked aggregate: 0 = items + reduce, 1 = items only, 2 = reduce only (bench timing)
   int att_lean = 1;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads (0: the generic half-wave form)
   int att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
@@ -3389,6 +3430,7 @@ const Knob* find_knob(const char* key) {
       {"agg_lean", &Tuning::agg_lean, nullptr},
       {"seg_lean", &Tuning::seg_lean, nullptr},
       {"seg_lean_w1", &Tuning::seg_lean_w1, nullptr},
+      {"seg_alpha1", &Tuning::seg_alpha1, nullptr},
       {"seg_phase", &Tuning::seg_phase, nullptr},
       {"att_lean", &Tuning::att_lean, nullptr},
       {"att_direct", &Tuning::att_direct, nullptr},
@@ -3751,7 +3793,10 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     // NT template bits: 1 = non-temporal index loads, 2 = non-temporal slab stores (measured -0.5 % / -1 %;
     // non-temporal weight loads +3 %: profiles/r02_nt_bits_ab.json)
     if (lean) {
+      const bool a1 = w && heads == 8 && ldw % 2 == 0 && aligned(w, 8) && tuning().seg_alpha1 &&
+                      static_cast<uint64_t>(nnz) * static_cast<uint64_t>(ldw) * 4u < (1ull << 32);
       if (w && heads == 1) k_agg_h32<true, 2, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+      else if (a1) k_agg_h32<true, 3, false, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
       else if (w) k_agg_h32<true, 3><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
       else k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
       GTA_LAUNCHED("k_agg_h32");
@@ -4269,13 +4314,28 @@ namespace {
 // waves per SIMD k_mm_wave<NT, FR> is built for (its __launch_bounds__): what its registers allow
 constexpr int wave_wps(int NT, int FR) { return NT == 4 || FR <= 2 ? 2 : 1; }
 
+// SIMDs of the current device (4 per CU: 1024 on an MI355X), read once per device (the
+// grid cap and the cost model below follow the device, not a constant)
+int64_t device_simds() {
+  static std::atomic<int64_t> cache[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 1024;
+  int64_t v = cache[dev].load(std::memory_order_relaxed);
+  if (v > 0) return v;
+  int cus = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0) return 1024;
+  v = 4 * static_cast<int64_t>(cus);
+  cache[dev].store(v, std::memory_order_relaxed);
+  return v;
+}
+
 // k_mm_wave unit cost model, in FR = 4 units (64 rows) of one wave alone on a SIMD, per unit of
 // each FR (profiles/r04/mm_wave_ab.log, K = 500 / 602): FR 3 (48 rows) 0.81, FR 2 (32 rows) 0.56 alone
 // and 1.3 per pair sharing a SIMD (its 2-waves-per-SIMD build).  A launch takes as many rounds of
-// its units as the most loaded SIMD holds: units spread over the 1024 SIMDs, FR 2 two deep.
-double wave_cost(int fr, int64_t units) {
-  if (fr == 2) return units <= 1024 ? 0.56 : static_cast<double>((units + 2047) / 2048) * 1.3;
-  return static_cast<double>((units + 1023) / 1024) * (fr == 3 ? 0.81 : 1.0);
+// its units as the most loaded SIMD holds: units spread over the device's SIMDs, FR 2 two deep.
+double wave_cost(int fr, int64_t units, int64_t simds) {
+  if (fr == 2) return units <= simds ? 0.56 : static_cast<double>((units + 2 * simds - 1) / (2 * simds)) * 1.3;
+  return static_cast<double>((units + simds - 1) / simds) * (fr == 3 ? 0.81 : 1.0);
 }
 
 struct WavePlan {
@@ -4288,19 +4348,19 @@ struct WavePlan {
 // the cheapest single launch, or whole FR = 4 rounds (every SIMD the same number of units) and the
 // remainder rows as a second launch with its own cheapest FR -- a partial last round of 64-row
 // units leaves SIMDs idle (232,965 x 602: 3.56 rounds)
-WavePlan wave_plan(int64_t M, int64_t ncb) {
+WavePlan wave_plan(int64_t M, int64_t ncb, int64_t simds) {
   WavePlan best;
   best.cost = 1e30;
   for (int f = 4; f >= 2; --f) {
-    const double c = wave_cost(f, (M + 16 * f - 1) / (16 * f) * ncb);
+    const double c = wave_cost(f, (M + 16 * f - 1) / (16 * f) * ncb, simds);
     if (c < best.cost - 1e-9) { best.cost = c; best.fr = f; best.rows = M; best.fr2 = 0; }
   }
-  const int64_t rounds = M / 64 * ncb / 1024;  // whole FR 4 rounds
+  const int64_t rounds = M / 64 * ncb / simds;  // whole FR 4 rounds
   if (rounds >= 1) {
-    const int64_t rows = rounds * 1024 / ncb * 64, rem = M - rows;
+    const int64_t rows = rounds * simds / ncb * 64, rem = M - rows;
     if (rem > 0 && rows > 0) {
       for (int f = 4; f >= 2; --f) {
-        const double c = static_cast<double>(rounds) + wave_cost(f, (rem + 16 * f - 1) / (16 * f) * ncb) + 0.1;
+        const double c = static_cast<double>(rounds) + wave_cost(f, (rem + 16 * f - 1) / (16 * f) * ncb, simds) + 0.1;
         if (c < best.cost - 1e-9) { best.cost = c; best.fr = 4; best.rows = rows; best.fr2 = f; }
       }
     }
@@ -4314,7 +4374,7 @@ int64_t wave_units(int64_t M, int64_t ncb, int fr) { return (M + 16 * fr - 1) / 
 void launch_wave_rows(int nt, int fr, hipStream_t s, const float* x, int64_t ldx, int64_t M, int K, const float* wt,
                       int64_t ldwt, int N, int sf, float* out, int64_t ldo) {
   const int64_t ncb = (N + 16 * nt - 1) / (16 * nt);
-  const dim3 gr(static_cast<unsigned>(std::min<int64_t>(wave_units(M, ncb, fr), 1024LL * wave_wps(nt, fr))));
+  const dim3 gr(static_cast<unsigned>(std::min<int64_t>(wave_units(M, ncb, fr), device_simds() * wave_wps(nt, fr))));
   const uint32_t xbu = static_cast<uint32_t>(((M - 1) * ldx + K) * 4);
   const uint32_t wbu = static_cast<uint32_t>((static_cast<int64_t>(N - 1) * ldwt + K) * 4);
 #define GTA_WAVE(NT_, FR_) \
@@ -4341,9 +4401,9 @@ bool launch_wave(int nt, hipStream_t s, const float* x, int64_t ldx, int64_t M, 
     pl.fr = frk;
     pl.rows = M;
   } else {
-    pl = wave_plan(M, ncb);
+    pl = wave_plan(M, ncb, device_simds());
   }
-  if (mode == 1 && (nt != 8 || K < 256 || wave_units(pl.rows, ncb, pl.fr) < 768)) return false;
+  if (mode == 1 && (nt != 8 || K < 256 || 4 * wave_units(pl.rows, ncb, pl.fr) < 3 * device_simds())) return false;
   launch_wave_rows(nt, pl.fr, s, x, ldx, pl.rows, K, wt, ldwt, N, sf, out, ldo);
   if (pl.fr2 && pl.rows < M)
     launch_wave_rows(nt, pl.fr2, s, x + pl.rows * ldx, ldx, M - pl.rows, K, wt, ldwt, N, sf, out + pl.rows * ldo, ldo);

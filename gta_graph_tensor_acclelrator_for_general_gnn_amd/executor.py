@@ -1287,6 +1287,8 @@ MLP_BF16_SUM = True  # default of Executor.mlp_bf16_sum: GIN's sum stored in bf1
 AUTO_GRAPH = True
 AUTO_GRAPH_MAX_EDGES = 1 << 40  # every graph (round 3: 1 << 23, launch-bound layers only)
 AUTO_GRAPH_MAX_ENTRIES = 32
+AUTO_GRAPH_MAX_POOL_BYTES = 64 << 30  # private pools of all captured graphs together: the
+                                      # largest other entries are dropped beyond it
 _AUTO = {}
 
 
@@ -1296,6 +1298,7 @@ class _AutoEntry:
         self.ptrs = {k: t.data_ptr() for k, t in tensors.items()}
         self.src = None                          # the caller's dict last seen with these tensors
         self.calls, self.run, self.failed = 0, None, False
+        self.pool_bytes = 0                      # device memory the capture reserved (its private pool)
 
 
 _AUTO_FAST = {}  # (ids of the call's objects, id of its tensors dict, knob state) -> entry: the per-call lookup
@@ -1348,13 +1351,30 @@ def _auto_graph(opgraph, stream, graph, tensors, semantics, plan_chunk):
     if ent.failed or ent.calls < 2:
         return None
     if ent.run is None:
+        before = torch.cuda.memory_reserved(graph.device)
         try:
             ent.run = GraphedRun(opgraph, stream, graph, ent.tensors, semantics, plan_chunk, warmup=1)
         except Exception:  # something in this stream is not capturable: stay eager for this key
             ent.failed = True
             torch.cuda.synchronize(graph.device)
             return None
+        ent.pool_bytes = max(0, torch.cuda.memory_reserved(graph.device) - before)
+        _evict_pools(keep=ent)
     return ent.run
+
+
+def _evict_pools(keep):
+    """Keep the captured graphs' pools within AUTO_GRAPH_MAX_POOL_BYTES: drop the largest entries
+    other than `keep` (a Reddit / products-sized layer holds GBs of intermediates)."""
+    total = sum(e.pool_bytes for e in _AUTO.values() if e.run is not None)
+    while total > AUTO_GRAPH_MAX_POOL_BYTES:
+        victims = [(e.pool_bytes, i, k) for i, (k, e) in enumerate(_AUTO.items()) if e.run is not None and e is not keep]
+        if not victims:
+            break
+        b, _, k = max(victims)
+        del _AUTO[k]
+        _AUTO_FAST.clear()
+        total -= b
 
 
 def run_stream(opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, sync=True, trace=False):

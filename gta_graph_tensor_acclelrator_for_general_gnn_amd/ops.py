@@ -591,7 +591,11 @@ def update_mlp(x, w1, w2, sf1=None, sf2=None, out=None):
     if out.shape[0] < M or out.shape[1] != N2:
         raise ValueError("update_mlp: out must be [M, N2]")
     xb = x.dtype == torch.bfloat16
-    check(_L().gta_update_mlp(_ptr(x), _rows(x, "x", x.dtype), M, K1, _ptr(w1t), _rows(w1t, "w1^T", torch.bfloat16), N1, _sf(sf1),
+    ldx = _rows(x, "x", x.dtype)
+    if M <= 1:  # one row: its stride is never used; give the kernel the 16-B multiple it checks
+        step = 8 if xb else 4
+        ldx = -(-ldx // step) * step
+    check(_L().gta_update_mlp(_ptr(x), ldx, M, K1, _ptr(w1t), _rows(w1t, "w1^T", torch.bfloat16), N1, _sf(sf1),
                               _ptr(w2t), _rows(w2t, "w2^T", torch.bfloat16), N2, _sf(sf2), _lib.GTA_BF16 if xb else _lib.GTA_F32_BF16,
                               _ptr(out), _rows(out, "out"), _stream(x.device)), "update_mlp")
     return out

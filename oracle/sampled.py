@@ -5,7 +5,15 @@ materialised op output is re-derived in fp64 at a random sample of rows from
 the executor's own values of that op's inputs -- recursively through virtual
 scatters and fused (never materialised) intermediates -- with the ISA
 semantics of isa_ref.  Together the per-op checks cover every kernel launch of
-the layer at full size.
+the layer at full size.  On small graphs (every golden stream on Cora) the same
+check runs at every row.
+
+Tolerance, per element: |got - exp| <= 1e-5 * sum|terms| + 1e-6, with sum|terms|
+the fp64 magnitude sum of the terms the op adds or multiplies, taken op-locally from the same
+executor inputs: a gather's sum of |edge values|, |a| + |b| for ADD / SUB, |a * b| and |a / b| for
+MUL / DIV, |f(x)| for an SF, sum_k |x_ik| |w_kj| for an MM (bf16 W: x rounded to bf16 as the kernel
+rounds it), |x| for a copy.  A value the executor stores in bf16 (GIN's sum handed to the fused MLP,
+ABI 10) adds its one RNE rounding, 2^-8 |exp|.
 """
 import numpy as np
 import torch
@@ -58,41 +66,61 @@ class SampledChecker:
 
     def expected(self, op, kind, idx):
         """fp64 value of op at rows idx, from its inputs' executor values."""
+        return self.expected2(op, kind, idx)[0]
+
+    def _col_edges(self, j):
+        """Edges whose source is column j, in CSR order (gather with DIRECTION src, ORDER C)."""
+        if getattr(self, "_csc", None) is None:
+            perm = np.argsort(self.ix, kind="stable")
+            cnt = np.bincount(self.ix, minlength=int(getattr(self.ex.graph, "n_cols", 0) or 0))
+            self._csc = (np.concatenate([[0], np.cumsum(cnt)]).astype(np.int64), perm)
+        ptr, perm = self._csc
+        return perm[ptr[j]:ptr[j + 1]] if j + 1 < len(ptr) else perm[:0]
+
+    def expected2(self, op, kind, idx):
+        """(fp64 value, fp64 sum|terms|) of op at rows idx, from its inputs' executor values."""
         idx = np.asarray(idx, np.int64)
         nin = len(self.g.inputs[op.idx])
         if op.type == "scatter":
             rows = self.ix[idx] if op.order == "C" else self.dst_of(idx)
-            return self.input_at(op, 0, "node", rows)
+            v = self.input_at(op, 0, "node", rows)
+            return v, np.abs(v)
         if op.type == "gather":
-            out = []
-            for r in idx:
-                e = np.arange(self.ip[r], self.ip[r + 1])
-                vals = self.input_at(op, 0, "edge", e) if len(e) else None
-                out.append(vals.sum(0) if vals is not None else None)
-            width = next((o.shape[0] for o in out if o is not None), None)
-            if width is None:
-                width = self.g.ops[op.idx].out_width
-            return np.stack([o if o is not None else np.zeros(width) for o in out])
+            lists = [self._col_edges(r) if op.order == "C" else np.arange(self.ip[r], self.ip[r + 1]) for r in idx]
+            edges = np.concatenate(lists) if lists else np.zeros(0, np.int64)
+            if edges.size == 0:
+                z = np.zeros((len(idx), self.g.ops[op.idx].out_width))
+                return z, z.copy()
+            vals = self.input_at(op, 0, "edge", edges)  # every sampled row's edges in one read
+            seg = np.repeat(np.arange(len(idx)), [len(x) for x in lists])
+            out = np.zeros((len(idx), vals.shape[1]))
+            mag = np.zeros_like(out)
+            np.add.at(out, seg, vals)
+            np.add.at(mag, seg, np.abs(vals))
+            return out, mag
         k = "edge" if op.type == "applyedge" else "node"
         if op.comp == "MM":
             W = self.tensors[f"w:{op.idx}"].double().cpu().numpy()
             x = self.input_at(op, 0, k, idx)
             if self.tensors[f"w:{op.idx}"].dtype == torch.bfloat16:
                 x = torch.from_numpy(x).to(torch.bfloat16).double().numpy()
-            return x @ W
+            return x @ W, np.abs(x) @ np.abs(W)
         if op.comp == "SF":
-            return isa_ref.sf(self.sem.sf_of(op), self.input_at(op, 0, k, idx))
+            v = isa_ref.sf(self.sem.sf_of(op), self.input_at(op, 0, k, idx))
+            return v, np.abs(v)
         b = self.sem.bin_of(op)
         ins = [self.input_at(op, s, k, idx) for s in range(nin)]
         extra = self.tensors.get(f"ext:{op.idx}:1")
         if nin == 1 and extra is not None:
             ins.append(self.value_at(self.ex._wrap_ext(extra), k, idx))
         if len(ins) == 1:
-            return ins[0]
+            return ins[0], np.abs(ins[0])
         A, B = ins[0], ins[1]
         if b == "RDIV":
             A, B, b = B, A, "DIV"
-        return isa_ref.binop(b, A, B)
+        v = isa_ref.binop(b, A, B)
+        mag = isa_ref.binop("ADD" if b in ("ADD", "SUB") else b, np.abs(A), np.abs(B))
+        return v, np.abs(mag)
 
     def special_rows(self, per_class=2):
         """{class: node ids} checked in every op on top of the random sample: the first
@@ -131,11 +159,15 @@ class SampledChecker:
             out[f"block_edge_B{B}"] = np.asarray(rows, np.int64)
         return {k: np.asarray(v, np.int64) for k, v in out.items() if len(v)}
 
-    def check(self, n_samples=48, seed=0, rtol=2e-4, skip_ops=(), n_gather=128):
-        """Returns {op: normalised max error}; raises AssertionError beyond rtol.  Node values are
-        checked at n_samples random rows (n_gather for gathers, the aggregates) plus every row of
+    def check(self, n_samples=48, seed=0, rtol=None, skip_ops=(), n_gather=128):
+        """Returns {op: max err / bound}; raises AssertionError when any element of any checked op
+        exceeds the per-element bound of the module docstring (rtol: None = that bound; a number =
+        the old normalised max|d| / max|ref| criterion instead).  Node values are checked at
+        n_samples random rows (n_gather for gathers, the aggregates) plus every row of
         special_rows(); edge values at n_samples random edges plus the first and last edge of each
-        special row.  The special rows are named in the assertion message and kept in self.special."""
+        special row (n_samples >= the row count: every row).  The special rows are named in the
+        assertion message and kept in self.special; self.detail[op] = (max err, its bound, max
+        err / bound, elements checked)."""
         from gta_graph_tensor_acclelrator_for_general_gnn_amd import executor as X
         rng = np.random.default_rng(seed)
         N, E = len(self.ip) - 1, len(self.ix)
@@ -144,7 +176,7 @@ class SampledChecker:
         nz = sp_rows[self.ip[sp_rows + 1] > self.ip[sp_rows]]
         sp_edges = np.unique(np.concatenate([self.ip[nz], self.ip[nz + 1] - 1])) if nz.size else np.zeros(0, np.int64)
         listing = ", ".join(f"{k}={v.tolist()}" for k, v in self.special.items())
-        report = {}
+        report, self.detail = {}, {}
         for op in self.g.ops:
             if op.idx in skip_ops:
                 continue
@@ -155,16 +187,33 @@ class SampledChecker:
                 continue
             kind = "node" if isinstance(v, X.NodeT) else "edge"
             total = N if kind == "node" else E
+            if op.type == "gather" and op.order == "C":
+                total = v.t.shape[0]  # one row per source column
             k = n_gather if op.type == "gather" else n_samples
             idx = rng.choice(total, size=min(k, total), replace=False)
-            idx = np.unique(np.concatenate([idx, sp_rows if kind == "node" else sp_edges]))
+            idx = np.unique(np.concatenate([idx, (sp_rows[sp_rows < total] if kind == "node" else sp_edges)]))
             got = self.value_at(v, kind, idx)
-            exp = self.expected(op, kind, idx)
+            exp, mag = self.expected2(op, kind, idx)
             fin = np.isfinite(exp)
             assert np.array_equal(np.isfinite(got), fin), f"op {op.idx}: non-finite pattern differs ({listing})"
-            scale = np.abs(exp[fin]).max() if fin.any() else 0.0
-            err = float(np.abs(got[fin] - exp[fin]).max() / (scale + 1e-30)) if fin.any() else 0.0
-            report[op.idx] = err
-            assert err <= rtol, (f"op {op.idx} ({op.type}/{op.comp}): normalised max err {err:.2e} over "
-                                 f"{idx.size} {kind}s incl. special rows {listing}")
+            if not fin.any():
+                report[op.idx] = 0.0
+                continue
+            d = np.abs(got[fin] - exp[fin])
+            if rtol is not None:
+                scale = np.abs(exp[fin]).max()
+                err = float(d.max() / (scale + 1e-30))
+                report[op.idx] = err
+                assert err <= rtol, (f"op {op.idx} ({op.type}/{op.comp}): normalised max err {err:.2e} over "
+                                     f"{idx.size} {kind}s incl. special rows {listing}")
+                continue
+            bound = 1e-5 * mag[fin] + 1e-6
+            if v.t.dtype == torch.bfloat16:  # stored rounded: one RNE rounding to bf16
+                bound = bound + 2.0 ** -8 * np.abs(exp[fin])
+            ratio = d / bound
+            j = int(np.argmax(ratio))
+            self.detail[op.idx] = (float(d[j]), float(bound[j]), float(ratio[j]), int(d.size))
+            report[op.idx] = float(ratio[j])
+            assert ratio[j] <= 1.0, (f"op {op.idx} ({op.type}/{op.comp}): |d| {d[j]:.3e} > bound {bound[j]:.3e} "
+                                     f"(1e-5 sum|terms| + 1e-6) over {idx.size} {kind}s incl. special rows {listing}")
         return report

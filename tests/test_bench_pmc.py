@@ -79,3 +79,19 @@ def test_rank_roofline_fields():
     per[0]["traffic"] = float("nan")
     r = bench.rank_roofline(per)
     assert r["per_rank"][0]["frac"] is None and r["job_achieved_GBps"] is None and r["frac"] is not None
+
+
+def test_layers_leg_fails_together_at_n_gt_1():
+    """on one GPU a failing layer becomes an error record and the next layer runs; with N > 1
+    ranks the failure propagates (torchrun then tears every rank down) instead of the rank running on
+    into collectives its peers are not in."""
+    import pytest
+
+    def record(name):
+        if name == "bad":
+            raise MemoryError("out of memory in run_stream")
+        return {"config": name, "ms_per_forward": 1.0}
+    recs = bench.layers_leg(["ok1", "bad", "ok2"], 1, record, say=lambda m: None)
+    assert [r["config"] for r in recs] == ["ok1", "bad", "ok2"] and "MemoryError" in recs[1]["error"]
+    with pytest.raises(MemoryError):
+        bench.layers_leg(["ok1", "bad", "ok2"], 2, record, say=lambda m: None)

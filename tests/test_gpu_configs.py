@@ -1,8 +1,9 @@
 """BASELINE configs end to end at FULL size on MI355X (front end -> fusion search -> stream -> kernels).
 
 Whole-graph fp64 is out of reach at Reddit/products scale, so every materialised op
-is checked locally on sampled rows against fp64 (oracle/sampled.py), tolerance
-max|d|/max|ref| <= 2e-4 (bf16 GEMMs: inputs rounded to bf16 in the reference too).
+is checked locally on sampled rows against fp64 (oracle/sampled.py), tolerance per
+element |d| <= 1e-5 * sum|terms| + 1e-6 from the op's own inputs (bf16 GEMMs: inputs
+rounded to bf16 in the reference too; a bf16-stored value: + its RNE rounding).
 """
 import pytest
 import torch
@@ -28,8 +29,9 @@ def test_config_full_size_sampled_parity(dev, name):
             if not lay.reorder:
                 assert fin.all(), f"{name}: non-finite output of op {k}"
         chk = SampledChecker(ex, ip, ix)
-        report = chk.check(n_samples=32, seed=1, n_gather=128)
+        report = chk.check(n_samples=32, seed=1, n_gather=128)  # per element: 1e-5 sum|terms| + 1e-6
         assert report, "nothing was checked"
+        print(name, lay.network, "max err / bound per op:", {k: round(v[2], 4) for k, v in chk.detail.items()})
         # the heaviest rows, split-row and column-block boundary rows, empty rows and
         # the first / last row are always among the checked rows
         sp = chk.special

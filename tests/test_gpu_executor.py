@@ -14,6 +14,7 @@ from gta_graph_tensor_acclelrator_for_general_gnn_amd import executor, graph as 
 from gta_graph_tensor_acclelrator_for_general_gnn_amd.semantics import Semantics
 from oracle import isa_ref
 from oracle.exec_ref import execute_ref
+from oracle.sampled import SampledChecker
 
 from .conftest import load_manifest
 from .test_ir_executor_cpu import compare
@@ -42,7 +43,11 @@ def _run(golden_dir, rec, ip, ix, dev, seed, plan_chunk):
     res, ex = executor.run_stream(og, st, gd, tensors, sem, plan_chunk=plan_chunk)
     ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors_c.items()})
     vals = {i: ex.tensor_of(i) for i in range(len(og))}
-    compare(vals, ref, range(len(og)), rtol=2e-4)
+    compare(vals, ref, range(len(og)), rtol=2e-4)  # end to end, through the whole op chain
+    # op-local and per element, at every row and edge: |d| <= 1e-5 sum|terms| + 1e-6 (oracle/sampled.py)
+    chk = SampledChecker(ex, ip, ix)
+    chk.check(n_samples=1 << 30, n_gather=1 << 30)
+    print(rec["file"], {k: round(v[2], 4) for k, v in chk.detail.items()})  # max err / bound per op
     return res
 
 

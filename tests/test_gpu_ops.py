@@ -388,11 +388,12 @@ def test_edge_softmax_other_sf_and_errors(dev):
         ops.edge_softmax(g, a, b[:, :4].contiguous())
 
 
-@pytest.mark.parametrize("knobs", [{"seg_lean": 0}, {"seg_lean_w1": 0}])
+@pytest.mark.parametrize("knobs", [{"seg_lean": 0}, {"seg_lean_w1": 0}, {"seg_alpha1": 0}])
 @pytest.mark.parametrize("F,heads", [(128, 8), (128, 0), (64, 4), (256, 16), (128, 1)])
 def test_aggregate_blocked_kernel_forms(dev, knobs, F, heads):
-    """The lean half-wave kernels (k_agg_h32, also with one weight per edge) == the generic
-    half-wave form bitwise (same per-item edge order and fma chain), and == the fp64 oracle."""
+    """The lean half-wave kernels (k_agg_h32, also with one weight per edge, and with 8 heads' weights
+    in one 8-B load per step, seg_alpha1) == the generic half-wave form / the two-load form bitwise
+    (same per-item edge order, weights and fma chain), and == the fp64 oracle."""
     n, e = 900, 30000
     g = G.synthetic(n, e, seed=F + heads, device=dev)
     ip, ix = g.numpy()
@@ -1319,3 +1320,20 @@ def test_csc_views_aggregate(dev, kind):
     xe = isa_ref.edge_operand(ip, ix, x.astype(np.float64), mode) * np.repeat(w, 8, axis=1)
     ref = isa_ref.gather_add(ip, xe, "C", ix, nc)
     _check(y, ref, isa_ref.gather_add(ip, np.abs(xe), "C", ix, nc), f"csc view {kind}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_update_mlp_one_row_products_width(dev, dtype):
+    """a one-row x at GIN products' width (K1 = 100, a row stride the kernel would reject
+    for bf16) runs the fused MLP; same bits as the same row inside a larger batch."""
+    rng = np.random.default_rng(3)
+    w1 = torch.from_numpy((rng.standard_normal((100, 128)) / 10).astype(np.float32)).to(torch.bfloat16).to(dev)
+    w2 = torch.from_numpy((rng.standard_normal((128, 128)) / 11).astype(np.float32)).to(torch.bfloat16).to(dev)
+    big = torch.zeros(64, 104, device=dev, dtype=dtype)[:, :100]  # rows padded to 16 B: a batch the kernel takes
+    big.copy_(torch.from_numpy(rng.standard_normal((64, 100)).astype(np.float32)).to(dev).to(dtype))
+    one = big[5:6].clone()  # a fresh [1, 100] tensor: stride 100
+    assert ops.update_mlp_supported(one, w1, w2)
+    got = ops.update_mlp(one, w1, w2, sf1="RELU", sf2="RELU")
+    ref = ops.update_mlp(big, w1, w2, sf1="RELU", sf2="RELU")[5:6]
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref)

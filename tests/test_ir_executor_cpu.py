@@ -95,6 +95,9 @@ def test_executor_plans_every_golden_stream(golden_dir, manifest, monkeypatch, i
     vals = {i: ex.tensor_of(i) for i in range(len(og))}
     compare(vals, ref, range(len(og)))
     assert set(outs) == {op.idx for op in og.ops if not op.out_list}
+    # the GPU tests' op-local per-element check (oracle/sampled.py), here over the fp64 stand-in
+    from oracle.sampled import SampledChecker
+    SampledChecker(ex, ip, ix).check(n_samples=200, n_gather=200, seed=idx)
 
 
 @pytest.mark.parametrize("network,reorder,expect", [
