@@ -703,6 +703,10 @@ def main():
     ab = metric.alg_bytes(crit["tile_rows"], crit["tile_edges"])
     alg_gbps = ab / (crit["compute_ms"] / 1e3) / 1e9
     roof = {"bound": "hbm", "achieved": rr["achieved"], "peak": PEAK_HBM_GBS, "unit": "GB/s", "frac": rr["frac"],
+            # what `traffic` / `frac` count -- no counter on this pool splits HBM from
+            # Infinity-Cache hits, so frac is an upper bound on the HBM fraction
+            "bytes_side": "fabric side of L2 (L2 misses: HBM reads + Infinity-Cache hits + writes); "
+                          "frac = those bytes / time / HBM peak, an upper bound on the HBM fraction",
             "traffic": rr["traffic"], "kernel_ms": rr["kernel_ms"],
             "kernels": "k_agg_h32 + k_seg_reduce" if agg.impl == "blocked" else "k_aggregate + combine",
             "rank_basis": rr["rank_basis"], "frac_min": rr["frac_min"], "frac_max": rr["frac_max"],

@@ -100,13 +100,30 @@ template <> struct Vec<4> {
     *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
   }
 };
+template <> struct Vec<8> {  // bf16 rows only: 8 elements = one 16-B piece (fp32 sides: two float4)
+  float v[8];
+  __device__ __forceinline__ void load(const float* p) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ void store(float* p) const {
+    *reinterpret_cast<float4*>(p) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+};
 
 // Vec<VW> from VW consecutive elements of a float or bf16 row (bf16 widened exactly: bits << 16)
 template <int VW>
 __device__ __forceinline__ void load_row(Vec<VW>& o, const float* p) { o.load(p); }
 template <int VW>
 __device__ __forceinline__ void load_row(Vec<VW>& o, const uint16_t* p) {
-  if constexpr (VW == 4) {
+  if constexpr (VW == 8) {  // one 16-B load (8-B aligned rows are fine for global loads)
+    const uint4 u = *reinterpret_cast<const uint4*>(p);
+    o.v[0] = __uint_as_float(u.x << 16); o.v[1] = __uint_as_float(u.x & 0xffff0000u);
+    o.v[2] = __uint_as_float(u.y << 16); o.v[3] = __uint_as_float(u.y & 0xffff0000u);
+    o.v[4] = __uint_as_float(u.z << 16); o.v[5] = __uint_as_float(u.z & 0xffff0000u);
+    o.v[6] = __uint_as_float(u.w << 16); o.v[7] = __uint_as_float(u.w & 0xffff0000u);
+  } else if constexpr (VW == 4) {
     const uint2 u = *reinterpret_cast<const uint2*>(p);
     o.v[0] = __uint_as_float(u.x << 16); o.v[1] = __uint_as_float(u.x & 0xffff0000u);
     o.v[2] = __uint_as_float(u.y << 16); o.v[3] = __uint_as_float(u.y & 0xffff0000u);
@@ -232,10 +249,11 @@ __global__ void k_plan_fill(const int64_t* __restrict__ indptr, int64_t n_rows, 
 //   bitwise reproducible run to run (no atomics).
 // ---------------------------------------------------------------------------
 enum { XM_IDX = 0, XM_EDGE = 1 };
+
 enum { WM_NONE = 0, WM_HEAD = 1, WM_FULL = 2 };
 
 // TX: the gathered rows' element type (float, or bf16 as uint16_t: widened exactly, fp32 sums)
-template <int LPE, int VW, int NV, int XMODE, int WMODE, typename TX = float>
+template <int LPE, int VW, int NV, int XMODE, int WMODE, typename TX = float, int URX = 0>
 __global__ void __launch_bounds__(kBlock)
 k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows,
             PlanView plan, int use_plan, int64_t chunk, int x_is_row,
@@ -251,7 +269,7 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
   constexpr int EPI = kWave / LPE;                 // edges per wave instruction
   // row loads in flight per lane: ~64 B of each lane's rows per unrolled step
   constexpr int XB = NV * VW * static_cast<int>(sizeof(TX));
-  constexpr int UR = (64 / XB) < 2 ? 2 : ((64 / XB) > 8 ? 8 : 64 / XB);
+  constexpr int UR = URX ? URX : ((64 / XB) < 2 ? 2 : ((64 / XB) > 8 ? 8 : 64 / XB));
   constexpr int STEP = UR * EPI;                    // edges per unrolled step
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t item = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
@@ -276,13 +294,18 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
   const float scale = (row_scale != nullptr && !split) ? row_scale[row] : 1.f;
 
   for (int c0 = 0; c0 < F; c0 += LPE * VW * NV) {
-    int col[NV], hcol[NV];
+    int col[NV], hcol[NV], lo[NV];
     bool cval[NV];
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
       const int c = c0 + (v * LPE + cl) * VW;
       cval[v] = c < F;
-      col[v] = cval[v] ? c : 0;
+      int cc = cval[v] ? c : 0;
+      lo[v] = 0;
+      if constexpr (VW == 8) {  // 16-B bf16 pieces, F % 4 == 0: the last lane's piece starts 4 early
+        if (cval[v] && cc + VW > F) { lo[v] = cc + VW - F; cc -= lo[v]; }  // (its first lo sums unused)
+      }
+      col[v] = cc;
       hcol[v] = (WMODE == WM_HEAD) ? col[v] / gsz : 0;
     }
     float acc[NV][VW];
@@ -363,10 +386,17 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
       for (int v = 0; v < NV; ++v) {
         if (!cval[v]) continue;
         Vec<VW> o;
+        // a piece whose first lo sums belong to the lane before: store its upper half only
+        auto put = [&](float* p) {
+          if constexpr (VW == 8) {
+            if (lo[v]) { *reinterpret_cast<float4*>(p + 4) = make_float4(o.v[4], o.v[5], o.v[6], o.v[7]); return; }
+          }
+          o.store(p);
+        };
         if (split) {
 #pragma unroll
           for (int k = 0; k < VW; ++k) o.v[k] = acc[v][k];
-          o.store(partial + item * static_cast<int64_t>(F) + col[v]);
+          put(partial + item * static_cast<int64_t>(F) + col[v]);
         } else {
           float* yp = y + row * ldy + col[v];
           if (accumulate) {
@@ -389,9 +419,10 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
           if (y_bf16) {
             uint16_t* yb = reinterpret_cast<uint16_t*>(y) + row * ldy + col[v];
 #pragma unroll
-            for (int k = 0; k < VW; ++k) yb[k] = to_bf16_bits(o.v[k]);
+            for (int k = 0; k < VW; ++k)
+              if (k >= lo[v]) yb[k] = to_bf16_bits(o.v[k]);
           } else {
-            o.store(yp);
+            put(yp);
           }
         }
       }
@@ -3309,10 +3340,10 @@ struct AggArgs {
   int y_bf16;                                            // y stored as bf16 (gta_aggregate_self, y_dtype)
 };
 
-template <int LPE, int VW, int NV, int XM, int WM, typename TX>
+template <int LPE, int VW, int NV, int XM, int WM, typename TX, int URX = 0>
 void launch_agg(const AggArgs& a, int64_t n_items_bound, hipStream_t s) {
   const int64_t blocks = (n_items_bound + kWavesPerBlock - 1) / kWavesPerBlock;
-  k_aggregate<LPE, VW, NV, XM, WM, TX><<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
+  k_aggregate<LPE, VW, NV, XM, WM, TX, URX><<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
       a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, a.x_is_row, static_cast<const TX*>(a.x), a.ldx, a.F,
       a.w, a.ldw, a.gsz, a.row_scale, a.y, a.ldy, a.accumulate, a.partial, static_cast<const TX*>(a.xs), a.ldxs,
       a.self_scale, a.y_bf16);
@@ -3343,6 +3374,23 @@ bool dispatch_x(int xm, int wm, bool bf, const AggArgs& a, int64_t nb, hipStream
                        : dispatch_w<LPE, VW, NV, XM_IDX>(wm, bf, a, nb, s);
 }
 
+// the 16-B bf16 form (VW = 8): indexed unweighted gathers (GIN's sum), one piece per lane; ur: row
+// loads in flight per lane per unrolled step (4: 16 rows per wave at 4 edges per instruction, 8: 32)
+template <int UR>
+bool dispatch_bf16_vw8_ur(int lpe, const AggArgs& a, int64_t nb, hipStream_t s) {
+  switch (lpe) {
+    case 64: launch_agg<64, 8, 1, XM_IDX, WM_NONE, uint16_t, UR>(a, nb, s); return true;
+    case 32: launch_agg<32, 8, 1, XM_IDX, WM_NONE, uint16_t, UR>(a, nb, s); return true;
+    case 16: launch_agg<16, 8, 1, XM_IDX, WM_NONE, uint16_t, UR>(a, nb, s); return true;
+    case 8: launch_agg<8, 8, 1, XM_IDX, WM_NONE, uint16_t, UR>(a, nb, s); return true;
+    case 4: launch_agg<4, 8, 1, XM_IDX, WM_NONE, uint16_t, UR>(a, nb, s); return true;
+  }
+  return false;
+}
+bool dispatch_bf16_vw8(int lpe, int ur, const AggArgs& a, int64_t nb, hipStream_t s) {
+  return ur == 8 ? dispatch_bf16_vw8_ur<8>(lpe, a, nb, s) : dispatch_bf16_vw8_ur<4>(lpe, a, nb, s);
+}
+
 template <int VW>
 bool dispatch_lpe(int lpe, int nv, int xm, int wm, bool bf, const AggArgs& a, int64_t nb, hipStream_t s) {
   switch (lpe) {
@@ -3370,6 +3418,8 @@ struct Tuning {
   int seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
   int seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
   int seg_alpha1 = 1;      // k_agg_h32 with 8 heads: one 8-B weight load per lane and step (A1) instead of two 4-B
+  int agg_bf16_vw8 = 4;    // k_aggregate over bf16 rows in 16-B pieces (VW = 8) instead of 8-B pieces:
+                           // 0 off, 4 / 8 = row loads in flight per lane and step (1 = 4)
   int seg_phase = 0;       // blocked aggregate: 0 = items + reduce, 1 = items only, 2 = reduce only (bench timing)
   int att_lean = 1;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads (0: the generic half-wave form)
   int att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
@@ -3431,6 +3481,7 @@ const Knob* find_knob(const char* key) {
       {"seg_lean", &Tuning::seg_lean, nullptr},
       {"seg_lean_w1", &Tuning::seg_lean_w1, nullptr},
       {"seg_alpha1", &Tuning::seg_alpha1, nullptr},
+      {"agg_bf16_vw8", &Tuning::agg_bf16_vw8, nullptr},
       {"seg_phase", &Tuning::seg_phase, nullptr},
       {"att_lean", &Tuning::att_lean, nullptr},
       {"att_direct", &Tuning::att_direct, nullptr},
@@ -3597,6 +3648,20 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
   }
   if (!bf && tuning().force_lpe == 32 && F == 128 && ok_vw(4)) { lpe = 32; vw = 4; nv = 1; }
   if (!bf && tuning().force_lpe == 64 && F == 128 && ok_vw(2)) { lpe = 64; vw = 2; nv = 1; }
+  // bf16 rows gathered in 16-B pieces (8 elements per lane, the last lane's piece clamped inside
+  // the row): half the gather instructions of 8-B pieces for the same rows (GIN products' 200-B
+  // rows: 13 lanes, 4 edges per wave instruction)
+  bool vw8 = false;
+  if (bf && tuning().agg_bf16_vw8 && wm == WM_NONE && xm == XM_IDX && F % 4 == 0 && F >= 8 && F <= 512 &&
+      ldx % 4 == 0 && aligned(x, 8) && (!xs || (ldxs % 4 == 0 && aligned(xs, 8))) &&
+      (y_bf16 ? (ldy % 4 == 0 && aligned(y, 8)) : (ldy % 4 == 0 && aligned(y, 16)))) {
+    const int64_t ln = (F + 7) / 8;
+    vw8 = true;
+    vw = 8;
+    nv = 1;
+    lpe = 4;
+    while (lpe < ln) lpe <<= 1;
+  }
 
   AggArgs a{};
   a.indptr = indptr; a.indices = indices; a.n_rows = n_rows;
@@ -3635,7 +3700,9 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
 #undef GTA_LEAN
     ok = true;
   }
+  if (!ok && vw8) ok = dispatch_bf16_vw8(lpe, tuning().agg_bf16_vw8, a, bound, s);
   if (!ok) switch (vw) {
+    case 8: break;
     case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, bf, a, bound, s); break;
     case 2: ok = dispatch_lpe<2>(lpe, nv, xm, wm, bf, a, bound, s); break;
     default: ok = dispatch_lpe<1>(lpe, nv, xm, wm, bf, a, bound, s); break;

@@ -921,8 +921,8 @@ def test_degenerate_graphs_every_op(dev, n):
 def test_aggregate_bf16_rows(dev, F, heads, plan, mode):
     """bf16 node rows gathered by index (the GIN products byte model: 200-B rows at F = 100),
     widened exactly and summed in fp32: within the fp32 bound of the fp64 oracle on the bf16
-    values, and bitwise equal to the same kernel form on the fp32-widened table (F = 100: both
-    run 32 lanes x 4 values per edge)."""
+    values; the 8-B-piece form (knob agg_bf16_vw8 = 0) is bitwise equal to the same kernel form on
+    the fp32-widened table (F = 100: both run 32 lanes x 4 values per edge)."""
     n, e = 400, 7000
     g, ip, ix = _graph(n, e, seed=F + heads, heavy_row=900, empty_rows=4, dev=dev)
     rng = np.random.default_rng(F)
@@ -933,8 +933,14 @@ def test_aggregate_bf16_rows(dev, F, heads, plan, mode):
     y = ops.aggregate(g, xd, mode, wd, plan=plan)
     xf = x.float().numpy()
     _check(y, isa_ref.aggregate(ip, ix, xf, mode, w), isa_ref.aggregate_abs(ip, ix, xf, mode, w), f"bf16 F={F}")
-    if F == 100:
-        assert torch.equal(y, ops.aggregate(g, xd.float(), mode, wd, plan=plan))
+    if F == 100:  # the 8-B-piece form (32 lanes x 4 values per edge) == the fp32 form on the widened table
+        ops.set_debug("agg_bf16_vw8", 0)
+        try:
+            y8 = ops.aggregate(g, xd, mode, wd, plan=plan)
+        finally:
+            ops.set_debug("agg_bf16_vw8", 4)
+        assert torch.equal(y8, ops.aggregate(g, xd.float(), mode, wd, plan=plan))
+        assert torch.equal(y, ops.aggregate(g, xd, mode, wd, plan=plan))  # the default form: deterministic
     acc = torch.randn(n, F, device=dev)
     y2 = ops.aggregate(g, xd, mode, wd, out=acc.clone(), accumulate=True, plan=plan)
     _check(y2, acc.cpu().numpy() + isa_ref.aggregate(ip, ix, xf, mode, w),
@@ -1337,3 +1343,41 @@ def test_update_mlp_one_row_products_width(dev, dtype):
     ref = ops.update_mlp(big, w1, w2, sf1="RELU", sf2="RELU")[5:6]
     torch.cuda.synchronize()
     assert torch.equal(got, ref)
+
+
+@pytest.mark.parametrize("F", [100, 128, 36, 12, 8, 200])
+@pytest.mark.parametrize("form", ["plain", "self_f32", "self_bf16"])
+def test_aggregate_bf16_16B_pieces(dev, F, form):
+    """bf16 rows gathered in 16-B pieces (knob agg_bf16_vw8, the default for unweighted bf16 gathers:
+    GIN products' 200-B rows in 13 lanes, 4 edges per wave instruction; F % 8 == 4 clamps the last
+    lane's piece inside the row) vs the fp64 oracle at the per-element bound, against the 8-B-piece
+    form at the same bound, deterministic; heavy rows split by the plan, empty rows, the last table
+    row gathered (its clamped piece must stay inside the allocation)."""
+    g, ip, ix = _graph(500, 9000, seed=F, heavy_row=2000, empty_rows=4, dev=dev)
+    ix = ix.copy()
+    ix[:50] = 499  # the table's last row
+    g = G.from_numpy(ip, ix, device=dev)
+    rng = np.random.default_rng(F)
+    x = torch.from_numpy(rng.standard_normal((500, F)).astype(np.float32)).to(dev).to(torch.bfloat16)
+    xn = x.float().cpu().numpy().astype(np.float64)
+    s = torch.tensor([[1.25]], device=dev)
+    ref, mag = isa_ref.aggregate(ip, ix, xn, "src", None), isa_ref.aggregate_abs(ip, ix, xn, "src", None)
+    if form != "plain":
+        ref, mag = ref + 1.25 * xn, mag + 1.25 * np.abs(xn)
+    outs = {}
+    for vw8 in (4, 8, 0):
+        ops.set_debug("agg_bf16_vw8", vw8)
+        try:
+            kw = {} if form == "plain" else {"self_term": (x, s),
+                                             "out_dtype": torch.bfloat16 if form == "self_bf16" else torch.float32}
+            y = ops.aggregate(g, x, "src", None, plan=64, **kw)
+            y2 = ops.aggregate(g, x, "src", None, plan=64, **kw)
+        finally:
+            ops.set_debug("agg_bf16_vw8", 4)
+        torch.cuda.synchronize()
+        assert torch.equal(y, y2)
+        got = y.float().cpu().numpy().astype(np.float64)
+        bound = 1e-5 * mag + 1e-6 + (2.0 ** -8 * np.abs(ref) if form == "self_bf16" else 0)
+        err = np.abs(got - ref)
+        assert (err <= bound).all(), f"vw8={vw8}: max err {err.max():.3e}"
+        outs[vw8] = y
