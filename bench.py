@@ -587,6 +587,11 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
+        # the ranks of this node share its CPUs: host-side torch ops (graph generation, the gloo
+        # rehearsals' staging) with every rank at the full OMP count oversubscribe them -- an 8-rank
+        # one-GPU rehearsal at 16 threads each on a 16-CPU quota stalled for minutes in shard building
+        cpus = cpu_quota() or len(os.sched_getaffinity(0))
+        torch.set_num_threads(max(1, int(cpus) // int(os.environ.get("LOCAL_WORLD_SIZE", world))))
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=dev)
         else:

@@ -92,12 +92,14 @@ class Shard:
         note(f"row group {i}: rows [{r0}, {r1}), {src.numel()} edges generated")
         alpha = alpha_rows(lip, gen, device, seed)
         del gen
+        note(f"row group {i}: alpha [{alpha.shape[0]}, {alpha.shape[1]}] ready")
         if pc > 1 and col_counts is not None:
             ccuts = [int(c) for c in partition.cuts_from_counts(col_counts.to(device), pc)]
         elif pc > 1:
             counts = torch.bincount(src, minlength=n)
             if count_reduce is not None:
                 counts = count_reduce(counts) // pc  # every rank of a row group added the same counts
+                note("column counts summed over the ranks")
             ccuts = [int(c) for c in partition.cuts_from_counts(counts, pc)]
             del counts
         else:

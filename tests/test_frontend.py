@@ -9,6 +9,8 @@ from gta_graph_tensor_acclelrator_for_general_gnn_amd import frontend
 def test_every_golden_op_yaml(golden_dir, manifest):
     assert len(manifest["ops"]) >= 50
     for rec in manifest["ops"]:
+        if rec.get("r5"):  # the hand-written ORDER-C op graphs of make_golden_r5.py: not genGraphOP output
+            continue
         text = frontend.dumps(frontend.gen_ops(rec["network"], rec["layer"], rec["N"], rec["E"], rec["F"],
                                                rec["reorder"]))
         with open(os.path.join(golden_dir, "ops", rec["file"])) as f:
