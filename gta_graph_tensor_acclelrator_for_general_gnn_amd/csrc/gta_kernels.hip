@@ -250,7 +250,11 @@ __global__ void k_plan_fill(const int64_t* __restrict__ indptr, int64_t n_rows, 
 // ---------------------------------------------------------------------------
 enum { XM_IDX = 0, XM_EDGE = 1 };
 
-enum { WM_NONE = 0, WM_HEAD = 1, WM_FULL = 2 };
+// WM_EDGE1: one weight per edge (H = 1: GCN's 1/sqrt(d_i d_j), GIN's edge operand) -- 64 weights
+// per coalesced load beside the 64 indices, broadcast to the edge's lanes like its index, instead of
+// one weight load per lane and edge (WM_HEAD's path, which doubles the vector-memory instructions
+// of a narrow row); the same product and sum per element, so bitwise equal to WM_HEAD at H = 1
+enum { WM_NONE = 0, WM_HEAD = 1, WM_FULL = 2, WM_EDGE1 = 3 };
 
 // TX: the gathered rows' element type (float, or bf16 as uint16_t: widened exactly, fp32 sums)
 template <int LPE, int VW, int NV, int XMODE, int WMODE, typename TX = float, int URX = 0>
@@ -318,11 +322,15 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
     // this block's rows are in flight (clamped address: the load is unconditional)
     const bool use_idx = (XMODE == XM_IDX) && !x_is_row;
     int idxv = 0;
+    float wv = 0.f;
     if (use_idx && eb < ee) idxv = indices[min(eb + lane, ee - 1)];
+    if (WMODE == WM_EDGE1 && eb < ee) wv = w[min(eb + lane, ee - 1) * ldw];
     for (int64_t e0 = eb; e0 < ee; e0 += kWave) {
       const int n = static_cast<int>(min<int64_t>(kWave, ee - e0));
       int idxn = 0;
+      float wn = 0.f;
       if (use_idx) idxn = indices[min(e0 + kWave + lane, ee - 1)];
+      if (WMODE == WM_EDGE1) wn = w[min(e0 + kWave + lane, ee - 1) * ldw];
       for (int s = 0; s < n; s += STEP) {
         Vec<VW> xv[UR][NV];
         float wh[UR][NV];
@@ -350,6 +358,12 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
             const float* wp = w + (e0 + jj) * ldw;
 #pragma unroll
             for (int v = 0; v < NV; ++v) wh[u][v] = wp[hcol[v]];
+          } else if (WMODE == WM_EDGE1) {
+            const float we = (LPE == kWave)
+                                 ? __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, wv), jj))
+                                 : __shfl(wv, jj);
+#pragma unroll
+            for (int v = 0; v < NV; ++v) wh[u][v] = we;
           } else if (WMODE == WM_FULL) {
             const float* wp = w + (e0 + jj) * ldw;
 #pragma unroll
@@ -363,7 +377,7 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
 #pragma unroll
             for (int k = 0; k < VW; ++k) {
               float t;
-              if (WMODE == WM_HEAD) t = wh[u][v] * xv[u][v].v[k];
+              if (WMODE == WM_HEAD || WMODE == WM_EDGE1) t = wh[u][v] * xv[u][v].v[k];
               else if (WMODE == WM_FULL) t = wf[u][v].v[k] * xv[u][v].v[k];
               else t = xv[u][v].v[k];
               acc[v][k] += valid[u] ? t : 0.f;
@@ -372,6 +386,7 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
         }
       }
       idxv = idxn;
+      wv = wn;
     }
     if (LPE < kWave) {  // fold the EPI edge slots (fixed butterfly order)
 #pragma unroll
@@ -3357,6 +3372,7 @@ bool dispatch_w(int wm, bool bf, const AggArgs& a, int64_t nb, hipStream_t s) {
     if constexpr (XM == XM_IDX) {
       if (wm == WM_NONE) { launch_agg<LPE, VW, NV, XM, WM_NONE, uint16_t>(a, nb, s); return true; }
       if (wm == WM_HEAD) { launch_agg<LPE, VW, NV, XM, WM_HEAD, uint16_t>(a, nb, s); return true; }
+      if (wm == WM_EDGE1) { launch_agg<LPE, VW, NV, XM, WM_EDGE1, uint16_t>(a, nb, s); return true; }
     }
     return false;
   }
@@ -3364,6 +3380,7 @@ bool dispatch_w(int wm, bool bf, const AggArgs& a, int64_t nb, hipStream_t s) {
     case WM_NONE: launch_agg<LPE, VW, NV, XM, WM_NONE, float>(a, nb, s); return true;
     case WM_HEAD: launch_agg<LPE, VW, NV, XM, WM_HEAD, float>(a, nb, s); return true;
     case WM_FULL: launch_agg<LPE, VW, NV, XM, WM_FULL, float>(a, nb, s); return true;
+    case WM_EDGE1: launch_agg<LPE, VW, NV, XM, WM_EDGE1, float>(a, nb, s); return true;
   }
   return false;
 }
@@ -3374,21 +3391,24 @@ bool dispatch_x(int xm, int wm, bool bf, const AggArgs& a, int64_t nb, hipStream
                        : dispatch_w<LPE, VW, NV, XM_IDX>(wm, bf, a, nb, s);
 }
 
-// the 16-B bf16 form (VW = 8): indexed unweighted gathers (GIN's sum), one piece per lane; ur: row
-// loads in flight per lane per unrolled step (4: 16 rows per wave at 4 edges per instruction, 8: 32)
-template <int UR>
+// the 16-B bf16 form (VW = 8): indexed gathers, unweighted or one weight per edge (GIN's sum), one
+// piece per lane; ur: row loads in flight per lane per unrolled step (4: 16 rows per wave at 4 edges
+// per instruction, 8: 32)
+template <int UR, int WM>
 bool dispatch_bf16_vw8_ur(int lpe, const AggArgs& a, int64_t nb, hipStream_t s) {
   switch (lpe) {
-    case 64: launch_agg<64, 8, 1, XM_IDX, WM_NONE, uint16_t, UR>(a, nb, s); return true;
-    case 32: launch_agg<32, 8, 1, XM_IDX, WM_NONE, uint16_t, UR>(a, nb, s); return true;
-    case 16: launch_agg<16, 8, 1, XM_IDX, WM_NONE, uint16_t, UR>(a, nb, s); return true;
-    case 8: launch_agg<8, 8, 1, XM_IDX, WM_NONE, uint16_t, UR>(a, nb, s); return true;
-    case 4: launch_agg<4, 8, 1, XM_IDX, WM_NONE, uint16_t, UR>(a, nb, s); return true;
+    case 64: launch_agg<64, 8, 1, XM_IDX, WM, uint16_t, UR>(a, nb, s); return true;
+    case 32: launch_agg<32, 8, 1, XM_IDX, WM, uint16_t, UR>(a, nb, s); return true;
+    case 16: launch_agg<16, 8, 1, XM_IDX, WM, uint16_t, UR>(a, nb, s); return true;
+    case 8: launch_agg<8, 8, 1, XM_IDX, WM, uint16_t, UR>(a, nb, s); return true;
+    case 4: launch_agg<4, 8, 1, XM_IDX, WM, uint16_t, UR>(a, nb, s); return true;
   }
   return false;
 }
-bool dispatch_bf16_vw8(int lpe, int ur, const AggArgs& a, int64_t nb, hipStream_t s) {
-  return ur == 8 ? dispatch_bf16_vw8_ur<8>(lpe, a, nb, s) : dispatch_bf16_vw8_ur<4>(lpe, a, nb, s);
+bool dispatch_bf16_vw8(int lpe, int ur, int wm, const AggArgs& a, int64_t nb, hipStream_t s) {
+  if (wm == WM_EDGE1)
+    return ur == 8 ? dispatch_bf16_vw8_ur<8, WM_EDGE1>(lpe, a, nb, s) : dispatch_bf16_vw8_ur<4, WM_EDGE1>(lpe, a, nb, s);
+  return ur == 8 ? dispatch_bf16_vw8_ur<8, WM_NONE>(lpe, a, nb, s) : dispatch_bf16_vw8_ur<4, WM_NONE>(lpe, a, nb, s);
 }
 
 template <int VW>
@@ -3420,6 +3440,7 @@ struct Tuning {
   int seg_alpha1 = 1;      // k_agg_h32 with 8 heads: one 8-B weight load per lane and step (A1) instead of two 4-B
   int agg_bf16_vw8 = 4;    // k_aggregate over bf16 rows in 16-B pieces (VW = 8) instead of 8-B pieces:
                            // 0 off, 4 / 8 = row loads in flight per lane and step (1 = 4)
+  int agg_w1 = 1;          // k_aggregate with one weight per edge: 64 per load, broadcast (WM_EDGE1); 0 = WM_HEAD
   int seg_phase = 0;       // blocked aggregate: 0 = items + reduce, 1 = items only, 2 = reduce only (bench timing)
   int att_lean = 1;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads (0: the generic half-wave form)
   int att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
@@ -3482,6 +3503,7 @@ const Knob* find_knob(const char* key) {
       {"seg_lean_w1", &Tuning::seg_lean_w1, nullptr},
       {"seg_alpha1", &Tuning::seg_alpha1, nullptr},
       {"agg_bf16_vw8", &Tuning::agg_bf16_vw8, nullptr},
+      {"agg_w1", &Tuning::agg_w1, nullptr},
       {"seg_phase", &Tuning::seg_phase, nullptr},
       {"att_lean", &Tuning::att_lean, nullptr},
       {"att_direct", &Tuning::att_direct, nullptr},
@@ -3619,7 +3641,7 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
   int wm = WM_NONE, gsz = 1;
   if (w) {
     if (heads <= 0 || F % heads != 0) return fail(GTA_ERR_ARG, "aggregate: heads must divide F");
-    wm = (heads == F) ? WM_FULL : WM_HEAD;
+    wm = (heads == F) ? WM_FULL : ((heads == 1 && tuning().agg_w1) ? WM_EDGE1 : WM_HEAD);
     gsz = static_cast<int>(F / heads);
   }
   const int xm = (x_mode == GTA_IDX_EDGE) ? XM_EDGE : XM_IDX;
@@ -3652,7 +3674,7 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
   // the row): half the gather instructions of 8-B pieces for the same rows (GIN products' 200-B
   // rows: 13 lanes, 4 edges per wave instruction)
   bool vw8 = false;
-  if (bf && tuning().agg_bf16_vw8 && wm == WM_NONE && xm == XM_IDX && F % 4 == 0 && F >= 8 && F <= 512 &&
+  if (bf && tuning().agg_bf16_vw8 && (wm == WM_NONE || wm == WM_EDGE1) && xm == XM_IDX && F % 4 == 0 && F >= 8 && F <= 512 &&
       ldx % 4 == 0 && aligned(x, 8) && (!xs || (ldxs % 4 == 0 && aligned(xs, 8))) &&
       (y_bf16 ? (ldy % 4 == 0 && aligned(y, 8)) : (ldy % 4 == 0 && aligned(y, 16)))) {
     const int64_t ln = (F + 7) / 8;
@@ -3681,7 +3703,7 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
   // lean path: one edge per instruction exactly filling the wave, SpMM form
   int gl = (wm == WM_HEAD) ? gsz / vw : 0;
   const bool lean_shape = !bf && !y_bf16 && tuning().agg_lean && lpe == kWave && nv == 1 && F == kWave * vw && xm == XM_IDX &&
-                          !a.x_is_row && wm != WM_FULL && (wm == WM_NONE || gl == 4 || gl == 8 || gl == 16);
+                          !a.x_is_row && wm != WM_FULL && wm != WM_EDGE1 && (wm == WM_NONE || gl == 4 || gl == 8 || gl == 16);
   if (lean_shape) {
     const int64_t blocks = (bound + kWavesPerBlock - 1) / kWavesPerBlock;
     const dim3 grid(static_cast<unsigned>(blocks)), blk(kBlock);
@@ -3700,7 +3722,7 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
 #undef GTA_LEAN
     ok = true;
   }
-  if (!ok && vw8) ok = dispatch_bf16_vw8(lpe, tuning().agg_bf16_vw8, a, bound, s);
+  if (!ok && vw8) ok = dispatch_bf16_vw8(lpe, tuning().agg_bf16_vw8, wm, a, bound, s);
   if (!ok) switch (vw) {
     case 8: break;
     case 4: ok = dispatch_lpe<4>(lpe, nv, xm, wm, bf, a, bound, s); break;
@@ -4375,6 +4397,7 @@ int gta_update_mm(const void* x, int64_t ldx, const int32_t* row_idx, int64_t M,
   return GTA_OK;
 }
 
+extern "C++" {  // C++ helpers (WavePlan is returned by value) inside the C ABI block
 namespace {
 // k_mm_ring launch: NT (4: N <= 64, 8: wider), ring depth D (3 / 4 / 8: blocks per CU the grid
 // needs), FR (A fragments per wave); kslice > 0: the split-K form (grid.y = K slices)
@@ -4506,6 +4529,7 @@ inline int64_t mm_kslice(int64_t K, int64_t splits) {
   return std::max<int64_t>(16, (per + 15) / 16 * 16);
 }
 }  // namespace
+}  // extern "C++"
 
 int64_t gta_update_mm_t_splits(int64_t M, int64_t K, int64_t N, int dtype, void* stream) {
   const CallTuning ct_(stream);  // the stream's attached knob set decides mm_split, as for the GEMM itself

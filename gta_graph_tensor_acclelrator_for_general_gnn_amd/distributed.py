@@ -27,7 +27,7 @@ the node-side GEMM that feeds it (x W, 128 columns, not x, 602).
 import torch
 import torch.distributed as dist
 
-from . import partition
+from . import ops, partition
 from .graph import Graph
 
 
@@ -134,7 +134,7 @@ class DistShard:
             elif kind == "edge":
                 out[k] = t[self.edge_ids.to(t.device)].contiguous()
             elif kind == "node":
-                out[k] = t[self.c0:self.c1].contiguous()
+                out[k] = ops.pitched(t[self.c0:self.c1]) if t.dim() == 2 else t[self.c0:self.c1].contiguous()
             else:
                 out[k] = t
         return out
@@ -178,7 +178,9 @@ class RowShard:
         key = (id(t), t._version)  # the entry holds t, so its id stays unique (data_ptr is 0 for every empty tensor)
         hit = self._padded.get(key)
         if hit is None:
-            full = t.new_zeros(self.world * self.m, *t.shape[1:])
+            full = (ops.node_table(self.world * self.m, t.shape[1], t.dtype, t.device) if t.dim() == 2
+                    else t.new_empty(self.world * self.m, *t.shape[1:]))
+            full.zero_()
             for q in range(self.world):
                 a, b = self.cuts[q], self.cuts[q + 1]
                 full[q * self.m: q * self.m + b - a] = t[a:b]
@@ -202,7 +204,7 @@ class RowShard:
             elif kind == "edge":
                 out[k] = t[self.e0:self.e1].contiguous()
             elif kind == "node":
-                out[k] = t[self.r0:self.r1].contiguous()
+                out[k] = ops.pitched(t[self.r0:self.r1]) if t.dim() == 2 else t[self.r0:self.r1].contiguous()
                 self.inputs_full[k] = t
             else:
                 out[k] = t

@@ -11,6 +11,7 @@ One function per ISA op / fused pattern of the GTA stream:
   tile_nnz     calculate_sparsity (code/preprocessing.py:12-40)            -> gta_tile_nnz
 Shapes and strides are validated on the host before any launch.
 """
+import math
 import threading
 import weakref
 
@@ -48,6 +49,52 @@ def _rows(t, name, dtype=torch.float32):
     if t.stride(1) != 1 and t.shape[1] > 1 or t.stride(0) < t.shape[1]:
         raise ValueError(f"{name}: need a row-major 2-D tensor with unit column stride")
     return t.stride(0)
+
+
+LINE_BYTES = 128  # the L2 / fabric line a gathered row is fetched in (MI355X_MICROARCH.md)
+
+
+def _lines_per_row(row_bytes, pitch_bytes):
+    """Mean number of LINE_BYTES lines a row_bytes-long row touches when rows start every
+    pitch_bytes from a line-aligned base (the start offsets cycle with period line / gcd)."""
+    period = LINE_BYTES // math.gcd(pitch_bytes, LINE_BYTES)
+    return sum(-(-((r * pitch_bytes) % LINE_BYTES + row_bytes) // LINE_BYTES) for r in range(period)) / period
+
+
+def line_pitch(F, elem_size, max_extra=0.5):
+    """Row pitch (elements) of a node table the aggregates gather whole rows from: F rounded up to
+    whole 128-B lines when that lowers the mean number of lines a gathered row touches, at most
+    max_extra more bytes; F otherwise.  GIN products' bf16 model input: 200-B rows touch 2.56 lines
+    at a 200-B pitch and 2 at 256 B, and the layer's aggregate runs 5.38 -> 4.66 ms
+    (scripts/gin_ld_ab.py, bitwise the same sums).  fp32 rows of 128 floats are whole lines already."""
+    row = int(F) * int(elem_size)
+    if row == 0:
+        return F
+    padded = -(-row // LINE_BYTES) * LINE_BYTES
+    if padded == row or padded - row > max_extra * row:
+        return F
+    return padded // elem_size if _lines_per_row(row, padded) < _lines_per_row(row, row) else F
+
+
+def node_table(n, F, dtype, device=None):
+    """A [n, F] node table on line-pitched storage (line_pitch), the padding zero."""
+    P = line_pitch(F, torch.empty(0, dtype=dtype).element_size())
+    if P == F:
+        return torch.empty(n, F, dtype=dtype, device=device)
+    buf = torch.empty(n, P, dtype=dtype, device=device)
+    buf[:, F:].zero_()
+    return buf[:, :F]
+
+
+def pitched(t):
+    """A copy of the 2-D node table t on line-pitched storage (node_table): the layout a table
+    should have before the aggregates gather it, chosen once where the table is made (the model
+    input, a shard's rows, the all-gathered table), never per call."""
+    if t.dim() != 2:
+        return t.clone()
+    out = node_table(t.shape[0], t.shape[1], t.dtype, t.device)
+    out.copy_(t)
+    return out
 
 
 def _sf(sf):

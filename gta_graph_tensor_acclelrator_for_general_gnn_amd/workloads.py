@@ -2,7 +2,8 @@
 
 For an OpGraph this builds every tensor the executor needs, named as the
 executor looks them up:
-  "x"              model input [N, F_in] ~ N(0, 1)
+  "x"              model input [N, F_in] ~ N(0, 1), on line-pitched storage (ops.line_pitch: the
+                   layout the aggregates gather whole rows from, chosen once here)
   "w:<op>"         MM weights [F_in_op, F_out_op] ~ N(0, 1/F_in)  (applynode/applyedge MM)
   "ext:<op>:<s>"   external (-1) inputs: scalar edge weights [E, 1] (GCN 1/sqrt(d_i d_j)
                    normalisation for GCN/SGC, 1/deg(i) for GraphSAGE-mean, 1 for GIN),
@@ -13,6 +14,7 @@ Shapes follow the op YAML sizes (bytes / 4).
 import torch
 
 from . import graph as G
+from . import ops
 
 
 def make_tensors(opgraph, graph, network=None, seed=0, device=None, dtype_w=torch.float32, dtype_x=torch.float32):
@@ -37,7 +39,7 @@ def make_tensors(opgraph, graph, network=None, seed=0, device=None, dtype_w=torc
                 if w and (fin is None):
                     fin = w
     if fin is not None:
-        t["x"] = randn(n, fin).to(dtype_x)
+        t["x"] = ops.pitched(randn(n, fin).to(dtype_x))
     for op in opgraph.ops:
         if op.comp == "MM":
             k = op.in_width(0)

@@ -1381,3 +1381,65 @@ def test_aggregate_bf16_16B_pieces(dev, F, form):
         err = np.abs(got - ref)
         assert (err <= bound).all(), f"vw8={vw8}: max err {err.max():.3e}"
         outs[vw8] = y
+
+
+@pytest.mark.parametrize("F,dtype,mode", [(100, "bf16", "src"), (100, "bf16", "dst"), (100, "f32", "src"),
+                                          (128, "f32", "src"), (602, "f32", "dst"), (16, "f32", "src"),
+                                          (3, "f32", "edge"), (36, "bf16", "src")])
+@pytest.mark.parametrize("plan", [None, 64])
+def test_aggregate_one_weight_per_edge(dev, F, dtype, mode, plan):
+    """One weight per edge ([E, 1]: GCN's normalisation, GIN's edge operand) takes 64 weights per
+    load beside the indices, broadcast like them (knob agg_w1, default): bitwise equal to the
+    per-lane weight loads it replaces (agg_w1 = 0) in the same lane layout, and within the fp64
+    bound in every form (bf16: also the 16-B-piece form, GIN products' layer)."""
+    n, e = 450, 8000
+    g, ip, ix = _graph(n, e, seed=F + 7, heavy_row=1500, empty_rows=3, dev=dev)
+    rng = np.random.default_rng(F)
+    rows = g.nnz if mode == "edge" else n
+    xf = rng.standard_normal((rows, F)).astype(np.float32)
+    x = torch.from_numpy(xf).to(dev)
+    if dtype == "bf16":
+        x = x.to(torch.bfloat16)
+        xf = x.float().cpu().numpy()
+    w = (rng.random((g.nnz, 1)) + 0.5).astype(np.float32)
+    wd = torch.from_numpy(w).to(dev)
+    ref, mag = isa_ref.aggregate(ip, ix, xf, mode, w), isa_ref.aggregate_abs(ip, ix, xf, mode, w)
+    outs = {}
+    for w1 in (1, 0):
+        ops.set_debug("agg_w1", w1)
+        ops.set_debug("agg_bf16_vw8", 0)
+        try:
+            outs[w1] = ops.aggregate(g, x, mode, wd, plan=plan)
+        finally:
+            ops.set_debug("agg_w1", 1)
+            ops.set_debug("agg_bf16_vw8", 4)
+    y = ops.aggregate(g, x, mode, wd, plan=plan)  # the defaults (bf16: 16-B pieces)
+    torch.cuda.synchronize()
+    assert torch.equal(outs[1], outs[0])
+    for name, t in (("edge1", outs[1]), ("default", y)):
+        err = np.abs(t.cpu().numpy().astype(np.float64) - ref)
+        assert (err <= 1e-5 * mag + 1e-6).all(), f"{name}: max err {err.max():.3e}"
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+@pytest.mark.parametrize("form", ["plain", "self_bf16"])
+def test_aggregate_line_pitched_table(dev, weighted, form):
+    """A node table on line-pitched storage (ops.pitched: GIN products' 200-B bf16 rows at a 256-B
+    pitch, what workloads.make_tensors builds) gives bitwise the sums of the same values stored
+    contiguously: the pitch changes addresses only.  The table's last row is gathered too."""
+    g, ip, ix = _graph(500, 9000, seed=11, heavy_row=2000, empty_rows=4, dev=dev)
+    ix = ix.copy()
+    ix[:40] = 499
+    g = G.from_numpy(ip, ix, device=dev)
+    rng = np.random.default_rng(5)
+    x = torch.from_numpy(rng.standard_normal((500, 100)).astype(np.float32)).to(dev).to(torch.bfloat16)
+    xp = ops.pitched(x)
+    assert xp.stride(0) == 128 and torch.equal(xp, x)
+    wd = torch.from_numpy((rng.random((g.nnz, 1)) + 0.5).astype(np.float32)).to(dev) if weighted else None
+    s = torch.tensor([[1.1]], device=dev)
+    res = []
+    for t in (x, xp):
+        kw = {} if form == "plain" else {"self_term": (t, s), "out_dtype": torch.bfloat16}
+        res.append(ops.aggregate(g, t, "src", wd, plan=64, **kw))
+    torch.cuda.synchronize()
+    assert torch.equal(res[0], res[1])
