@@ -64,7 +64,7 @@ def _lines_per_row(row_bytes, pitch_bytes):
 def line_pitch(F, elem_size, max_extra=0.5):
     """Row pitch (elements) of a node table the aggregates gather whole rows from: F rounded up to
     whole 128-B lines when that lowers the mean number of lines a gathered row touches, at most
-    max_extra more bytes; F otherwise.  GIN products' bf16 model input: 200-B rows touch 2.56 lines
+    max_extra more bytes; F otherwise.  GIN products' bf16 model input: 200-B rows touch 2.5 lines
     at a 200-B pitch and 2 at 256 B, and the layer's aggregate runs 5.38 -> 4.66 ms
     (scripts/gin_ld_ab.py, bitwise the same sums).  fp32 rows of 128 floats are whole lines already."""
     row = int(F) * int(elem_size)
@@ -87,11 +87,15 @@ def node_table(n, F, dtype, device=None):
 
 
 def pitched(t):
-    """A copy of the 2-D node table t on line-pitched storage (node_table): the layout a table
-    should have before the aggregates gather it, chosen once where the table is made (the model
-    input, a shard's rows, the all-gathered table), never per call."""
+    """The 2-D node table t on line-pitched storage (node_table): t itself when its rows already
+    sit at that pitch (a row block of a pitched table is a view, no copy), else a copy.  The
+    layout a table should have before the aggregates gather it, chosen once where the table is
+    made (the model input, a shard's rows, the all-gathered table), never per call."""
     if t.dim() != 2:
-        return t.clone()
+        return t.contiguous()
+    P = line_pitch(t.shape[1], t.element_size())
+    if t.shape[0] > 1 and t.stride(1) == 1 and t.stride(0) == P:
+        return t
     out = node_table(t.shape[0], t.shape[1], t.dtype, t.device)
     out.copy_(t)
     return out

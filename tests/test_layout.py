@@ -36,8 +36,11 @@ def test_node_table_and_pitched():
     assert p.shape == x.shape and p.stride() == (128, 1) and torch.equal(p, x)
     base = p.as_strided((7, 128), (128, 1))
     assert torch.count_nonzero(base[:, 100:]) == 0  # zero padding
+    assert ops.pitched(p) is p and ops.pitched(p[2:5]).data_ptr() == p[2:5].data_ptr()  # already pitched: no copy
     q = ops.pitched(torch.randn(5, 128))
     assert q.is_contiguous()
+    flat = torch.randn(6, 100).to(torch.bfloat16)
+    assert ops.pitched(flat).stride(0) == 128 and ops.pitched(flat).data_ptr() != flat.data_ptr()
     t = ops.node_table(3, 602, torch.float32)
     assert t.shape == (3, 602) and t.stride(0) == 608
 
