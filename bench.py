@@ -542,9 +542,10 @@ def main():
     ap.add_argument("--n", "--graph-nodes", dest="n", type=int, default=N_REDDIT)
     ap.add_argument("--e", "--graph-edges", dest="e", type=int, default=E_REDDIT)
     ap.add_argument("--parity-rows", type=int, default=256, help="sampled rows per rank for the fp64 oracle")
-    ap.add_argument("--layers", default="sage-reddit,gin-products",
+    ap.add_argument("--layers", default="auto",
                     help="BASELINE-config layers timed after the metric at the same N (destination-row shards; "
-                         "'none' to skip): the 'layers' field")
+                         "'none' to skip; 'auto': every BASELINE config on one GPU -- GCN Cora, GAT-8 Flickr, "
+                         "GraphSAGE Reddit, GIN products -- and the two multi-GPU ones at N > 1): the 'layers' field")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-baseline-s", type=float, default=12.0,
                     help="CPU work per thread count of the cpu_baseline leg (seconds, approx.)")
@@ -768,7 +769,10 @@ def main():
     if args.layers and args.layers != "none":
         del agg
         torch.cuda.empty_cache()
-        result["layers"] = layers_leg(args.layers.split(","), world,
+        names = args.layers.split(",")
+        if args.layers == "auto":  # BASELINE.json configs #1-#4; #1 / #2 are one-GPU configs
+            names = (["gcn-cora", "gat8-flickr"] if world == 1 else []) + ["sage-reddit", "gin-products"]
+        result["layers"] = layers_leg(names, world,
                                       lambda name: distributed.layer_record(name, dev, rank, world, reps=3,
                                                                             backend=backend),
                                       lambda msg: log(rank, msg))
