@@ -1,7 +1,7 @@
 """Fabric traffic of the GIN products aggregate: rocprofv3 --pmc FETCH_SIZE and
 WRITE_SIZE, separate passes, over the exact launch the layer runs -- gta_aggregate_self over bf16
-200-B rows, (1 + eps) x formed in the epilogue, the executor's 512-edge plan, y stored in bf16 for
-the fused MLP (ABI 10) -- calibrated in the same pass like bench.py's metric traffic: a 1 GiB
+200-B rows (at the model input's line pitch, round 5), the layer's [E, 1] edge operand, (1 + eps) x
+formed in the epilogue, the executor's 512-edge plan, y stored in bf16 for the fused MLP (ABI 10) -- calibrated in the same pass like bench.py's metric traffic: a 1 GiB
 float4 copy gives the streaming read factor, and the same aggregate kernel over a permutation graph
 (one edge per row: every 200-B row of the 2.45 M-row bf16 table read once, in random order, 4 x
 64-B sectors each at 8-B alignment) gives this row gather's factor.  The real launch's FETCH is then
@@ -33,11 +33,12 @@ def child():
     _, g, tensors = configs.build("gin-products", dev)
     x = tensors[0]["x"]
     assert x.dtype == torch.bfloat16 and x.shape[1] == F, (x.dtype, x.shape)
+    w = next(v for k, v in tensors[0].items() if k.startswith("ext:") and tuple(v.shape) == (g.nnz, 1))
     s = torch.tensor([[1.1]], device=dev)
     n = g.n_rows
     if "--no-calib" in sys.argv:  # the layer's launches only (counter groups of scripts/pmc_sq.py)
         for _ in range(REPS + 1):
-            ops.aggregate(g, x, "src", None, plan=512, self_term=(x, s), out_dtype=torch.bfloat16)
+            ops.aggregate(g, x, "src", w, plan=512, self_term=(x, s), out_dtype=torch.bfloat16)
         torch.cuda.synchronize()
         return 0
     # streaming calibration: a float4 copy of a 1 GiB table (k_apply_node4: read once, written once)
@@ -56,10 +57,10 @@ def child():
     torch.cuda.synchronize()
     del gc, ip, perm
     for _ in range(REPS):
-        ops.aggregate(g, x, "src", None, plan=512, self_term=(x, s), out_dtype=torch.bfloat16)
+        ops.aggregate(g, x, "src", w, plan=512, self_term=(x, s), out_dtype=torch.bfloat16)
     torch.cuda.synchronize()
     with open(os.environ["GIN_PMC_META"], "w") as fh:
-        json.dump({"n": int(n), "e": int(g.nnz)}, fh)
+        json.dump({"n": int(n), "e": int(g.nnz), "pitch_bytes": int(x.stride(0) * x.element_size())}, fh)
     return 0
 
 
@@ -99,6 +100,9 @@ def main():
         res[ctr] = counters(d, ctr)
     m = json.load(open(meta))
     n, e = m["n"], m["e"]
+    pitch = m.get("pitch_bytes", 2 * F)
+    # the self-term row read in order: whole 64-B sectors of a line-pitched row, 200 B of a packed one
+    self_row = -(-2 * F // 64) * 64 if pitch % 64 == 0 else 2 * F
     fetch, write = res["FETCH_SIZE"], res["WRITE_SIZE"]
     copies = [v for k, v in fetch if k == "copy"]
     aggs = [v for k, v in fetch if k == "agg"]
@@ -107,22 +111,23 @@ def main():
     # gather (each row once: 4 x 64-B sectors at 8-B alignment, + 4 B index + 8 B row pointer)
     kr_s = CALIB_ROWS * 512 / (copies[1] * 1024.0)
     cal_streams = n * (4 + 8)
-    kr_g = n * 256 / ((aggs[1] - cal_streams / kr_s / 1024.0) * 1024.0)
+    kr_g = n * 256 / ((aggs[1] - cal_streams / kr_s / 1024.0) * 1024.0)  # 4 sectors per row at either pitch
     real_kb = sorted(aggs[2:2 + REPS])[REPS // 2]
     real_w_kb = sorted(aggs_w[2:2 + REPS])[REPS // 2]
-    # the real launch: known streams (indices 4 B per edge, row pointers 8 B and the self-term row
-    # 200 B per row, read in order) at kr_s, the rest of FETCH is row gathers at kr_g
-    streams = e * 4 + n * (8 + 200)
+    # the real launch: known streams (indices and edge weights 4 + 4 B per edge, row pointers 8 B and
+    # the self-term row per row, read in order) at kr_s, the rest of FETCH is row gathers at kr_g
+    streams = e * 8 + n * (8 + self_row)
     gathers = (real_kb * 1024.0 - streams / kr_s) * kr_g
     traffic = streams + gathers + real_w_kb * 1024.0
-    rec = {"what": "GIN products aggregate (gta_aggregate_self, bf16 200-B rows, plan 512, bf16 y)", "n": n, "e": e,
+    rec = {"what": "GIN products aggregate (gta_aggregate_self, bf16 200-B rows, [E, 1] edge weights, plan 512, bf16 y)",
+           "n": n, "e": e, "row_pitch_bytes": pitch,
            "fetch_kb": {"copy": copies[1], "gather_calibration": aggs[1], "launch_median": real_kb},
            "write_kb_launch_median": real_w_kb, "read_factor_stream": round(kr_s, 4),
            "read_factor_gather": round(kr_g, 4), "streams_GB": round(streams / 1e9, 3),
            "gathers_GB": round(gathers / 1e9, 3), "writes_GB": round(real_w_kb * 1024.0 / 1e9, 3),
            "traffic_GB": round(traffic / 1e9, 3), "gather_B_per_edge": round(gathers / e, 1),
            "sector_model_gather_B_per_edge": 256,
-           "algorithmic_GB": round((e * (4 + 200) + n * (8 + 200 + 200)) / 1e9, 3)}
+           "algorithmic_GB": round((e * (4 + 4 + 200) + n * (8 + 200 + 200)) / 1e9, 3)}
     print(json.dumps(rec))
     return 0
 
