@@ -246,10 +246,20 @@ def _edge_sums(cache, data, tt, fl):
             d = data.values if tt == data.length else _data_slice(data.dense(), tt)  # zeros add nothing
         else:
             d = _data_slice(data, tt)
-        cache[key] = {"nnz": int(d.sum()), "c8": int(((d + 7) // 8).sum()), "d": d}
+        # one histogram pass over the (106 M-entry) slice, then every sum over its distinct values:
+        # the same per-value expression as the element-wise form, times each value's count
+        d = np.asarray(d, dtype=np.int64)
+        try:
+            cnt = np.bincount(d) if d.size else np.zeros(1, np.int64)
+            v = np.arange(cnt.size, dtype=np.int64)
+            keep = cnt > 0
+            v, cnt = v[keep], cnt[keep]
+        except ValueError:  # a negative count (never from a tile list): the element-wise form
+            v, cnt = d, np.ones_like(d)
+        cache[key] = {"nnz": int((v * cnt).sum()), "c8": int((((v + 7) // 8) * cnt).sum()), "v": v, "cnt": cnt}
     ent = cache[key]
     if fl not in ent:
-        ent[fl] = int(np.ceil((ent["d"] * fl) / BW).sum())
+        ent[fl] = int((np.ceil((ent["v"] * fl) / BW).astype(np.int64) * ent["cnt"]).sum())
     return ent["nnz"], ent["c8"], ent[fl]
 
 
