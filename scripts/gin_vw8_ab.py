@@ -1,8 +1,8 @@
 """A/B of GIN products' aggregate: bf16 200-B rows in 8-B pieces (25 lanes, two
 edges per wave instruction) against 16-B pieces (13 lanes, four edges per wave instruction, knob
-agg_bf16_vw8), on the layer's exact launch (gta_aggregate_self: (1 + eps) x formed in the
-epilogue, 512-edge plan, bf16 y for the fused MLP), interleaved rounds, HIP events on the launch
-stream.  Prints one JSON line per form (median ms, G edges/s) and the max |d| between the forms.
+agg_bf16_vw8), on the layer's launch shape without its [E, 1] edge operand (gta_aggregate_self:
+(1 + eps) x formed in the epilogue, 512-edge plan, bf16 y for the fused MLP; scripts/gin_ld_ab.py
+times the weighted launch the layer makes), interleaved rounds, HIP events on the launch stream.  Prints one JSON line per form (median ms, G edges/s) and the max |d| between the forms.
 
 Usage: python scripts/gin_vw8_ab.py [--rounds R] [--reps K] [--ur N]"""
 import json
