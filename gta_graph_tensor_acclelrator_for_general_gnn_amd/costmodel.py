@@ -249,12 +249,13 @@ def _edge_sums(cache, data, tt, fl):
         # one histogram pass over the (106 M-entry) slice, then every sum over its distinct values:
         # the same per-value expression as the element-wise form, times each value's count
         d = np.asarray(d, dtype=np.int64)
-        try:
-            cnt = np.bincount(d) if d.size else np.zeros(1, np.int64)
+        lo, hi = (int(d.min()), int(d.max())) if d.size else (0, 0)
+        if 0 <= lo and hi < (1 << 22):  # tile counts are at most a tile's rows
+            cnt = np.bincount(d, minlength=1)
             v = np.arange(cnt.size, dtype=np.int64)
             keep = cnt > 0
             v, cnt = v[keep], cnt[keep]
-        except ValueError:  # a negative count (never from a tile list): the element-wise form
+        else:  # a negative or huge count (never from a tile list): the element-wise form
             v, cnt = d, np.ones_like(d)
         cache[key] = {"nnz": int((v * cnt).sum()), "c8": int((((v + 7) // 8) * cnt).sum()), "v": v, "cnt": cnt}
     ent = cache[key]
