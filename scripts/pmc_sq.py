@@ -3,6 +3,8 @@ within the per-block slot limits).  Targets (PMC_TARGET):
   metric (default) -- `bench.py --pmc-child`: the bench's own inputs and launches (k_agg_h32 + k_seg_reduce)
   gin              -- `scripts/gin_pmc.py --child --no-calib`: GIN products' aggregate exactly as the
                       layer launches it (k_aggregate<..., ushort> of gta_aggregate_self, bf16 y)
+  mm               -- `scripts/mm_pmc_child.py`: the Reddit x.W fp32 UPDATE ([232,965 x 602] at the
+                      model input's 608 pitch . [602 x 128], k_mm_wave), with the MFMA group
 Per-kernel means over the launches after the first (cold) one.
 Usage: python scripts/pmc_sq.py OUT_DIR [bench args]  -> OUT_DIR/<group>/... CSVs and OUT_DIR/summary.json"""
 import csv
@@ -21,12 +23,16 @@ GROUPS = {
                  "SQ_ACTIVE_INST_LDS", "SQ_INSTS_SMEM", "GRBM_GUI_ACTIVE"],
     "l2": ["TCC_HIT_sum", "TCC_MISS_sum", "TCP_TCC_READ_REQ_sum"],
     # the texture path (round 4): TA / TD busy and stall cycles, L1 -> L2 read latency
+    # MFMA occupancy and the effective clock (round 5): fp32 UPDATE
+    "mfma": ["SQ_VALU_MFMA_BUSY_CYCLES", "SQ_BUSY_CYCLES", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY",
+             "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU", "GRBM_GUI_ACTIVE"],
     "tex": ["TA_TA_BUSY_sum", "TA_ADDR_STALLED_BY_TC_CYCLES_sum", "TD_TD_BUSY_sum", "TD_TC_STALL_sum",
             "TCP_TCC_READ_REQ_LATENCY_sum", "TCP_TCC_READ_REQ_sum", "TCP_PENDING_STALL_CYCLES_sum", "GRBM_GUI_ACTIVE"],
 }
 TARGETS = {
     "metric": (["bench.py", "--pmc-child", "--steps", "4"], ("k_agg_h32", "k_seg_reduce")),
     "gin": (["scripts/gin_pmc.py", "--child", "--no-calib"], ("k_aggregate",)),
+    "mm": (["scripts/mm_pmc_child.py"], ("k_mm_wave",)),
 }
 TARGET = os.environ.get("PMC_TARGET", "metric")
 KERNELS = TARGETS[TARGET][1]
@@ -45,6 +51,8 @@ def summarize(d):
             k = _kernel(name)
             if k is None:
                 continue
+            if os.environ.get("PMC_SPLIT"):  # one entry per template instance (e.g. k_mm_wave<8, 4, 1>)
+                k = name.replace("(anonymous namespace)::", "").replace("void ", "").split("(")[0]
             did = int(row.get("Dispatch_Id") or row.get("Correlation_Id") or 0)
             per.setdefault((k, row["Counter_Name"]), []).append((did, float(row["Counter_Value"])))
     out = {}
