@@ -820,8 +820,10 @@ class Executor:
                         return NodeT(y)
             v = self._materialize_deferred(v)
         if isinstance(v, Scat):
-            view = c.view("dst" if v.mode == "dst" else "src")
-            y = ops.aggregate(view, v.t, "src", None, plan=self._plan())
+            if v.mode == "dst":  # the transposed aggregate: column-blocked like direction R when the table is large
+                y = self._spmm(v.t, "src", None, graph=c.view("dst"))
+            else:
+                y = ops.aggregate(c.view("src"), v.t, "src", None, plan=self._plan())
             self._count(E * (4 + v.t.shape[1] * v.t.element_size()) + nc * (8 + v.t.shape[1] * 4))
             return NodeT(y)
         xe = self._to_edge_tensor(v)
@@ -857,7 +859,10 @@ class Executor:
             view, table = c.view("dst" if x.mode == "dst" else "src"), x.t
         else:
             view, table = c.view("edge"), self._to_edge_tensor(x)
-        y = ops.aggregate(view, table, "src", wc, plan=self._plan())
+        if isinstance(x, Scat) and x.mode == "dst":  # column-blocked like direction R when the table is large
+            y = self._spmm(table, "src", wc, graph=view)
+        else:
+            y = ops.aggregate(view, table, "src", wc, plan=self._plan())
         F, H = table.shape[1], wc.shape[1]
         self._count(E * 8 * H + E * (4 + 4 * H + table.element_size() * F) + nc * (8 + 4 * F))
         return y
@@ -891,34 +896,37 @@ class Executor:
         self._count(E * (4 + 4 * wt.shape[1] + xt.element_size() * xt.shape[1]) + n * (8 + y.element_size() * xt.shape[1]))
         return y
 
-    def _spmm(self, xt, mode, wt, acc=None, self_term=None, out_dtype=torch.float32):
+    def _spmm(self, xt, mode, wt, acc=None, self_term=None, out_dtype=torch.float32, graph=None):
         """SpMM-form aggregate: column-blocked when the gathered table outgrows L2, else row-chunked.
         self_term (x, s): y = x * s + the aggregate in one launch (row-chunked form; None back when
         x's dtype is not the gathered table's, or when the column-blocked form is the better one:
-        the caller then accumulates into the formed x * s instead)."""
-        B = self._blocked_blocks(xt, mode, 0 if wt is None else wt.shape[1])
+        the caller then accumulates into the formed x * s instead).  graph: the graph the rows
+        and indices come from (default the layer's CSR; a CSC view for the ORDER-C gathers)."""
+        g = self.graph if graph is None else graph
+        B = self._blocked_blocks(xt, mode, 0 if wt is None else wt.shape[1], g)
         if self_term is not None:
             xs, sc = self_term
-            if B or xs.dtype != xt.dtype or xs.shape[1] != xt.shape[1] or xs.shape[0] < self.graph.n_rows:
+            if B or xs.dtype != xt.dtype or xs.shape[1] != xt.shape[1] or xs.shape[0] < g.n_rows:
                 return None
-            return ops.aggregate(self.graph, xt, mode, wt, plan=self._plan(), self_term=(xs, sc), out_dtype=out_dtype)
+            return ops.aggregate(g, xt, mode, wt, plan=self._plan(), self_term=(xs, sc), out_dtype=out_dtype)
         if B:
-            return ops.aggregate_blocked(self.graph, xt, wt, out=acc, accumulate=acc is not None, blocks=B)
-        return ops.aggregate(self.graph, xt, mode, wt, out=acc, accumulate=acc is not None, plan=self._plan())
+            return ops.aggregate_blocked(g, xt, wt, out=acc, accumulate=acc is not None, blocks=B)
+        return ops.aggregate(g, xt, mode, wt, out=acc, accumulate=acc is not None, plan=self._plan())
 
-    def _blocked_blocks(self, xt, mode, heads):
+    def _blocked_blocks(self, xt, mode, heads, graph=None):
         """Column blocks of the blocked aggregate for this gathered table, or 0 for the row-chunked
         form: a source table of at least blocked_min_table_bytes (its own element size) of a dtype
         and width the blocked kernels take."""
+        g = self.graph if graph is None else graph
         if not (mode == "src" and self.blocked_blocks and xt.dtype in ops.BlockedPlan.DTYPES
                 and xt.shape[0] * xt.shape[1] * xt.element_size() >= self.blocked_min_table_bytes
                 and ops.BlockedPlan.supports(xt.shape[1], heads, xt.dtype)):
             return 0
         B = self.blocked_blocks
         if B == "auto":
-            B = ops.BlockedPlan.auto_blocks(self.graph, xt.shape[1], xt.element_size())
+            B = ops.BlockedPlan.auto_blocks(g, xt.shape[1], xt.element_size())
             B = B if B >= 4 else 0
-        return B if B and self.graph.blocked_plan(B).sorted else 0
+        return B if B and g.blocked_plan(B).sorted else 0
 
     def _unweighted(self, x):
         if isinstance(x, Scat):

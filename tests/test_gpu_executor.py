@@ -10,7 +10,7 @@ import numpy as np
 import pytest
 import torch
 
-from gta_graph_tensor_acclelrator_for_general_gnn_amd import executor, graph as G, ir, workloads
+from gta_graph_tensor_acclelrator_for_general_gnn_amd import executor, graph as G, ir, ops, workloads
 from gta_graph_tensor_acclelrator_for_general_gnn_amd.semantics import Semantics
 from oracle import isa_ref
 from oracle.exec_ref import execute_ref
@@ -467,3 +467,65 @@ def test_bf16_source_table_takes_the_row_chunked_aggregate(golden_dir, manifest,
         ref = isa_ref.aggregate(ip, ix, xr, "src", wr)
         bound = 1e-5 * isa_ref.aggregate_abs(ip, ix, xr, "src", wr) + 1e-6
         assert np.all(np.abs(y.cpu().numpy() - ref) <= bound)
+
+
+BIDIR_STREAMS = [s for s in STREAMS if s["network"] == "BIDIR"][:2]
+
+
+@pytest.mark.parametrize("rec", BIDIR_STREAMS, ids=[r["file"][:-5] for r in BIDIR_STREAMS])
+def test_gather_c_column_blocked_on_gpu(golden_dir, cora, dev, rec):
+    """ORDER-C gather of a scatter-R operand (the transposed aggregate, BIDIR op 3) takes the
+    column-blocked kernels over the CSC "dst" view when its table is large, as direction R does
+    (forced on Cora: size gate 0, B = 4); every op per element within the bound at every row."""
+    sem = Semantics.for_network(rec["network"], rec["reorder"])
+    og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+    ip, ix = cora
+    gd = G.from_numpy(ip, ix, device=dev)
+    tc = workloads.make_tensors(og, G.from_numpy(ip, ix), rec["network"], seed=3)
+    ex = executor.Executor(og, st, gd, {k: v.to(dev) for k, v in tc.items()}, sem)
+    ex.blocked_min_table_bytes, ex.blocked_blocks = 0, 4
+    ex.run()
+    torch.cuda.synchronize()
+    view = ops.csc(gd).view("dst")
+    assert any(isinstance(k, tuple) and k[0] == "blocked" for k in view._plans)
+    chk = SampledChecker(ex, ip, ix)
+    chk.check(n_samples=1 << 30, n_gather=1 << 30)
+
+
+@pytest.mark.parametrize("H", [0, 1, 8])
+def test_transposed_spmm_column_blocked(cora, dev, H):
+    """The executor's SpMM over the CSC "dst" view (y[j] = sum over the edges whose source is j of
+    w(e) x[dst(e)]): column-blocked (B = 4) and row-chunked forms, unweighted, one weight per edge
+    and 8 heads, against the fp64 restatement at the per-element bound."""
+    ip, ix = cora
+    gd = G.from_numpy(ip, ix, device=dev)
+    rec = [s for s in STREAMS if s["network"] == "BIDIR"][0]
+    sem = Semantics.for_network("BIDIR", False)
+    golden = os.path.join(os.path.dirname(__file__), "golden")
+    og = ir.OpGraph.load(os.path.join(golden, "ops", rec["op_yaml"]), sem.inputs)
+    st = ir.Stream.load(os.path.join(golden, "streams", rec["file"]))
+    tc = workloads.make_tensors(og, G.from_numpy(ip, ix), "BIDIR", seed=1)
+    ex = executor.Executor(og, st, gd, {k: v.to(dev) for k, v in tc.items()}, sem)
+    view = ops.csc(gd).view("dst")
+    rng = np.random.default_rng(H)
+    n, E = len(ip) - 1, len(ix)
+    x = rng.standard_normal((n, 128)).astype(np.float32)
+    w = (rng.random((E, H)) + 0.5).astype(np.float32) if H else None
+    dst = np.repeat(np.arange(n), np.diff(ip))
+    perm = np.argsort(ix, kind="stable")  # CSC order: a column's edges in CSR order
+    xe = x[dst].astype(np.float64)
+    if H:
+        xe = xe * np.repeat(w.astype(np.float64), 128 // H, axis=1)
+    ref = np.zeros((n, 128))
+    mag = np.zeros((n, 128))
+    np.add.at(ref, ix, xe)
+    np.add.at(mag, ix, np.abs(xe))
+    wc = None if w is None else torch.from_numpy(w[perm]).to(dev)
+    xd = torch.from_numpy(x).to(dev)
+    for blocked in (4, 0):
+        ex.blocked_min_table_bytes, ex.blocked_blocks = 0, blocked
+        y = ex._spmm(xd, "src", wc, graph=view)
+        torch.cuda.synchronize()
+        err = np.abs(y.cpu().numpy() - ref)
+        assert (err <= 1e-5 * mag + 1e-6).all(), (blocked, float(err.max()))
