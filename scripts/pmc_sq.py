@@ -3,6 +3,8 @@ within the per-block slot limits).  Targets (PMC_TARGET):
   metric (default) -- `bench.py --pmc-child`: the bench's own inputs and launches (k_agg_h32 + k_seg_reduce)
   gin              -- `scripts/gin_pmc.py --child --no-calib`: GIN products' aggregate exactly as the
                       layer launches it (k_aggregate<..., ushort> of gta_aggregate_self, bf16 y)
+  wcost            -- `scripts/sage_w1_probe.py --pmc-child`: the Reddit blocked pair unweighted, with [E, 1]
+                      and with [E, 8] weights (PMC_SPLIT=1 keeps the k_agg_h32 instances apart)
   mm               -- `scripts/mm_pmc_child.py`: the Reddit x.W fp32 UPDATE ([232,965 x 602] at the
                       model input's 608 pitch . [602 x 128], k_mm_wave), with the MFMA group
 Per-kernel means over the launches after the first (cold) one.
@@ -33,6 +35,7 @@ TARGETS = {
     "metric": (["bench.py", "--pmc-child", "--steps", "4"], ("k_agg_h32", "k_seg_reduce")),
     "gin": (["scripts/gin_pmc.py", "--child", "--no-calib"], ("k_aggregate",)),
     "mm": (["scripts/mm_pmc_child.py"], ("k_mm_wave",)),
+    "wcost": (["scripts/sage_w1_probe.py", "--pmc-child"], ("k_agg_h32",)),
 }
 TARGET = os.environ.get("PMC_TARGET", "metric")
 KERNELS = TARGETS[TARGET][1]

@@ -16,7 +16,21 @@ sys.path.insert(0, ROOT)
 from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G, ops  # noqa: E402
 
 
+def pmc_child():
+    """Under rocprofv3 --pmc (scripts/pmc_sq.py PMC_TARGET=wcost): each form's launch pair 4 times."""
+    dev = torch.device("cuda", 0)
+    g = G.dataset_graph("reddit", device=dev)
+    x = torch.randn(g.n_rows, 128, device=dev)
+    for w in (None, torch.rand(g.nnz, 1, device=dev) + 0.5, torch.rand(g.nnz, 8, device=dev) + 0.5):
+        for _ in range(4):
+            ops.aggregate_blocked(g, x, w, blocks=20)
+        torch.cuda.synchronize()
+    return 0
+
+
 def main():
+    if "--pmc-child" in sys.argv:
+        return pmc_child()
     rounds = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 5
     reps = int(sys.argv[sys.argv.index("--reps") + 1]) if "--reps" in sys.argv else 10
     dev = torch.device("cuda", 0)
@@ -42,4 +56,4 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())
