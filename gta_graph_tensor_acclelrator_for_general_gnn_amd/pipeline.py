@@ -16,7 +16,9 @@ class Layer:
     """One compiled GNN layer bound to a graph: op graph, chosen partition, stream."""
 
     def __init__(self, network, layer, graph, feature, reorder=False, heads=16, candidate=0, tile_start=None,
-                 op_array=None, tile_size_list=None, metadata=None):
+                 op_array=None, tile_size_list=None, metadata=None, pingpang=True, sinput=False):
+        """pingpang / sinput: compile()'s isPingpang / isSinput (code/compiler.py:475-510) for the
+        fusion search; the reference's start.py passes its command-line flags through."""
         self.network, self.layer, self.reorder = network, layer, reorder
         self.graph = graph
         self.records = frontend.gen_ops(network, layer, graph.n_rows, graph.nnz, feature, reorder, heads)
@@ -29,7 +31,7 @@ class Layer:
                 metadata = tiles.metadata(graph, start=tile_start or 64, end=min(graph.n_rows, 4096))
             self.metadata = metadata
             sizes, maxl = metadata
-            cands = compiler.search(self.records, graph.n_rows, sizes, maxl, pingpang=True)
+            cands = compiler.search(self.records, graph.n_rows, sizes, maxl, pingpang=pingpang, sinput=sinput)
             self.candidates = cands
             if cands:
                 op_array, tile_size_list = cands[min(candidate, len(cands) - 1)][:2]
