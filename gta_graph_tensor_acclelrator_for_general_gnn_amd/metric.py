@@ -41,19 +41,16 @@ def x_rows(ids, device, seed=SEED, f=F):
 
 def alpha_rows(lip, gen, device, seed=SEED, heads=HEADS):
     """alpha [E_rows, H] fp32 of a row range in CSR order: softmax over each row's in-edges, per head,
-    of N(0, 1) logits keyed by the edge's generation id.  Row sums in fp64 via a prefix sum
-    (deterministic, order-independent to fp64 rounding), one fp32 divide per edge."""
+    of N(0, 1) logits keyed by the edge's generation id.  Row sums in fp64, one segment per row summed
+    in edge order (deterministic, and the same whatever row range a rank generates), one fp32 divide
+    per edge.  (Until round 5 the sums were differences of one fp64 prefix sum over the rank's
+    edges, whose rounding depended on where the rank's range started.)"""
     if gen.numel() == 0:
         return torch.empty(0, heads, device=device)
     k = gen[:, None] * heads + torch.arange(heads, device=device, dtype=torch.int64)
     ex = torch.exp(G.hash_normal(k, seed, STREAM_LOGIT))
     del k
-    # [H, E+1] so each head's prefix sum runs along the contiguous dimension (torch's outer-dim
-    # scan of an [E, H] tensor takes tens of seconds at E = 1e8)
-    c = torch.zeros(heads, gen.numel() + 1, device=device, dtype=torch.float64)
-    torch.cumsum(ex.t().double(), 1, out=c[:, 1:])
-    s = (c[:, lip[1:]] - c[:, lip[:-1]]).t().to(torch.float32)  # [n_rows, H]
-    del c
+    s = torch.segment_reduce(ex.double(), "sum", lengths=lip[1:] - lip[:-1], axis=0).to(torch.float32)  # [n_rows, H]
     row = torch.repeat_interleave(torch.arange(lip.numel() - 1, device=device), lip[1:] - lip[:-1])
     return ex.div_(s[row])
 
