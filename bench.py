@@ -525,6 +525,9 @@ def rank_roofline(per_rank, peak=PEAK_HBM_GBS):
 
 # ----------------------------------------------------------------------------------------------
 def main():
+    if os.environ.get("GTA_STALL_DUMP"):  # diagnostics: every rank prints its Python stack every S seconds
+        import faulthandler
+        faulthandler.dump_traceback_later(float(os.environ["GTA_STALL_DUMP"]), repeat=True, file=sys.stderr)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
