@@ -430,6 +430,28 @@ def oracle_parity(shard, y_own, owned, k=256):
     return float((err / bound).max()), float(err.max()), len(s["rows"])
 
 
+def gin_bf16_accuracy(dev, n_random=64):
+    """gin-products' bf16 storage choice (x, W5, W7 in bf16) against fp64 of the UNROUNDED fp32
+    inputs at sampled rows (oracle/sampled.gin_unrounded_errors, SURVEY.md §8c rtol 2e-2; the
+    full-size test is tests/test_gpu_configs.py::test_gin_products_bf16_vs_fp64_of_unrounded_inputs).
+    One eager forward, after the timed layers."""
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import configs, workloads
+    from oracle.sampled import SampledChecker, gin_unrounded_errors
+    results, g = configs.run("gin-products", dev)
+    lay, _, ex = results[0]
+    t32 = workloads.make_tensors(lay.opgraph, g, "GIN", seed=0)
+    ip, ix = g.numpy()
+    chk = SampledChecker(ex, ip, ix)
+    sp = np.concatenate(list(chk.special_rows().values()))
+    rows = np.unique(np.concatenate([sp, np.random.default_rng(3).choice(g.n_rows, n_random, replace=False)]))
+    errs = gin_unrounded_errors(chk, t32, rows)
+    return {"check": f"bf16 layer vs fp64 of the unrounded fp32 x / W5 / W7 on {len(rows)} rows "
+                     "(special rows + random), per op: max|d| / max|ref|", "rtol": 2e-2,
+            "max_rel_err": {f"op{k}": round(v[0], 6) for k, v in errs.items()},
+            "max_err_over_terms": {f"op{k}": round(v[1], 6) for k, v in errs.items()},
+            "within_rtol": all(v[0] <= 2e-2 and v[1] <= 2e-2 for v in errs.values())}
+
+
 def cpu_quota():
     """CPUs of the cgroup v2 quota (cpu.max), or None."""
     try:
@@ -779,6 +801,14 @@ def main():
                                       lambda name: distributed.layer_record(name, dev, rank, world, reps=3,
                                                                             backend=backend),
                                       lambda msg: log(rank, msg))
+        for rec in result["layers"]:  # the bf16 choice's accuracy beside its time
+            if rec.get("config") == "gin-products" and world == 1 and "error" not in rec:
+                try:
+                    rec["bf16_vs_fp64_unrounded"] = gin_bf16_accuracy(dev)
+                except Exception as exc:  # reported, not fatal
+                    rec["bf16_vs_fp64_unrounded"] = {"error": f"{type(exc).__name__}: {exc}"[:300]}
+                log(rank, f"gin-products bf16 accuracy: {rec['bf16_vs_fp64_unrounded']}")
+                torch.cuda.empty_cache()
     if rank == 0 and not args.no_cpu_baseline:  # after the timed region; other ranks wait at the barrier
         log(rank, "cpu baseline")
         result["cpu_baseline"] = cpu_baseline(shard, target_s=args.cpu_baseline_s)

@@ -10,7 +10,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgta.so")
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 # enum mirrors of include/gta.h
 GTA_F32, GTA_BF16, GTA_F32_BF16 = 0, 1, 2
@@ -58,6 +58,9 @@ SIGNATURES = {
     "gta_update_mm_t_split": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _i64, _vp,
                                      _i64, _vp]),
     "gta_tile_nnz": (_i32, [_vp, _vp, _i64, _i64, _i64, _vp, _vp]),
+    "gta_synth_alpha": (_i32, [_vp, _vp, _i64, _i64, _i32, _i64, _i64, _vp, _vp]),
+    "gta_row_ids": (_i32, [_vp, _i64, _i64, _vp, _vp]),
+    "gta_build_id": (_cp, []),
     "gta_debug_set": (_i32, [_cp, _i64]),
     "gta_debug_get": (_i32, [_cp, ctypes.POINTER(_i64)]),
     "gta_tuning_create": (_vp, []),
@@ -94,8 +97,25 @@ def load(path=LIB_PATH):
         v = lib.gta_abi_version()
         if v != ABI_VERSION:
             raise GTAError(f"libgta ABI {v} != expected {ABI_VERSION}; rebuild")
+        check_build_id(lib.gta_build_id().decode(), path)
         _lib = lib
         return lib
+
+
+def check_build_id(built, path=LIB_PATH):
+    """Refuse a library compiled from other sources than the ones beside it:
+    the id is a hash of csrc/gta_kernels.hip + include/gta.h taken at build time (_build.py).
+    Where the sources are absent (a library shipped alone) there is nothing to compare against."""
+    from . import _build
+    want = _build.source_id()
+    if want is not None and built != want:
+        raise GTAError(f"{path} was built from other sources (build id {built}, sources {want}): "
+                       "stale libgta.so -- rebuild with __graft_entry__.build()")
+
+
+def build_id():
+    """The build id of the loaded libgta.so (first 16 hex digits of the sources' sha256)."""
+    return load().gta_build_id().decode()
 
 
 def check(rc, what):

@@ -2752,13 +2752,26 @@ k_mm_wave(const float* __restrict__ x, int64_t ldx, int64_t M, int K, const floa
       step(a2, b0, b1, a1, t + 2);
       step(a3, b1, b0, a2, t + 3);
     }
+    // nested, so the control-flow graph holds only the feasible paths (a third step always follows
+    // the first two): asmcheck.py's path-insensitive wait analysis then proves every operand landed
     const int rem = SF - t;
-    if (rem >= 1) step(a0, b0, b1, a3, t);
-    if (rem >= 2) step(a1, b1, b0, a0, t + 1);
-    if (rem >= 3) step(a2, b0, b1, a1, t + 2);
+    if (rem >= 1) {
+      step(a0, b0, b1, a3, t);
+      if (rem >= 2) {
+        step(a1, b1, b0, a0, t + 1);
+        if (rem >= 3) step(a2, b0, b1, a1, t + 2);
+      }
+    }
     // the loads issued past the last stage, and the stores below, drained before the next unit
     // counts its own loads
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // ... and every load target kept live until that wait: a stage loaded past the end is dead, and
+    // the compiler gave such registers to other values while the load was still in flight (a late
+    // return then overwrote them; asmcheck.py found it in the remainder of k_mm_wave<8, 4, 1>)
+#pragma unroll
+    for (int i = 0; i < FR; ++i) asm volatile("" ::"v"(a0[i]), "v"(a1[i]), "v"(a2[i]), "v"(a3[i]));
+#pragma unroll
+    for (int c = 0; c < NT; ++c) asm volatile("" ::"v"(b0[c]), "v"(b1[c]));
     store_tile(acc, sf, out, ldo, M, N, mw, n0, lane, vstore);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -3340,6 +3353,76 @@ k_tile_nnz(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indic
     // a dense adjacency holds each (row, j) once: skip self loops and repeats of the previous column
     if (j != row && (e == eb || indices[e - 1] != j)) atomicAdd(base + j, 1);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Synthetic-workload setup (the bench's GAT alpha and CSR row ids), ABI 12.  One wave per row and
+// no dependency between workgroups: no device-wide scan, sort or look-back, so a shard builds the
+// same way whatever else shares the GPU (the 8-process one-GPU rehearsal stalled in
+// torch's scan-based segment_reduce / repeat_interleave).
+// ---------------------------------------------------------------------------
+// graph.mix32 / graph.hash32: the lowbias32 counter hash, in uint32 arithmetic (the Python form
+// masks to 32 bits at the same points, so the two agree bit for bit).
+__host__ __device__ inline uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  return x ^ (x >> 16);
+}
+
+__host__ __device__ inline uint32_t hash_key(int64_t seed, int64_t stream) {  // key of graph.hash32, before mix32
+  return static_cast<uint32_t>((static_cast<uint64_t>(seed) * 0x9E3779B9ull + static_cast<uint64_t>(stream) * 0x85EBCA6Bull +
+                                0x27D4EB2Full) & 0xFFFFFFFFull);
+}
+
+// graph.hash_normal(idx, seed, stream) for one idx: Box-Muller in fp64 on two counter hashes, each
+// operation rounded where torch rounds it (one kernel per op there), then one cast to fp32.
+__device__ __forceinline__ float hash_normal1(uint64_t idx, uint32_t k1, uint32_t s1, uint32_t k2, uint32_t s2) {
+  const uint32_t lo = static_cast<uint32_t>(idx);
+  const uint32_t h1 = mix32(mix32(lo ^ k1) + s1), h2 = mix32(mix32(lo ^ k2) + s2);
+  const double u1 = (static_cast<double>(h1) + 0.5) * (1.0 / 4294967296.0);
+  const double u2 = static_cast<double>(h2) * (1.0 / 4294967296.0);
+  const double r = sqrt(-2.0 * log(u1));
+  const double c = cos(6.283185307179586 * u2);
+  return static_cast<float>(r * c);
+}
+
+// alpha[e, h] = ex[e, h] / s[row(e), h], ex = exp(hash_normal(gen[e] * H + h)), s = the row's fp64
+// sum of ex in edge order, cast to fp32 (metric.alpha_rows).  Lane = (edge slot e % (64 / H), head
+// h); the serial sum runs in every lane of head h (shuffles from the slots in edge order), so it
+// adds the same values in the same order as a one-thread-per-(row, head) loop.
+__global__ void __launch_bounds__(kBlock)
+k_synth_alpha(const int64_t* __restrict__ indptr, const int64_t* __restrict__ gen, int64_t n_rows, int H,
+              uint32_t k1, uint32_t s1, uint32_t k2, uint32_t s2, float* __restrict__ out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  const int per = kWave / H, slot = lane / H, h = lane % H;
+  const int64_t eb = indptr[row], ee = indptr[row + 1];
+  double s = 0.0;
+  for (int64_t e0 = eb; e0 < ee; e0 += per) {
+    const int64_t e = e0 + slot;
+    float ex = 0.f;
+    if (e < ee) {
+      ex = expf(hash_normal1(static_cast<uint64_t>(gen[e]) * static_cast<uint64_t>(H) + static_cast<uint64_t>(h), k1, s1,
+                             k2, s2));
+      out[e * H + h] = ex;
+    }
+    const int n = static_cast<int>(min<int64_t>(per, ee - e0));
+    for (int j = 0; j < n; ++j) s += static_cast<double>(__shfl(ex, j * H + h));
+  }
+  const float sf = static_cast<float>(s);
+  for (int64_t e = eb + slot; e < ee; e += per) out[e * H + h] = out[e * H + h] / sf;
+}
+
+// row id of every CSR edge (torch.repeat_interleave(arange(n_rows), degrees)), int64
+__global__ void __launch_bounds__(kBlock)
+k_row_ids(const int64_t* __restrict__ indptr, int64_t n_rows, int64_t* __restrict__ out) {
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  if (row >= n_rows) return;
+  for (int64_t e = indptr[row] + lane; e < indptr[row + 1]; e += kWave) out[e] = row;
 }
 
 // ---------------------------------------------------------------------------
@@ -4761,5 +4844,35 @@ int gta_tile_nnz(const int64_t* indptr, const int32_t* indices, int64_t n_rows, 
   GTA_LAUNCHED("k_tile_nnz");
   return GTA_OK;
 }
+
+int gta_synth_alpha(const int64_t* indptr, const int64_t* gen, int64_t n_rows, int64_t nnz, int heads, int64_t seed,
+                    int64_t logit_stream, float* out, void* stream) {
+  if (!indptr || n_rows < 0 || nnz < 0 || heads <= 0 || heads > kWave || kWave % heads != 0 || seed < 0 ||
+      logit_stream < 0 || (nnz > 0 && (!gen || !out)))
+    return fail(GTA_ERR_ARG, "synth_alpha: bad arguments (heads must divide 64)");
+  if (n_rows == 0 || nnz == 0) return GTA_OK;
+  const uint32_t s1 = static_cast<uint32_t>(2 * logit_stream), s2 = s1 + 1u;
+  const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+  k_synth_alpha<<<grid, dim3(kBlock), 0, S(stream)>>>(indptr, gen, n_rows, heads, mix32(hash_key(seed, s1)), s1,
+                                                     mix32(hash_key(seed, s2)), s2, out);
+  GTA_LAUNCHED("k_synth_alpha");
+  return GTA_OK;
+}
+
+int gta_row_ids(const int64_t* indptr, int64_t n_rows, int64_t nnz, int64_t* out, void* stream) {
+  if (!indptr || n_rows < 0 || nnz < 0 || (nnz > 0 && !out)) return fail(GTA_ERR_ARG, "row_ids: bad arguments");
+  if (n_rows == 0 || nnz == 0) return GTA_OK;
+  const dim3 grid(static_cast<unsigned>((n_rows + kWavesPerBlock - 1) / kWavesPerBlock));
+  k_row_ids<<<grid, dim3(kBlock), 0, S(stream)>>>(indptr, n_rows, out);
+  GTA_LAUNCHED("k_row_ids");
+  return GTA_OK;
+}
+
+// _build.py passes a hash of this file and include/gta.h; _lib.load() refuses a library whose id
+// differs from the sources beside it (a stale binary never runs silently)
+#ifndef GTA_BUILD_ID
+#define GTA_BUILD_ID "unversioned"
+#endif
+const char* gta_build_id(void) { return GTA_BUILD_ID; }
 
 }  // extern "C"

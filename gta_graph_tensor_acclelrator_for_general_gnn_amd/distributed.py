@@ -27,7 +27,7 @@ the node-side GEMM that feeds it (x W, 128 columns, not x, 602).
 import torch
 import torch.distributed as dist
 
-from . import ops, partition
+from . import graph as G, ops, partition
 from .graph import Graph
 
 
@@ -501,8 +501,7 @@ class GridShard:
         self.mks = [b - a for a, b in zip(self.offs[:-1], self.offs[1:])]
         self.mk = -(-self.m // self.chunks)  # the equal-chunk size (rows mode pads every rank's chunks to it)
         keep = (src >= c0) & (src < c1)
-        deg = lip[1:] - lip[:-1]
-        rows = torch.repeat_interleave(torch.arange(r1 - r0, device=dev), deg)[keep]
+        rows = G.expand_rows(lip, src.numel())[keep]
         local_src = (src[keep] - c0).to(torch.int32)
         self.local_edge_ids = torch.nonzero(keep, as_tuple=False).flatten()
         if self.chunks > 1:  # chunk-major padded rows; a stable sort keeps each row's edge order

@@ -237,7 +237,7 @@ class CounterCSR:
         e0, e1 = int(self.indptr_np[r0]), int(self.indptr_np[r1])
         src = self.sources(e0, e1, device)
         lip = (ip[r0:r1 + 1] - e0).contiguous()
-        row = torch.repeat_interleave(torch.arange(r1 - r0, device=device, dtype=torch.int64), lip[1:] - lip[:-1])
+        row = expand_rows(lip, e1 - e0)
         order = torch.sort(row * self.n + src, stable=True).indices  # duplicates keep generation order
         del row
         return lip, src[order].contiguous(), order + e0
@@ -263,6 +263,17 @@ def gcn_norm_weights(graph):
 def mean_weights(graph):
     """SAGE-mean row scale 1/deg(i) (0-degree rows scale by 1)."""
     return 1.0 / graph.degrees().to(torch.float32).clamp_min(1.0)
+
+
+def expand_rows(lip, nnz):
+    """int64 [nnz]: the row of each edge of a CSR row range (lip local, from 0).  On the device this
+    is libgta's one-wave-per-row gta_row_ids, not torch.repeat_interleave, whose device-wide scan
+    stalled the 8-process one-GPU rehearsal; on the CPU, repeat_interleave."""
+    if lip.is_cuda:
+        from . import ops
+        return ops.row_ids(lip, nnz)
+    return torch.repeat_interleave(torch.arange(lip.numel() - 1, device=lip.device, dtype=torch.int64),
+                                   lip[1:] - lip[:-1])
 
 
 def ceil_div(a, b):

@@ -44,7 +44,22 @@ def alpha_rows(lip, gen, device, seed=SEED, heads=HEADS):
     of N(0, 1) logits keyed by the edge's generation id.  Row sums in fp64, one segment per row summed
     in edge order (deterministic, and the same whatever row range a rank generates), one fp32 divide
     per edge.  (Until round 5 the sums were differences of one fp64 prefix sum over the rank's
-    edges, whose rounding depended on where the rank's range started.)"""
+    edges, whose rounding depended on where the rank's range started.)
+
+    On the device this is one libgta launch (gta_synth_alpha: a wave per row, no device-wide scan;
+    round 6, after torch's segment_reduce / repeat_interleave stalled the 8-process one-GPU
+    rehearsal); alpha_rows_torch is the same formula in torch ops, the CPU path and the GPU test's
+    bitwise reference (tests/test_gpu_metric.py)."""
+    if gen.numel() == 0:
+        return torch.empty(0, heads, device=device)
+    if torch.device(device).type == "cuda":
+        from . import ops
+        return ops.synth_alpha(lip.to(device), gen.to(device), heads, seed, STREAM_LOGIT)
+    return alpha_rows_torch(lip, gen, device, seed, heads)
+
+
+def alpha_rows_torch(lip, gen, device, seed=SEED, heads=HEADS):
+    """alpha_rows in torch ops (exp of the hashed logits, torch.segment_reduce's fp64 row sums)."""
     if gen.numel() == 0:
         return torch.empty(0, heads, device=device)
     k = gen[:, None] * heads + torch.arange(heads, device=device, dtype=torch.int64)

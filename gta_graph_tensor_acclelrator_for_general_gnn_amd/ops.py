@@ -703,6 +703,30 @@ def tile_nnz(graph, T):
     return counts
 
 
+def synth_alpha(indptr, gen, heads, seed, logit_stream):
+    """GAT alpha [nnz, heads] fp32 of a CSR row range (indptr local, from 0) from counter-hashed
+    logits keyed by gen[e] * heads + h: per-row softmax with an fp64 edge-order row sum
+    (gta_synth_alpha; metric.alpha_rows).  One wave per row, no device-wide scan."""
+    _need_gpu(indptr, gen)
+    indptr = indptr.to(torch.int64).contiguous()
+    gen = gen.to(torch.int64).contiguous()
+    n_rows, nnz = indptr.numel() - 1, gen.numel()
+    out = torch.empty(nnz, heads, dtype=torch.float32, device=gen.device)
+    check(_L().gta_synth_alpha(_ptr(indptr), _ptr(gen), n_rows, nnz, int(heads), int(seed), int(logit_stream), _ptr(out),
+                               _stream(gen.device)), "synth_alpha")
+    return out
+
+
+def row_ids(indptr, nnz):
+    """int64 [nnz]: the row of every CSR edge (torch.repeat_interleave(arange, degrees) without a
+    device-wide scan; gta_row_ids)."""
+    _need_gpu(indptr)
+    indptr = indptr.to(torch.int64).contiguous()
+    out = torch.empty(int(nnz), dtype=torch.int64, device=indptr.device)
+    check(_L().gta_row_ids(_ptr(indptr), indptr.numel() - 1, int(nnz), _ptr(out), _stream(indptr.device)), "row_ids")
+    return out
+
+
 _ATTACHED = {}  # raw stream handle -> id of the Tuning whose values it carries (the executor stays eager on them)
 _TLS = threading.local()  # per thread: {key: (value before the first set, current value)} of knobs set here
 

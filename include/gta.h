@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 11 /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+#define GTA_ABI_VERSION 12 /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
                               hooks; 4: knob sets attached to streams (gta_tuning_*); 5: every UPDATE
                               on hand-written kernels (no vendor library), gta_update_mm_t_splits,
                               the blocked workspace is the slab rows alone and required, bf16
@@ -47,7 +47,8 @@ extern "C" {
                               gta_update_mm_t_splits takes the stream (its attached knob set); 9:
                               gta_update_mlp (two chained node GEMMs in one pass); 10: bf16 y of
                               gta_aggregate_self, bf16 x of gta_update_mlp; 11: gta_gather_add takes the ISA
-                              DIRECTION (dir R / C) and the CSC view of gta_csc_build */
+                              DIRECTION (dir R / C) and the CSC view of gta_csc_build; 12:
+                              gta_build_id, gta_synth_alpha and gta_row_ids (scan-free setup) */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -80,6 +81,10 @@ enum { GTA_SF_NONE = 0, GTA_SF_RELU = 1, GTA_SF_EXP_LEAKY_RELU = 2 /* exp(leaky_
 
 int gta_abi_version(void);
 const char* gta_last_error(void);
+/* ABI 12: the first 16 hex digits of sha256(csrc/gta_kernels.hip || include/gta.h) the library
+ * was compiled from ("unversioned" when built without _build.py).  The Python binding refuses a
+ * library whose id differs from the sources beside it. */
+const char* gta_build_id(void);
 
 /* Tuning hooks (benchmarks and kernel-form tests): named knobs that pick between kernel forms
  * the defaults reach on some shape, or split a launch for per-kernel timing.  They are per calling THREAD -- a knob set on one thread never
@@ -345,6 +350,21 @@ int gta_update_mm_t_split(const void* x, int64_t ldx, const int32_t* row_idx, in
  * count_nonzero per T x 1 block after removing self loops). */
 int gta_tile_nnz(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t n_cols,
                  int64_t T, int32_t* counts, void* stream);
+
+/* ---- synthetic-workload setup (ABI 12) -----------------------------------
+ * Inputs of the bench's metric workload, built with one wave per row and no
+ * dependency between workgroups (no device-wide scan or sort), so shards build the same way
+ * however many processes share a GPU.
+ * gta_synth_alpha: GAT alpha of rows [0, n_rows) of a CSR (indptr local, starting at 0) whose edge
+ * e has generation id gen[e]: out[e, h] = ex[e, h] / (float)s[row, h] with
+ * ex = expf(N(0,1) logit keyed by gen[e] * heads + h) and s = the row's fp64 sum of ex in edge
+ * order -- the per-head softmax over in-edges of GAT ops 6-10 (vTCAD/GraphOP/genGraphOP.py:55-59).
+ * The logit is the counter hash of the Python generator (graph.hash_normal, stream logit_stream).
+ * heads must divide 64.
+ * gta_row_ids: out[e] = the row of edge e (int64 [nnz]). */
+int gta_synth_alpha(const int64_t* indptr, const int64_t* gen, int64_t n_rows, int64_t nnz, int heads, int64_t seed,
+                    int64_t logit_stream, float* out, void* stream);
+int gta_row_ids(const int64_t* indptr, int64_t n_rows, int64_t nnz, int64_t* out, void* stream);
 
 #ifdef __cplusplus
 }

@@ -217,3 +217,53 @@ class SampledChecker:
             assert ratio[j] <= 1.0, (f"op {op.idx} ({op.type}/{op.comp}): |d| {d[j]:.3e} > bound {bound[j]:.3e} "
                                      f"(1e-5 sum|terms| + 1e-6) over {idx.size} {kind}s incl. special rows {listing}")
         return report
+
+
+def gin_unrounded_errors(checker, t32, rows):
+    """The bf16 GIN layer (configs 'gin-products': x, W5, W7 stored in bf16, every sum in fp32)
+    against fp64 evaluated from the UNROUNDED fp32 inputs t32 (workloads.make_tensors with fp32
+    dtypes and the same seed: the values the bf16 configuration rounds), at node rows `rows`.
+    GIN op graph (vTCAD/GraphOP/genGraphOP.py:97-108; SFs of semantics.py):
+        op 2 = sum_{e -> i} x[src(e)] * w_e (w_e = 1, op 1's -1 input)   op 3 = x * (1 + eps)
+        op 4 = op 2 + op 3      op 5 = op 4 . W5     op 6 = relu     op 7 = op 6 . W7     op 8 = relu
+    Returns {op: (max |d| / max |ref|, max |d| / sum|terms|, elements)} for every op the executor
+    holds a value of: the error the bf16 storage choice adds end to end, which the op-local checks
+    (inputs rounded as the kernel rounds them) do not see.  SURVEY.md §8c's bound is rtol 2e-2."""
+    rows = np.asarray(rows, np.int64)
+    ip, ix = checker.ip, checker.ix
+
+    def host(t, idx=None):
+        t2 = t.view(-1, 1) if t.dim() == 1 else t
+        if idx is not None:
+            t2 = t2[torch.as_tensor(idx, device=t2.device, dtype=torch.long)]
+        return t2.double().cpu().numpy()
+
+    x_rows = host(t32["x"], rows)
+    agg = np.zeros_like(x_rows)
+    agg_abs = np.zeros_like(x_rows)
+    w_e = t32["ext:1:1"]
+    for k, r in enumerate(rows):
+        e = np.arange(ip[r], ip[r + 1])
+        if e.size:
+            xs = host(t32["x"], ix[e]) * host(w_e, e)
+            agg[k] = xs.sum(axis=0)
+            agg_abs[k] = np.abs(xs).sum(axis=0)
+    eps1 = float(host(t32["ext:3:1"]).ravel()[0])
+    m3 = x_rows * eps1
+    a4 = agg + m3
+    w5, w7 = host(t32["w:5"]), host(t32["w:7"])
+    z5 = a4 @ w5
+    s6 = np.maximum(z5, 0.0)
+    z7 = s6 @ w7
+    ref = {2: (agg, agg_abs), 3: (m3, np.abs(m3)), 4: (a4, agg_abs + np.abs(m3)),
+           5: (z5, (agg_abs + np.abs(m3)) @ np.abs(w5)), 6: (s6, np.abs(s6)), 7: (z7, np.abs(s6) @ np.abs(w7)),
+           8: (np.maximum(z7, 0.0), np.abs(np.maximum(z7, 0.0)))}
+    out = {}
+    for op, (exp, mag) in ref.items():
+        v = checker.ex.values.get(op)
+        if v is None:
+            continue
+        got = checker.value_at(v, "node", rows)
+        d = np.abs(got - exp)
+        out[op] = (float(d.max() / (np.abs(exp).max() + 1e-30)), float((d / (mag + 1e-30)).max()), int(d.size))
+    return out

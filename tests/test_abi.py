@@ -150,3 +150,71 @@ def test_split_count_reads_the_streams_knob_set(lib):
     finally:
         ops.Tuning.detach(fake_stream)
     assert lib.gta_update_mm_t_splits(M, K, N, 0, fake_stream) == default
+
+
+def test_build_id_ties_the_library_to_its_sources(lib, tmp_path, monkeypatch):
+    """the loaded libgta.so carries the hash of the sources it was built from,
+    and a library whose id differs from the sources beside it is refused."""
+    built = lib.gta_build_id().decode()
+    assert built == _build.source_id() and len(built) == 16
+    _lib.check_build_id(built)  # the matching pair passes
+    # touch a copy of the kernel source: the same library no longer matches
+    src = tmp_path / "gta_kernels.hip"
+    src.write_bytes(open(_build.SRC, "rb").read() + b"\n// touched\n")
+    monkeypatch.setattr(_build, "SRC", str(src))
+    assert _build.source_id() != built
+    with pytest.raises(_lib.GTAError, match="stale libgta.so"):
+        _lib.check_build_id(built)
+    # a library built outside _build.py carries no id and is refused too
+    with pytest.raises(_lib.GTAError):
+        _lib.check_build_id("unversioned")
+
+
+def test_asmcheck_finds_no_in_flight_register_use_in_the_built_library(lib):
+    """every kernel of the shipped code object (inline-asm loads of k_mm_wave /
+    k_mm_ring included) leaves a register alone until the load writing it has been waited for."""
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import asmcheck
+    hazards, n = asmcheck.check_library(_lib.LIB_PATH)
+    assert n > 100, n
+    assert not hazards, hazards[:5]
+
+
+def _fn(lines):
+    """A tiny disassembly in llvm-objdump's format (one kernel at 0x1000)."""
+    out, addr = ["0000000000001000 <k>:"], 0x1000
+    for ln in lines:
+        out.append(f"\t{ln:<58}// {addr:012X}: 00000000")
+        addr += 4
+    return "\n".join(out) + "\n"
+
+
+def test_asmcheck_flags_a_read_before_the_wait():
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import asmcheck
+    ok = _fn(["buffer_load_dwordx4 v[4:7], v1, s[0:3], 0 offen", "buffer_load_dwordx4 v[8:11], v1, s[0:3], 0 offen",
+              "s_waitcnt vmcnt(1)", "v_mov_b32_e32 v20, v5", "s_waitcnt vmcnt(0)", "v_mov_b32_e32 v21, v9",
+              "s_endpgm"])
+    assert asmcheck.check_function("k", asmcheck.parse(ok)["k"]) == []
+    bad = _fn(["buffer_load_dwordx4 v[4:7], v1, s[0:3], 0 offen", "buffer_load_dwordx4 v[8:11], v1, s[0:3], 0 offen",
+               "s_waitcnt vmcnt(1)", "v_mov_b32_e32 v20, v9", "s_endpgm"])
+    hz = asmcheck.check_function("k", asmcheck.parse(bad)["k"])
+    assert len(hz) == 1 and hz[0][4] == ("v9",)
+    # reusing a dead load's register for another value before the wait is a hazard too (the load
+    # lands later and overwrites it): the k_mm_wave remainder case asmcheck caught
+    reuse = _fn(["buffer_load_dwordx4 v[4:7], v1, s[0:3], 0 offen", "v_mov_b32_e32 v6, 0", "s_waitcnt vmcnt(0)",
+                 "s_endpgm"])
+    assert asmcheck.check_function("k", asmcheck.parse(reuse)["k"])[0][4] == ("v6",)
+    # LDS reads count on lgkmcnt; with a scalar load in flight only lgkmcnt(0) retires them
+    lds = _fn(["s_load_dword s4, s[0:1], 0x0", "ds_read_b128 v[4:7], v1", "s_waitcnt lgkmcnt(1)",
+               "v_mov_b32_e32 v20, v4", "s_endpgm"])
+    assert asmcheck.check_function("k", asmcheck.parse(lds)["k"])
+
+
+def test_asmcheck_joins_paths_conservatively():
+    """A load issued on one arm of a branch is still in flight after the join."""
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import asmcheck
+    text = _fn(["s_cbranch_scc0 1", "buffer_load_dword v4, v1, s[0:3], 0 offen", "v_mov_b32_e32 v20, v4",
+                "s_endpgm"])
+    # patch the branch target the way llvm-objdump prints it (<k+0x8> = the v_mov after the load)
+    text = text.replace("// 000000001000: 00000000", "// 000000001000: 00000000 <k+0x8>")
+    hz = asmcheck.check_function("k", asmcheck.parse(text)["k"])
+    assert hz and hz[0][4] == ("v4",)

@@ -39,3 +39,31 @@ def test_config_full_size_sampled_parity(dev, name):
             assert cls in sp, (name, sorted(sp))
         assert any(c.startswith("block_edge_B") for c in sp) or not any(
             isinstance(k, tuple) and k[0] == "blocked" and k[1] > 1 for k in g._plans), (name, sorted(sp))
+
+
+def test_gin_products_bf16_vs_fp64_of_unrounded_inputs(dev):
+    """the bf16 storage choice of gin-products (x, W5 and W7 in bf16; every sum
+    and GEMM accumulation in fp32) measured against fp64 evaluated from the UNROUNDED fp32 inputs,
+    at SURVEY.md §8c's rtol 2e-2, end to end through the layer (ops 2-8 of the GIN op graph,
+    vTCAD/GraphOP/genGraphOP.py:97-108), at the special rows (heaviest, lightest, first, last, ...)
+    plus 256 random rows.  The op-local check above rounds the oracle's inputs as the kernel does,
+    so it cannot see this error."""
+    import numpy as np
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import workloads
+    from oracle.sampled import gin_unrounded_errors
+    results, g = configs.run("gin-products", dev)
+    lay, res, ex = results[0]
+    t32 = workloads.make_tensors(lay.opgraph, g, "GIN", seed=0)  # fp32: what the bf16 config rounded
+    assert ex.tensors["x"].dtype == torch.bfloat16 and t32["x"].dtype == torch.float32
+    assert torch.equal(t32["x"].to(torch.bfloat16), ex.tensors["x"])  # the same values, unrounded
+    ip, ix = g.numpy()
+    chk = SampledChecker(ex, ip, ix)
+    sp = np.concatenate(list(chk.special_rows().values()))
+    rows = np.unique(np.concatenate([sp, np.random.default_rng(3).choice(g.n_rows, 256, replace=False)]))
+    errs = gin_unrounded_errors(chk, t32, rows)
+    print("gin-products bf16 vs fp64 of unrounded fp32 inputs, per op (max|d|/max|ref|, max|d|/sum|terms|, n):",
+          {k: (round(a, 5), round(b, 5), n) for k, (a, b, n) in errs.items()})
+    assert {2, 4, 5, 7, 8} <= set(errs), sorted(errs)
+    for op, (rel, rel_terms, n) in errs.items():
+        assert rel <= 2e-2, f"op {op}: max|d|/max|ref| {rel:.3e} > 2e-2"
+        assert rel_terms <= 2e-2, f"op {op}: max|d|/sum|terms| {rel_terms:.3e} > 2e-2"

@@ -57,3 +57,29 @@ def test_metric_single_pass_full_reddit_vs_oracle(shard):
     torch.cuda.synchronize()
     _check(shard, y, k=128)
 
+
+
+def test_setup_alpha_kernel_bitwise_equals_torch_form(dev):
+    """the bench setup's alpha now comes from libgta's one-wave-per-row
+    gta_synth_alpha (no device-wide scan).  It is bitwise equal to the torch form it replaced
+    (metric.alpha_rows_torch: exp of the hashed logits, fp64 segment_reduce row sums, one divide),
+    on row ranges that start mid-graph and hold the heaviest row, and on a 1-row range; and the
+    scan-free row expansion equals repeat_interleave."""
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import graph as G
+    csr = G.CounterCSR(metric.N_REDDIT, metric.E_REDDIT, metric.SEED)
+    deg = np.diff(csr.indptr_np)
+    heavy = int(np.argmax(deg))
+    for r0, r1 in ((0, 4000), (heavy - 1500, heavy + 1500), (150000, 150001), (metric.N_REDDIT - 3000, metric.N_REDDIT)):
+        lip, src, gen = csr.rows(r0, r1, dev)
+        a = metric.alpha_rows(lip, gen, dev)
+        b = metric.alpha_rows_torch(lip, gen, dev)
+        torch.cuda.synchronize()
+        assert a.shape == b.shape == (gen.numel(), metric.HEADS)
+        assert torch.equal(a, b), f"rows [{r0}, {r1}): {(a != b).sum().item()} elements differ"
+        ri = ops.row_ids(lip, gen.numel())
+        rt = torch.repeat_interleave(torch.arange(r1 - r0, device=dev), lip[1:] - lip[:-1])
+        assert torch.equal(ri, rt)
+    # heads other than 8 (1 and 16 divide 64) follow the same formula
+    lip, src, gen = csr.rows(1000, 1200, dev)
+    for h in (1, 16):
+        assert torch.equal(metric.alpha_rows(lip, gen, dev, heads=h), metric.alpha_rows_torch(lip, gen, dev, heads=h))
