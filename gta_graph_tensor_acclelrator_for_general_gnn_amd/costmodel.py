@@ -239,8 +239,12 @@ def _data_slice(data, tt):
 
 def _edge_sums(cache, data, tt, fl):
     """(sum nnz, sum ceil(nnz/8), sum ceil(nnz*fl/BW)) over the instruction's iterations, cached per
-    (tt, fl): the metric block's three edge instructions share one 106 M-entry pass each."""
+    (tt, fl): the metric block's three edge instructions share one 106 M-entry pass each.  The entry
+    holds `data` itself, so the id in its key cannot be reused by another array while it lives
+    (a freed per-tile-size array's id could otherwise alias the next one's)."""
     key = (id(data), tt)
+    if key in cache and cache[key]["data"] is not data:
+        del cache[key]
     if key not in cache:
         if isinstance(data, TileCounts):
             d = data.values if tt == data.length else _data_slice(data.dense(), tt)  # zeros add nothing
@@ -257,7 +261,8 @@ def _edge_sums(cache, data, tt, fl):
             v, cnt = v[keep], cnt[keep]
         else:  # a negative or huge count (never from a tile list): the element-wise form
             v, cnt = d, np.ones_like(d)
-        cache[key] = {"nnz": int((v * cnt).sum()), "c8": int((((v + 7) // 8) * cnt).sum()), "v": v, "cnt": cnt}
+        cache[key] = {"nnz": int((v * cnt).sum()), "c8": int((((v + 7) // 8) * cnt).sum()), "v": v, "cnt": cnt,
+                      "data": data}
     ent = cache[key]
     if fl not in ent:
         ent[fl] = int((np.ceil((ent["v"] * fl) / BW).astype(np.int64) * ent["cnt"]).sum())

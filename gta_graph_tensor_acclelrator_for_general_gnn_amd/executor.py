@@ -1307,8 +1307,11 @@ class _AutoEntry:
         self.src = None                          # the caller's dict last seen with these tensors
         self.calls, self.run, self.failed = 0, None, False
         self.pool_bytes = 0                      # device memory the capture reserved (its private pool)
+        self.last_use = 0                        # _AUTO_CLOCK value of the latest call (LRU eviction)
+        self.evicted = False                     # its graph was dropped for room: it stays eager from then on
 
 
+_AUTO_CLOCK = [0]
 _AUTO_FAST = {}  # (ids of the call's objects, id of its tensors dict, knob state) -> entry: the per-call lookup
 
 
@@ -1356,7 +1359,9 @@ def _auto_graph(opgraph, stream, graph, tensors, semantics, plan_chunk):
             _AUTO_FAST.clear()
         _AUTO_FAST[fkey] = ent
     ent.calls += 1
-    if ent.failed or ent.calls < 2:
+    _AUTO_CLOCK[0] += 1
+    ent.last_use = _AUTO_CLOCK[0]
+    if ent.failed or ent.evicted or ent.calls < 2:
         return None
     if ent.run is None:
         before = torch.cuda.memory_reserved(graph.device)
@@ -1372,17 +1377,21 @@ def _auto_graph(opgraph, stream, graph, tensors, semantics, plan_chunk):
 
 
 def _evict_pools(keep):
-    """Keep the captured graphs' pools within AUTO_GRAPH_MAX_POOL_BYTES: drop the largest entries
-    other than `keep` (a Reddit / products-sized layer holds GBs of intermediates)."""
+    """Keep the captured graphs' pools within AUTO_GRAPH_MAX_POOL_BYTES (a Reddit / products-sized
+    layer holds GBs of intermediates): drop the graphs of the least recently used entries other than
+    `keep`, and mark those entries to stay eager.  (deleting the largest other entry made
+    two large alternating layers evict each other on every capture and recapture two calls later --
+    repeated captures and warm-ups instead of replays.  An evicted entry keeps its call history, so
+    it is never recaptured.)  pool_bytes is the memory_reserved() growth across the capture: the
+    caching allocator's view, which may under-count a pool that reused freed blocks."""
     total = sum(e.pool_bytes for e in _AUTO.values() if e.run is not None)
     while total > AUTO_GRAPH_MAX_POOL_BYTES:
-        victims = [(e.pool_bytes, i, k) for i, (k, e) in enumerate(_AUTO.items()) if e.run is not None and e is not keep]
+        victims = [(e.last_use, i, e) for i, e in enumerate(_AUTO.values()) if e.run is not None and e is not keep]
         if not victims:
             break
-        b, _, k = max(victims)
-        del _AUTO[k]
-        _AUTO_FAST.clear()
-        total -= b
+        _, _, e = min(victims)
+        total -= e.pool_bytes
+        e.run, e.evicted = None, True
 
 
 def run_stream(opgraph, stream, graph, tensors, semantics=None, plan_chunk=512, sync=True, trace=False):

@@ -129,3 +129,17 @@ def test_starved_gather_c_stream_raises_instead_of_spinning(golden_dir, tiles_fo
     # the per-instruction closed form needs no cycle loop and still answers
     insts = costmodel.per_instruction(blocks, [[128, 1]], 2708, tiles_for)
     assert sum(r["rw_bytes"] for r in insts) == costmodel.model_rw(blocks, 2708, int(sum(tiles_for(128))))
+
+
+def test_edge_sums_cache_cannot_alias_a_freed_array():
+    """_edge_sums keys on id(data); an entry left by an array whose id a new array now
+    carries must not be returned for the new one (the entry holds its array and is checked)."""
+    import numpy as np
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import costmodel
+    cache = {}
+    a = np.array([1, 2, 3, 9], np.int64)
+    b = np.array([5, 5, 5, 5], np.int64)
+    ra = costmodel._edge_sums(cache, a, 4, 16)
+    cache[(id(b), 4)] = cache.pop((id(a), 4))  # what a recycled id would look like
+    rb = costmodel._edge_sums(cache, b, 4, 16)
+    assert ra[0] == 15 and rb[0] == 20

@@ -28,7 +28,7 @@ def _free_port():
     return p
 
 
-def _worker(rank, world, port, golden_dir, q, layout="cols"):
+def _worker(rank, world, port, golden_dir, q, layout="cols", nets=None):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -45,9 +45,13 @@ def _worker(rank, world, port, golden_dir, q, layout="cols"):
         ip, ix = z["indptr"], z["indices"]
         g = G.from_numpy(ip, ix)
         report = []
-        for net, reorder in STREAMS:
-            rec = [s for s in man["streams"] if "file" in s and s["dataset"] == "cora" and s["network"] == net
-                   and s["reorder"] == reorder][0]
+        if nets is None:
+            recs = [[s for s in man["streams"] if "file" in s and s["dataset"] == "cora" and s["network"] == net
+                     and s["reorder"] == reorder][0] for net, reorder in STREAMS]
+        else:  # every golden stream of these networks (the round-5 ORDER-C gathers: all their fusions)
+            recs = [s for s in man["streams"] if "file" in s and s["network"] in nets]
+        for rec in recs:
+            net, reorder = rec["network"], rec["reorder"]
             sem = Semantics.for_network(net, reorder)
             og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
             st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
@@ -98,6 +102,32 @@ def test_layer_streams_distributed_gloo(golden_dir, world, layout):
     assert len(info) == len(STREAMS) and all(b > 0 for _, b in info)
 
 
+GATHER_C_NETS = ("GCNT", "BIDIR", "EDGEC")
+
+
+@pytest.mark.parametrize("world,layout", [(2, "cols"), (4, "cols"), (2, "rows"), (4, "rows-allgather"), (3, "rows-empty")])
+def test_gather_c_streams_distributed_gloo(golden_dir, world, layout):
+    """the ORDER-C gather exchange (distributed.Comm.reduce_cols: a reduce-scatter of the
+    padded [world * m] column table for row shards, the unreduced y[:n_local] slice for column
+    shards) on every reference-lowered gather-C golden stream (GCNT = the transposed GCN aggregate,
+    BIDIR = in + out sums, EDGEC = an SF edge tensor gathered to its source; 22 streams, every
+    fusion partition the reference emitted), world 2 / 3 / 4, both shard layouts; the re-assembled
+    sink outputs equal the single-device fp64 oracle."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, golden_dir, q, layout, GATHER_C_NETS))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    status, info = q.get(timeout=10)
+    assert status == "ok", info
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    assert len(info) == 22 and all(b > 0 for _, b in info), info
+
+
 def test_row_shard_layout_single_process():
     """Row shards: contiguous CSR slices with padded column ids; the padded table gathers back to x."""
     from gta_graph_tensor_acclelrator_for_general_gnn_amd import distributed, graph as G
@@ -136,9 +166,13 @@ def test_row_shards_with_empty_ranks(golden_dir):
     try:
         man = json.load(open(os.path.join(golden_dir, "manifest.json")))
         g = G.from_numpy(np.array([0, 2, 2, 5]), np.array([1, 2, 0, 1, 2], dtype=np.int32))
-        for net, reorder in STREAMS:
-            rec = [s for s in man["streams"] if "file" in s and s["dataset"] == "cora" and s["network"] == net
-                   and s["reorder"] == reorder][0]
+        if nets is None:
+            recs = [[s for s in man["streams"] if "file" in s and s["dataset"] == "cora" and s["network"] == net
+                     and s["reorder"] == reorder][0] for net, reorder in STREAMS]
+        else:  # every golden stream of these networks (the round-5 ORDER-C gathers: all their fusions)
+            recs = [s for s in man["streams"] if "file" in s and s["network"] in nets]
+        for rec in recs:
+            net, reorder = rec["network"], rec["reorder"]
             sem = Semantics.for_network(net, reorder)
             og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
             st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))

@@ -418,3 +418,25 @@ def test_trace_carries_the_per_instruction_model(golden_dir, manifest, monkeypat
     model_ev = [e for e in full.trace if e["pid"] == "GTA model"]
     assert len(model_ev) == sum(1 for r in full.model_insts if r["starts"] > 0)
     assert max(e["ts"] + e["dur"] for e in model_ev) * 1e3 <= full.model_cycles + 1
+
+
+def test_graph_pool_eviction_is_lru_and_never_recaptures(monkeypatch):
+    """past AUTO_GRAPH_MAX_POOL_BYTES the least recently used captured graphs are dropped
+    (not the largest other one), and a dropped entry stays eager instead of being recaptured two
+    calls later (two big alternating layers used to evict each other on every capture)."""
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import executor as X
+    monkeypatch.setattr(X, "_AUTO", {})
+    monkeypatch.setattr(X, "AUTO_GRAPH_MAX_POOL_BYTES", 100)
+    ents = []
+    for k, (b, use) in enumerate([(60, 3), (50, 1), (30, 2)]):
+        e = X._AutoEntry((), {})
+        e.run, e.pool_bytes, e.last_use, e.calls = object(), b, use, 2
+        X._AUTO[k] = e
+        ents.append(e)
+    X._evict_pools(keep=ents[2])  # 140 > 100: drop the LRU entry other than the new one (not the largest)
+    assert ents[1].run is None and ents[1].evicted and 1 in X._AUTO
+    assert ents[0].run is not None and ents[2].run is not None  # 90 <= 100: done
+    X._AUTO[3] = e = X._AutoEntry((), {})
+    e.run, e.pool_bytes, e.last_use = object(), 40, 4
+    X._evict_pools(keep=e)  # 130: the least recently used live graph now is entry 2
+    assert ents[2].evicted and ents[0].run is not None and e.run is not None
