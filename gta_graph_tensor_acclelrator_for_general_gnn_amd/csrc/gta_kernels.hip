@@ -943,6 +943,221 @@ k_agg_h32(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_ite
   }
 }
 
+// Round 6: the metric kernel with its two streamed inputs -- alpha (32 B per edge) and the source
+// indices (4 B) -- pre-fetched into L2 by SCALAR loads (knob seg_pf; k_agg_h32<A1> otherwise).
+// Why: counters of k_agg_h32 (profiles/r05/wcost_pmc_summary.json) put the kernel's limit in the
+// vector L1's outstanding-request capacity: ~90 line requests in flight per CU, so throughput =
+// capacity / mean latency.  The alpha lines are all HBM misses (~1,800 cycles each against ~360
+// for the gathered rows, 70 % L2 hits) and hold a third of that capacity: without alpha the
+// same loop runs in 0.68 of the time.  A vector prefetch cannot help -- loads return in order, so
+// waiting for a step's rows waits for any earlier prefetch too -- but a scalar load is counted on
+// lgkmcnt and travels the scalar cache: issued PD steps ahead it brings the alpha lines (and the
+// next chunk's index line) into L2, and the vector loads then hit.  For that the loop keeps no LDS
+// operation in flight (lgkmcnt would otherwise mix the two): the index of edge u reaches the
+// half-wave by a DPP row broadcast (row_newbcast) from a register in which lanes j and j + 16 hold
+// the same index, instead of ds_swizzle.  The prefetched values are never used; each is kept live
+// until an explicit s_waitcnt lgkmcnt(0) one step later, so no register is reused while its load
+// is in flight (asmcheck.py checks the built code).  s_buffer_load through a descriptor bounded
+// by the tensor: a prefetch past the end reads nothing.  PFB = prefetch granule (64 or 128 B).
+// Same per-lane edge order and fma chain as k_agg_h32: bitwise equal to it.
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ i32x4_t buf_desc(const void* p, uint32_t bytes) {  // raw buffer: stride 0, bounds = bytes
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  return i32x4_t{static_cast<int>(a & 0xffffffffu), static_cast<int>((a >> 32) & 0xffffu), static_cast<int>(bytes),
+                 0x00020000};
+}
+template <int K>
+__device__ __forceinline__ int row_bcast(int v) {  // lane K of each 16-lane row (gfx90a+ DPP row_newbcast)
+  return __builtin_amdgcn_update_dpp(0, v, 0x150 + K, 0xF, 0xF, false);
+}
+
+template <int K>
+__device__ __forceinline__ int idx_bcast(int lo, int hi) {  // index K (< 32) of the chunk to the half-wave
+  return K < 16 ? row_bcast<K % 16>(lo) : row_bcast<K % 16>(hi);
+}
+
+__device__ __forceinline__ void spf(int& d, const i32x4_t& rs, uint32_t off) {  // scalar L2 prefetch of one granule
+  asm volatile("s_buffer_load_dword %0, %1, %2" : "=s"(d) : "s"(rs), "s"(off) : "memory");
+}
+
+template <int NT, int PFB, int PD>
+__global__ void __launch_bounds__(kBlock)
+k_agg_h32pf(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
+            uint32_t row_bytes, const float* __restrict__ w, int64_t ldw, float* __restrict__ slabs,
+            const SegItem* __restrict__ items, uint32_t w_bytes, uint32_t i_bytes) {
+  constexpr int G = 32, F = 128, U = 8;
+  constexpr int NPA = 256 / PFB;  // granules of one item's alpha per step (8 edges x 32 B)
+  const int lane = threadIdx.x & (kWave - 1);
+  const int l32 = lane & (G - 1);
+  const int64_t k = (static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform()) * 2 + (lane >> 5);
+  const int64_t n_items = *n_items_p;
+  SegItem it{0, 0, 0};
+  if (k < n_items) it = items[k];
+  const int len = it.len;
+  const int other = __shfl_xor(len, 32);
+  const int maxlen = __builtin_amdgcn_readfirstlane(max(len, other));
+  const int minlen = __builtin_amdgcn_readfirstlane(min(len, other));
+  if (maxlen == 0) return;
+  // the two items as scalars (A: lanes 0-31, B: lanes 32-63); edge ids < 2^27 (host: nnz * 32 < 2^32)
+  const uint32_t begA = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(it.beg), 0));
+  const uint32_t begB = static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(it.beg), 32));
+  const int lenA = __builtin_amdgcn_readlane(len, 0), lenB = __builtin_amdgcn_readlane(len, 32);
+  const uint32_t wrow = static_cast<uint32_t>(ldw) * 4u;
+  const i32x4_t rsw = buf_desc(w, w_bytes), rsi = buf_desc(indices, i_bytes);
+  const uint32_t colb = static_cast<uint32_t>(l32) * 16u;
+  const char* xb = reinterpret_cast<const char*>(x);
+  const int h = l32 >> 2, q = l32 & 3;
+  const int32_t* ic = indices + it.beg;
+  const char* wbase = reinterpret_cast<const char*>(w);
+  uint32_t woff = static_cast<uint32_t>((it.beg * ldw + h) * 4);
+  auto wat = [&](uint32_t off) { return *reinterpret_cast<const float*>(wbase + off); };
+  float acc[4] = {0.f, 0.f, 0.f, 0.f};
+  auto ldi = [&](const int32_t* p) { return (NT & 1) ? __builtin_nontemporal_load(p) : *p; };
+  auto row = [&](int src) -> float4 {
+    return *reinterpret_cast<const float4*>(xb + (__umul24(static_cast<uint32_t>(src), row_bytes) + colb));
+  };
+  // prefetch bookkeeping: the granules issued at the previous step, kept live until the next wait
+  int pfa[2 * NPA], pfi[4];
+#pragma unroll
+  for (int j = 0; j < 2 * NPA; ++j) pfa[j] = 0;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) pfi[j] = 0;
+  auto retire = [&]() __attribute__((always_inline)) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < 2 * NPA; ++j) asm volatile("" ::"s"(pfa[j]));
+#pragma unroll
+    for (int j = 0; j < 4; ++j) asm volatile("" ::"s"(pfi[j]));
+  };
+  // alpha of step t (edges 8t .. 8t + 7 of each item) into L2
+  auto pf_alpha = [&](int t) __attribute__((always_inline)) {
+    const int e = 8 * t;
+    if (e < lenA) {
+      const uint32_t o = ((begA + static_cast<uint32_t>(e)) * wrow) & ~static_cast<uint32_t>(PFB - 1);
+#pragma unroll
+      for (int j = 0; j < NPA; ++j) spf(pfa[j], rsw, o + j * PFB);
+    }
+    if (e < lenB) {
+      const uint32_t o = ((begB + static_cast<uint32_t>(e)) * wrow) & ~static_cast<uint32_t>(PFB - 1);
+#pragma unroll
+      for (int j = 0; j < NPA; ++j) spf(pfa[NPA + j], rsw, o + j * PFB);
+    }
+  };
+  // the 128 B of indices of chunk c (32 edges) into L2
+  auto pf_idx = [&](int c) __attribute__((always_inline)) {
+    if (c < lenA) {
+      const uint32_t o = ((begA + static_cast<uint32_t>(c)) * 4u) & ~63u;
+      spf(pfi[0], rsi, o);
+      spf(pfi[1], rsi, o + 64);
+    }
+    if (c < lenB) {
+      const uint32_t o = ((begB + static_cast<uint32_t>(c)) * 4u) & ~63u;
+      spf(pfi[2], rsi, o);
+      spf(pfi[3], rsi, o + 64);
+    }
+  };
+#pragma unroll
+  for (int t = 1; t <= PD; ++t) pf_alpha(t);
+  pf_idx(G);
+  // lanes j and j + 16 of a half hold the same index: lo = index j % 16, hi = index 16 + j % 16
+  const int jl = l32 & 15;
+  int ilo = (jl < len) ? ldi(ic + jl) : 0;
+  int ihi = (16 + jl < len) ? ldi(ic + 16 + jl) : 0;
+  for (int c = 0; c < maxlen; c += G) {
+    // opaque to loop strength reduction: otherwise each of the 32 (step, edge) weight offsets of a
+    // chunk became its own induction register (95 VGPRs)
+    asm volatile("" : "+v"(woff));
+    const int ilon = (c + G + jl < len) ? ldi(ic + G + jl) : 0;
+    const int ihin = (c + G + 16 + jl < len) ? ldi(ic + G + 16 + jl) : 0;
+#pragma unroll
+    for (int s = 0; s < G; s += U) {
+      if (c + s >= maxlen) break;
+      // the previous step's prefetches have landed; issue the step PD ahead (and at a chunk's
+      // first step, the indices of the chunk after the next)
+      retire();
+      pf_alpha((c + s) / U + PD + 1);
+      if (s == 0) pf_idx(c + 2 * G);
+      // keep each step's index broadcasts in the step: hoisted to the chunk start they held 32
+      // more VGPRs (95: 5 waves per SIMD instead of 8)
+      __builtin_amdgcn_sched_barrier(0);
+      float4 xv[U];
+      float wu[U];
+      if (c + s + U <= minlen) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          int src;
+          switch (s + u) {
+#define GTA_IB(K_) case K_: src = idx_bcast<K_>(ilo, ihi); break;
+            GTA_IB(0) GTA_IB(1) GTA_IB(2) GTA_IB(3) GTA_IB(4) GTA_IB(5) GTA_IB(6) GTA_IB(7)
+            GTA_IB(8) GTA_IB(9) GTA_IB(10) GTA_IB(11) GTA_IB(12) GTA_IB(13) GTA_IB(14) GTA_IB(15)
+            GTA_IB(16) GTA_IB(17) GTA_IB(18) GTA_IB(19) GTA_IB(20) GTA_IB(21) GTA_IB(22) GTA_IB(23)
+            GTA_IB(24) GTA_IB(25) GTA_IB(26) GTA_IB(27) GTA_IB(28) GTA_IB(29) GTA_IB(30) GTA_IB(31)
+#undef GTA_IB
+            default: src = 0;
+          }
+          xv[u] = row(src);
+        }
+        const float2 pr = *reinterpret_cast<const float2*>(
+            wbase + (woff + static_cast<uint32_t>((h & 1) + s + 2 * q) * wrow + static_cast<uint32_t>(2 * (h >> 1) - h) * 4u));
+        const bool odd = h & 1;
+        const float own = odd ? pr.y : pr.x, oth = xmask4(odd ? pr.x : pr.y, odd);
+        float a[4], b[4];
+        a[0] = quad_bcast<0>(own); b[0] = quad_bcast<0>(oth);
+        a[1] = quad_bcast<1>(own); b[1] = quad_bcast<1>(oth);
+        a[2] = quad_bcast<2>(own); b[2] = quad_bcast<2>(oth);
+        a[3] = quad_bcast<3>(own); b[3] = quad_bcast<3>(oth);
+#pragma unroll
+        for (int k2 = 0; k2 < 4; ++k2) {
+          wu[2 * k2] = odd ? b[k2] : a[k2];
+          wu[2 * k2 + 1] = odd ? a[k2] : b[k2];
+        }
+      } else {
+        const int rem = len - c - s;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          int src;
+          switch (s + u) {
+#define GTA_IB(K_) case K_: src = idx_bcast<K_>(ilo, ihi); break;
+            GTA_IB(0) GTA_IB(1) GTA_IB(2) GTA_IB(3) GTA_IB(4) GTA_IB(5) GTA_IB(6) GTA_IB(7)
+            GTA_IB(8) GTA_IB(9) GTA_IB(10) GTA_IB(11) GTA_IB(12) GTA_IB(13) GTA_IB(14) GTA_IB(15)
+            GTA_IB(16) GTA_IB(17) GTA_IB(18) GTA_IB(19) GTA_IB(20) GTA_IB(21) GTA_IB(22) GTA_IB(23)
+            GTA_IB(24) GTA_IB(25) GTA_IB(26) GTA_IB(27) GTA_IB(28) GTA_IB(29) GTA_IB(30) GTA_IB(31)
+#undef GTA_IB
+            default: src = 0;
+          }
+          if (u < rem) {
+            xv[u] = row(src);
+            wu[u] = wat(woff + static_cast<uint32_t>(s + u) * wrow);
+          } else {
+            xv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            wu[u] = 0.f;
+          }
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc[0] = fmaf(wu[u], xv[u].x, acc[0]);
+        acc[1] = fmaf(wu[u], xv[u].y, acc[1]);
+        acc[2] = fmaf(wu[u], xv[u].z, acc[2]);
+        acc[3] = fmaf(wu[u], xv[u].w, acc[3]);
+      }
+    }
+    ilo = ilon;
+    ihi = ihin;
+    ic += G;
+    woff += static_cast<uint32_t>(G) * wrow;
+  }
+  retire();  // no scalar load in flight when the wave ends
+  if (len > 0) {
+    float* o = slabs + k * F + l32 * 4;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if (NT & 2) __builtin_nontemporal_store(acc[t], o + t);
+      else o[t] = acc[t];
+    }
+  }
+}
+
 // Lean half-wave form of the fused GAT attention item (k_agg_seg4<4, 8, ATT, SFC = exp-leaky-
 // relu, G = 32>) for F = 128, 8 heads: the weighted k_agg_h32 loop with the edge weight computed,
 // v = exp(leaky_relu(a[row, h] + b[src, h])), instead of loaded.  Per full 8-edge step lane
@@ -2663,12 +2878,6 @@ k_mm_ring(const float* __restrict__ x, int64_t ldx, const int32_t* __restrict__ 
 // exposed per 1.7 us stage.  The K tail is one more stage whose lanes past K are zeroed (loads past
 // the tensor read 0 through the buffer bounds); stages past the last re-read it.  Same
 // per-accumulator k order and fma chain as k_mm_rows / k_mm_ring: bitwise equal to them.
-typedef int i32x4_t __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ i32x4_t buf_desc(const void* p, uint32_t bytes) {  // raw buffer: stride 0, bounds = bytes
-  const uint64_t a = reinterpret_cast<uint64_t>(p);
-  return i32x4_t{static_cast<int>(a & 0xffffffffu), static_cast<int>((a >> 32) & 0xffffu), static_cast<int>(bytes),
-                 0x00020000};
-}
 __device__ __forceinline__ void buf_load16(f32x4& v, uint32_t voff, const i32x4_t& rs, int soff) {
   asm volatile("buffer_load_dwordx4 %0, %1, %2, %3 offen" : "=v"(v) : "v"(voff), "s"(rs), "s"(soff) : "memory");
 }
@@ -3520,6 +3729,8 @@ struct Tuning {
   int agg_lean = 1;        // k_agg_lean for F = 64*VW SpMM shapes (0: k_aggregate, the form of other shapes)
   int seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
   int seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
+  int seg_pf = 0;          // k_agg_h32pf: alpha / index lines pre-fetched into L2 by scalar loads (1: 64-B granules,
+                           // 1 step ahead; 2: 128 B, 1 step; 3: 64 B, 2 steps; 4: 128 B, 2 steps; 0: off)
   int seg_alpha1 = 1;      // k_agg_h32 with 8 heads: one 8-B weight load per lane and step (A1) instead of two 4-B
   int agg_bf16_vw8 = 4;    // k_aggregate over bf16 rows in 16-B pieces (VW = 8) instead of 8-B pieces:
                            // 0 off, 4 / 8 = row loads in flight per lane and step (1 = 4)
@@ -3585,6 +3796,7 @@ const Knob* find_knob(const char* key) {
       {"seg_lean", &Tuning::seg_lean, nullptr},
       {"seg_lean_w1", &Tuning::seg_lean_w1, nullptr},
       {"seg_alpha1", &Tuning::seg_alpha1, nullptr},
+      {"seg_pf", &Tuning::seg_pf, nullptr},
       {"agg_bf16_vw8", &Tuning::agg_bf16_vw8, nullptr},
       {"agg_w1", &Tuning::agg_w1, nullptr},
       {"seg_phase", &Tuning::seg_phase, nullptr},
@@ -3967,8 +4179,14 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
     if (lean) {
       const bool a1 = w && heads == 8 && ldw % 2 == 0 && aligned(w, 8) && tuning().seg_alpha1 &&
                       static_cast<uint64_t>(nnz) * static_cast<uint64_t>(ldw) * 4u < (1ull << 32);
+      const int pf = tuning().seg_pf;
+      const uint32_t wbytes = static_cast<uint32_t>(nnz * ldw * 4), ibytes = static_cast<uint32_t>(nnz * 4);
       if (w && heads == 1) k_agg_h32<true, 2, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-      else if (a1) k_agg_h32<true, 3, false, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
+      else if (a1 && ldw == 8 && pf >= 1 && pf <= 4) {
+#define GTA_PF(PFB_, PD_) k_agg_h32pf<3, PFB_, PD_><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its, wbytes, ibytes)
+        if (pf == 1) GTA_PF(64, 0); else if (pf == 2) GTA_PF(128, 0); else if (pf == 3) GTA_PF(64, 1); else GTA_PF(128, 1);
+#undef GTA_PF
+      } else if (a1) k_agg_h32<true, 3, false, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
       else if (w) k_agg_h32<true, 3><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
       else k_agg_h32<false, 2><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
       GTA_LAUNCHED("k_agg_h32");

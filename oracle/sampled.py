@@ -255,9 +255,10 @@ def gin_unrounded_errors(checker, t32, rows):
     z5 = a4 @ w5
     s6 = np.maximum(z5, 0.0)
     z7 = s6 @ w7
+    # an SF's error is its input's (relu passes it or drops it): its terms are the GEMM's before it
+    m5, m7 = (agg_abs + np.abs(m3)) @ np.abs(w5), np.abs(s6) @ np.abs(w7)
     ref = {2: (agg, agg_abs), 3: (m3, np.abs(m3)), 4: (a4, agg_abs + np.abs(m3)),
-           5: (z5, (agg_abs + np.abs(m3)) @ np.abs(w5)), 6: (s6, np.abs(s6)), 7: (z7, np.abs(s6) @ np.abs(w7)),
-           8: (np.maximum(z7, 0.0), np.abs(np.maximum(z7, 0.0)))}
+           5: (z5, m5), 6: (s6, m5), 7: (z7, m7), 8: (np.maximum(z7, 0.0), m7)}
     out = {}
     for op, (exp, mag) in ref.items():
         v = checker.ex.values.get(op)

@@ -1443,3 +1443,29 @@ def test_aggregate_line_pitched_table(dev, weighted, form):
         res.append(ops.aggregate(g, t, "src", wd, plan=64, **kw))
     torch.cuda.synchronize()
     assert torch.equal(res[0], res[1])
+
+
+@pytest.mark.parametrize("pf", [1, 2, 3, 4])
+@pytest.mark.parametrize("n,e,blocks", [(900, 30000, 8), (3000, 600000, 2), (5, 2000, 1)])
+def test_aggregate_blocked_scalar_prefetch_bitwise(dev, pf, n, e, blocks):
+    """k_agg_h32pf (round 6, knob seg_pf: alpha / index lines pre-fetched into L2 by scalar loads,
+    indices broadcast by DPP row_newbcast instead of ds_swizzle) == k_agg_h32's 8-head form bitwise,
+    on short items, multi-chunk items (several prefetch steps and index chunks) and 256-edge items
+    of a few very heavy rows; and == the fp64 oracle."""
+    g = G.synthetic(n, e, seed=n + pf, device=dev)
+    ip, ix = g.numpy()
+    rng = np.random.default_rng(n)
+    x = torch.from_numpy(rng.standard_normal((n, 128)).astype(np.float32)).to(dev)
+    w = torch.from_numpy(rng.random((g.nnz, 8)).astype(np.float32)).to(dev)
+    old = ops.get_debug("seg_pf")
+    try:
+        ops.set_debug("seg_pf", 0)
+        y0 = ops.aggregate_blocked(g, x, w, blocks=blocks)
+        ops.set_debug("seg_pf", pf)
+        y = ops.aggregate_blocked(g, x, w, blocks=blocks)
+    finally:
+        ops.set_debug("seg_pf", old)
+    torch.cuda.synchronize()
+    xn, wn = x.cpu().numpy(), w.cpu().numpy()
+    _check(y, isa_ref.aggregate(ip, ix, xn, "src", wn), isa_ref.aggregate_abs(ip, ix, xn, "src", wn), f"seg_pf={pf}")
+    assert torch.equal(y, y0)
