@@ -607,7 +607,7 @@ class Executor:
             return None
         B = self.attention_blocks or ops.BlockedPlan.auto_blocks(self.graph, F)
         # the lean fused kernel (F = 128, 8 heads) beats softmax + aggregate even unblocked (B = 1:
-        # Flickr 102 vs 168 us, scripts/att_small_probe.py); other shapes need a blocked table
+        # Flickr 102 vs 168 us; the round-4 probe, profiles/r04/layer_bench_*.log); other shapes need a blocked table
         lean = F == 128 and H == 8
         if B < (1 if (self.attention_blocks or lean) else 4) or not ops.blocked_ready(self.graph, B):
             return None

@@ -66,7 +66,7 @@ def line_pitch(F, elem_size, max_extra=0.5):
     whole 128-B lines when that lowers the mean number of lines a gathered row touches, at most
     max_extra more bytes; F otherwise.  GIN products' bf16 model input: 200-B rows touch 2.5 lines
     at a 200-B pitch and 2 at 256 B, and the layer's aggregate runs 5.38 -> 4.66 ms
-    (scripts/gin_ld_ab.py, bitwise the same sums).  fp32 rows of 128 floats are whole lines already."""
+    (profiles/r05/gin_ld_ab_*.log, bitwise the same sums).  fp32 rows of 128 floats are whole lines already."""
     row = int(F) * int(elem_size)
     if row == 0:
         return F

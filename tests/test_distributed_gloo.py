@@ -166,13 +166,9 @@ def test_row_shards_with_empty_ranks(golden_dir):
     try:
         man = json.load(open(os.path.join(golden_dir, "manifest.json")))
         g = G.from_numpy(np.array([0, 2, 2, 5]), np.array([1, 2, 0, 1, 2], dtype=np.int32))
-        if nets is None:
-            recs = [[s for s in man["streams"] if "file" in s and s["dataset"] == "cora" and s["network"] == net
-                     and s["reorder"] == reorder][0] for net, reorder in STREAMS]
-        else:  # every golden stream of these networks (the round-5 ORDER-C gathers: all their fusions)
-            recs = [s for s in man["streams"] if "file" in s and s["network"] in nets]
-        for rec in recs:
-            net, reorder = rec["network"], rec["reorder"]
+        for net, reorder in STREAMS:
+            rec = [s for s in man["streams"] if "file" in s and s["dataset"] == "cora" and s["network"] == net
+                   and s["reorder"] == reorder][0]
             sem = Semantics.for_network(net, reorder)
             og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
             st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
