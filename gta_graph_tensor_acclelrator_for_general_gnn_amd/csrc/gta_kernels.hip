@@ -980,8 +980,8 @@ __device__ __forceinline__ void spf(int& d, const i32x4_t& rs, uint32_t off) {  
   asm volatile("s_buffer_load_dword %0, %1, %2" : "=s"(d) : "s"(rs), "s"(off) : "memory");
 }
 
-template <int NT, int PFB, int PD>
-__global__ void __launch_bounds__(kBlock)
+template <int NT, int PFB, int PD, int MINW = 1>
+__global__ void __launch_bounds__(kBlock, MINW)
 k_agg_h32pf(const int32_t* __restrict__ indices, const int64_t* __restrict__ n_items_p, const float* __restrict__ x,
             uint32_t row_bytes, const float* __restrict__ w, int64_t ldw, float* __restrict__ slabs,
             const SegItem* __restrict__ items, uint32_t w_bytes, uint32_t i_bytes) {
@@ -3730,7 +3730,8 @@ struct Tuning {
   int seg_lean = 1;        // k_agg_h32 (32-bit row offsets, unmasked full steps, DPP weights) for F = 128
   int seg_lean_w1 = 1;     // k_agg_h32 with one weight per edge (H = 1: GCN, GraphSAGE-mean) for F = 128
   int seg_pf = 0;          // k_agg_h32pf: alpha / index lines pre-fetched into L2 by scalar loads (1: 64-B granules,
-                           // 1 step ahead; 2: 128 B, 1 step; 3: 64 B, 2 steps; 4: 128 B, 2 steps; 0: off)
+                           // 1 step ahead; 2: 128 B, 1 step; 3: 64 B, 2 steps; 4: 128 B, 2 steps; 5: as 1, held to
+                           // 8 waves per SIMD; 0: off)
   int seg_alpha1 = 1;      // k_agg_h32 with 8 heads: one 8-B weight load per lane and step (A1) instead of two 4-B
   int agg_bf16_vw8 = 4;    // k_aggregate over bf16 rows in 16-B pieces (VW = 8) instead of 8-B pieces:
                            // 0 off, 4 / 8 = row loads in flight per lane and step (1 = 4)
@@ -4182,9 +4183,10 @@ int gta_aggregate_blocked(const int64_t* indptr, const int32_t* indices, int64_t
       const int pf = tuning().seg_pf;
       const uint32_t wbytes = static_cast<uint32_t>(nnz * ldw * 4), ibytes = static_cast<uint32_t>(nnz * 4);
       if (w && heads == 1) k_agg_h32<true, 2, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
-      else if (a1 && ldw == 8 && pf >= 1 && pf <= 4) {
+      else if (a1 && ldw == 8 && pf >= 1 && pf <= 5) {
 #define GTA_PF(PFB_, PD_) k_agg_h32pf<3, PFB_, PD_><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its, wbytes, ibytes)
-        if (pf == 1) GTA_PF(64, 0); else if (pf == 2) GTA_PF(128, 0); else if (pf == 3) GTA_PF(64, 1); else GTA_PF(128, 1);
+        if (pf == 1) GTA_PF(64, 0); else if (pf == 2) GTA_PF(128, 0); else if (pf == 3) GTA_PF(64, 1); else if (pf == 4) GTA_PF(128, 1);
+        else k_agg_h32pf<3, 64, 0, 8><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its, wbytes, ibytes);
 #undef GTA_PF
       } else if (a1) k_agg_h32<true, 3, false, true><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);
       else if (w) k_agg_h32<true, 3><<<g2h, blk2, 0, s>>>(indices, nit, x, rb, w, ldw, slabs, its);

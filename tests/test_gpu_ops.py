@@ -1445,7 +1445,7 @@ def test_aggregate_line_pitched_table(dev, weighted, form):
     assert torch.equal(res[0], res[1])
 
 
-@pytest.mark.parametrize("pf", [1, 2, 3, 4])
+@pytest.mark.parametrize("pf", [1, 2, 3, 4, 5])
 @pytest.mark.parametrize("n,e,blocks", [(900, 30000, 8), (3000, 600000, 2), (5, 2000, 1)])
 def test_aggregate_blocked_scalar_prefetch_bitwise(dev, pf, n, e, blocks):
     """k_agg_h32pf (round 6, knob seg_pf: alpha / index lines pre-fetched into L2 by scalar loads,
