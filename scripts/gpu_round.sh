@@ -33,7 +33,9 @@ for s in $STEPS; do
       rc=$?; echo "pmc write rc=$rc"; stop_if_fatal $rc pmc ;;
     bench2)
       for m in ${BENCH2_MODES:-edges rows}; do
-        GTA_DIST_BACKEND=gloo GTA_SINGLE_DEVICE=1 timeout -k 10 ${T_BENCH:-600} python -m torch.distributed.run \
+        # several ranks on ONE GPU starve each other for tens of seconds on this pool unless completion
+        # signals are polled: rehearsals only; the N-GPU runs keep the default
+        HSA_ENABLE_INTERRUPT=0 GTA_DIST_BACKEND=gloo GTA_SINGLE_DEVICE=1 timeout -k 10 ${T_BENCH:-600} python -m torch.distributed.run \
           --nnodes=1 --nproc-per-node ${BENCH2_RANKS:-2} --master-addr 127.0.0.1 --master-port 29511 bench.py \
           --gpus ${BENCH2_RANKS:-2} --steps 3 --warmup 1 --mode $m ${BENCH2_ARGS} > gpurun_out/bench2_$m.log 2>&1
         rc=$?; echo "bench2 $m rc=$rc"; grep '^{' gpurun_out/bench2_$m.log | tail -1; stop_if_fatal $rc bench2
