@@ -207,6 +207,11 @@ def test_asmcheck_flags_a_read_before_the_wait():
     lds = _fn(["s_load_dword s4, s[0:1], 0x0", "ds_read_b128 v[4:7], v1", "s_waitcnt lgkmcnt(1)",
                "v_mov_b32_e32 v20, v4", "s_endpgm"])
     assert asmcheck.check_function("k", asmcheck.parse(lds)["k"])
+    # a scalar (prefetch) load's SGPR is in flight until lgkmcnt(0): k_agg_h32pf's pattern
+    smem = _fn(["s_buffer_load_dword s5, s[8:11], s12", "s_mov_b32 s5, 0", "s_waitcnt lgkmcnt(0)", "s_endpgm"])
+    assert asmcheck.check_function("k", asmcheck.parse(smem)["k"])[0][4] == ("s5",)
+    smem_ok = _fn(["s_buffer_load_dword s5, s[8:11], s12", "s_waitcnt lgkmcnt(0)", "s_mov_b32 s5, 0", "s_endpgm"])
+    assert asmcheck.check_function("k", asmcheck.parse(smem_ok)["k"]) == []
 
 
 def test_asmcheck_joins_paths_conservatively():
