@@ -223,3 +223,42 @@ def test_asmcheck_joins_paths_conservatively():
     text = text.replace("// 000000001000: 00000000", "// 000000001000: 00000000 <k+0x8>")
     hz = asmcheck.check_function("k", asmcheck.parse(text)["k"])
     assert hz and hz[0][4] == ("v4",)
+
+
+_HZ_KERNEL = r'''
+#include <hip/hip_runtime.h>
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+__device__ inline i32x4_t desc(const void* p) {
+  const unsigned long long a = reinterpret_cast<unsigned long long>(p);
+  return i32x4_t{static_cast<int>(a), static_cast<int>((a >> 32) & 0xffff), 1 << 20, 0x00020000};
+}
+extern "C" __global__ void k(const float* x, float* out) {
+  f32x4 v;
+  const i32x4_t rs = desc(x);
+  unsigned off = threadIdx.x * 16u;
+  asm volatile("buffer_load_dwordx4 %0, %1, %2, 0 offen" : "=v"(v) : "v"(off), "s"(rs) : "memory");
+#ifdef USE_BEFORE_WAIT
+  out[threadIdx.x + 64] = v[0] * 2.f;
+#endif
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  out[threadIdx.x] = v[1] + v[2];
+}
+'''
+
+
+def test_asmcheck_catches_a_real_compiler_hazard(tmp_path):
+    """The check on hipcc's own output, not a hand-written listing: an inline-asm load whose value
+    the code reads before its counted wait is flagged; the same kernel without that read passes."""
+    import subprocess
+    from gta_graph_tensor_acclelrator_for_general_gnn_amd import asmcheck
+    src = tmp_path / "hz.hip"
+    src.write_text(_HZ_KERNEL)
+    found = {}
+    for name, flags in (("ok", []), ("bad", ["-DUSE_BEFORE_WAIT"])):
+        so = tmp_path / f"{name}.so"
+        subprocess.run([_build.hipcc(), f"--offload-arch={_build.ARCH}", "-O3", "-fPIC", "-shared", *flags, "-o", str(so),
+                        str(src)], check=True, capture_output=True)
+        found[name] = asmcheck.check_library(str(so))[0]
+    assert found["ok"] == []
+    assert found["bad"] and found["bad"][0][0] == "k"
