@@ -79,7 +79,14 @@ def test_setup_alpha_kernel_bitwise_equals_torch_form(dev):
         ri = ops.row_ids(lip, gen.numel())
         rt = torch.repeat_interleave(torch.arange(r1 - r0, device=dev), lip[1:] - lip[:-1])
         assert torch.equal(ri, rt)
-    # heads other than 8 (1 and 16 divide 64) follow the same formula
+    # every head count that divides 64 follows the same formula
     lip, src, gen = csr.rows(1000, 1200, dev)
-    for h in (1, 16):
+    for h in (1, 2, 4, 16, 32, 64):
         assert torch.equal(metric.alpha_rows(lip, gen, dev, heads=h), metric.alpha_rows_torch(lip, gen, dev, heads=h))
+    # empty rows (no edges: nothing written), a one-edge row (alpha = 1), arbitrary generation ids
+    lip = torch.tensor([0, 0, 3, 3, 4, 4, 9], dtype=torch.int64, device=dev)
+    gen = torch.tensor([7, 123456789, 5, 99, 0, 1, 2, 3, 10 ** 9], dtype=torch.int64, device=dev)
+    a, b = metric.alpha_rows(lip, gen, dev), metric.alpha_rows_torch(lip, gen, dev)
+    assert torch.equal(a, b) and torch.all(a[3] == 1.0)
+    with pytest.raises(ops._lib.GTAError):
+        ops.synth_alpha(lip, gen, 3, 0, metric.STREAM_LOGIT)  # 3 does not divide 64
