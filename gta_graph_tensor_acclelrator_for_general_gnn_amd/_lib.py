@@ -10,7 +10,7 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgta.so")
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 # enum mirrors of include/gta.h
 GTA_F32, GTA_BF16, GTA_F32_BF16 = 0, 1, 2
@@ -48,6 +48,8 @@ SIGNATURES = {
     "gta_apply_edge": (_i32, [_i32, _i32, _vp, _vp, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp,
                               _i64, _vp]),
     "gta_edge_softmax": (_i32, [_vp, _vp, _i64, _i64, _vp, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _vp, _vp]),
+    "gta_apply_edge_flat": (_i32, [_i32, _i32, _vp, _vp, _i64, _vp, _i32, _i64, _i64, _vp, _i32, _i64, _i64, _vp, _i64,
+                                   _vp]),
     "gta_apply_node": (_i32, [_i32, _i32, _i64, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _vp, _i64, _vp]),
     "gta_update_mm": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),
     "gta_update_mm_t": (_i32, [_vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _i32, _i32, _vp, _i64, _vp]),

@@ -1856,6 +1856,56 @@ k_apply_edge_cols(int bin, int sf, const int64_t* __restrict__ indptr, const int
   }
 }
 
+// Round 6: the edge-parallel form (gta_apply_edge_flat) for outputs of exactly 64 * VW columns:
+// a wave takes 32 consecutive edges whatever their rows -- so Flickr's 10-edge rows no longer leave
+// a wave a few edges and three dependent round trips (row bounds, indices, rows) each -- reads their
+// source ids and destination rows (the graph's cached edge -> row table) in one coalesced load,
+// and walks them 8 at a time: each edge's operand rows are uniform addresses (readlane), one
+// 64-lane instruction per 512-B row, 8 edges' rows in flight.  Per element the same
+// sf(bin(a, b)) as every K3 form: bitwise equal to them.
+template <int VW>
+__global__ void __launch_bounds__(kBlock)
+k_apply_edge_flat(int bin, int sf, const int32_t* __restrict__ erow, const int32_t* __restrict__ indices, int64_t nnz,
+                  const float* __restrict__ a, int a_mode, int64_t lda, int ga, const float* __restrict__ b, int b_mode,
+                  int64_t ldb, int gb, float* __restrict__ out, int64_t ldo) {
+  constexpr int EPW = 32, U = 8;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t e0 = (static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform()) * EPW;
+  if (e0 >= nnz) return;
+  const int n = static_cast<int>(min<int64_t>(EPW, nnz - e0));
+  const bool need_src = a_mode == GTA_IDX_SRC || (b != nullptr && ldb != 0 && b_mode == GTA_IDX_SRC);
+  const bool need_dst = a_mode == GTA_IDX_DST || (b != nullptr && ldb != 0 && b_mode == GTA_IDX_DST);
+  const int src = (need_src && lane < n) ? indices[e0 + lane] : 0;
+  const int dst = (need_dst && lane < n) ? erow[e0 + lane] : 0;
+  auto rowof = [&](int mode, int k) -> int64_t {  // k: uniform edge slot of this chunk
+    return mode == GTA_IDX_EDGE ? e0 + k
+                                : static_cast<int64_t>(__builtin_amdgcn_readlane(mode == GTA_IDX_SRC ? src : dst, k));
+  };
+  const int c = lane * VW;
+  for (int u0 = 0; u0 < n; u0 += U) {
+    float va[U][VW], vb[U][VW];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u0 + u < n) {
+        ld_vec<VW>(a + rowof(a_mode, u0 + u) * lda, va[u], ga, c);
+        if (b != nullptr) ld_vec<VW>(b + (ldb == 0 ? 0 : rowof(b_mode, u0 + u)) * ldb, vb[u], gb, c);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u0 + u < n) {
+        float o[VW];
+#pragma unroll
+        for (int q = 0; q < VW; ++q) o[q] = sf_apply(sf, b != nullptr ? bin_apply(bin, va[u][q], vb[u][q]) : va[u][q]);
+        float* op = out + (e0 + u0 + u) * ldo + c;
+        if (VW == 4) *reinterpret_cast<float4*>(op) = make_float4(o[0], o[1], o[2], o[3]);
+        else if (VW == 2) *reinterpret_cast<float2*>(op) = make_float2(o[0], o[1]);
+        else op[0] = o[0];
+      }
+    }
+  }
+}
+
 __global__ void __launch_bounds__(kBlock)
 k_apply_edge_pack(int bin, int sf, const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices,
                   int64_t n_rows, const float* __restrict__ a, int a_mode, int64_t lda, int ga,
@@ -4593,6 +4643,42 @@ int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indice
                                                                  b, b_mode, ldb, gb, out, ldo, fo);
   }
   GTA_LAUNCHED("k_apply_edge");
+  return GTA_OK;
+}
+
+int gta_apply_edge_flat(int bin, int sf, const int32_t* edge_rows, const int32_t* indices, int64_t nnz, const float* a,
+                        int a_mode, int64_t lda, int64_t Fa, const float* b, int b_mode, int64_t ldb, int64_t Fb,
+                        float* out, int64_t ldo, void* stream) {
+  const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
+  if (nnz < 0 || Fa <= 0) return fail(GTA_ERR_ARG, "apply_edge_flat: bad sizes");
+  if (nnz == 0) return GTA_OK;
+  if (!a || !out) return fail(GTA_ERR_ARG, "apply_edge_flat: bad arguments");
+  const bool b_rows = b && ldb != 0;
+  if ((a_mode == GTA_IDX_SRC || (b_rows && b_mode == GTA_IDX_SRC)) && !indices)
+    return fail(GTA_ERR_ARG, "apply_edge_flat: SRC operand needs indices");
+  if ((a_mode == GTA_IDX_DST || (b_rows && b_mode == GTA_IDX_DST)) && !edge_rows)
+    return fail(GTA_ERR_ARG, "apply_edge_flat: DST operand needs edge_rows");
+  int64_t Fo;
+  if (check_bcast(Fa, Fb, b != nullptr, &Fo)) return fail(GTA_ERR_ARG, "apply_edge_flat: widths must divide");
+  const int ga = static_cast<int>(Fo / Fa), gb = b ? static_cast<int>(Fo / Fb) : 1;
+  int vw = 0;
+  for (int c : {4, 2, 1})
+    if (Fo == static_cast<int64_t>(kWave) * c) vw = c;
+  auto vec_ok = [&](int w) {
+    if (ldo % w || !aligned(out, 4 * w)) return false;
+    if (ga == 1 ? (lda % w || !aligned(a, 4 * w)) : (ga % w != 0)) return false;
+    if (b && (gb == 1 ? (ldb % w || !aligned(b, 4 * w)) : (gb % w != 0))) return false;
+    return true;
+  };
+  if (!vw || !vec_ok(vw))
+    return fail(GTA_ERR_UNSUPPORTED, "apply_edge_flat: the output must be 64, 128 or 256 columns, rows aligned to them");
+  const dim3 grid(static_cast<unsigned>((nnz + 32 * kWavesPerBlock - 1) / (32 * kWavesPerBlock)));
+#define GTA_AEF(VW_)                                                                                             \
+  k_apply_edge_flat<VW_><<<grid, dim3(kBlock), 0, S(stream)>>>(bin, sf, edge_rows, indices, nnz, a, a_mode, lda, ga, \
+                                                              b, b_mode, ldb, gb, out, ldo)
+  if (vw == 4) GTA_AEF(4); else if (vw == 2) GTA_AEF(2); else GTA_AEF(1);
+#undef GTA_AEF
+  GTA_LAUNCHED("k_apply_edge_flat");
   return GTA_OK;
 }
 

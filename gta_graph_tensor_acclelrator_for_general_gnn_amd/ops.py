@@ -514,10 +514,33 @@ def apply_edge(graph, bin, sf, a, a_mode="edge", b=None, b_mode="edge", out=None
         need = {"edge": graph.nnz, "src": graph.n_cols, "dst": graph.n_rows}[m]
         if t.shape[0] < need:
             raise ValueError(f"apply_edge {name}: {m}-mode operand needs {need} rows")
+    if APPLY_EDGE_FLAT and Fo in (64, 128, 256) and graph.nnz > 0 and _flat_aligned(Fo, a, lda, b, ldb, out, ldo):
+        # edge-parallel form (ABI 13): 32 edges per wave whatever the row lengths
+        dst = "dst" in (a_mode, None if (b is None or b_broadcast_row) else b_mode)
+        check(_L().gta_apply_edge_flat(_BINS[bin], _sf(sf), _ptr(graph.row_of_edge()) if dst else None,
+                                       _ptr(graph.indices), graph.nnz, _ptr(a), _MODES[a_mode], lda, a.shape[1],
+                                       _ptr(b), _MODES[b_mode], ldb, 0 if b is None else b.shape[1], _ptr(out), ldo,
+                                       _stream(a.device)), "apply_edge_flat")
+        return out
     check(_L().gta_apply_edge(_BINS[bin], _sf(sf), _ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz,
                               _ptr(a), _MODES[a_mode], lda, a.shape[1], _ptr(b), _MODES[b_mode], ldb,
                               0 if b is None else b.shape[1], _ptr(out), ldo, _stream(a.device)), "apply_edge")
     return out
+
+
+APPLY_EDGE_FLAT = True  # gta_apply_edge_flat where it applies (round 6); False: the row-sweep forms (A/B)
+
+
+def _flat_aligned(Fo, a, lda, b, ldb, out, ldo):
+    """The vector width of gta_apply_edge_flat (Fo / 64) divides every row start it reads or writes."""
+    vw = Fo // 64
+
+    def ok(t, ld, width):
+        if t is None:
+            return True
+        g = Fo // width
+        return (ld % vw == 0 and t.data_ptr() % (4 * vw) == 0) if g == 1 else g % vw == 0
+    return ok(a, lda, a.shape[1]) and ok(b, ldb, None if b is None else b.shape[1]) and ok(out, ldo, Fo)
 
 
 def edge_softmax(graph, a_dst, b_src, sf="EXP_LEAKY_RELU", normalize=True, out=None, sums=None,

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 12 /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+#define GTA_ABI_VERSION 13 /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
                               hooks; 4: knob sets attached to streams (gta_tuning_*); 5: every UPDATE
                               on hand-written kernels (no vendor library), gta_update_mm_t_splits,
                               the blocked workspace is the slab rows alone and required, bf16
@@ -48,7 +48,7 @@ extern "C" {
                               gta_update_mlp (two chained node GEMMs in one pass); 10: bf16 y of
                               gta_aggregate_self, bf16 x of gta_update_mlp; 11: gta_gather_add takes the ISA
                               DIRECTION (dir R / C) and the CSC view of gta_csc_build; 12:
-                              gta_build_id, gta_synth_alpha and gta_row_ids (scan-free setup) */
+                              gta_build_id, gta_synth_alpha and gta_row_ids (scan-free setup); 13: gta_apply_edge_flat */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -274,6 +274,14 @@ int gta_apply_edge(int bin, int sf, const int64_t* indptr, const int32_t* indice
                    const float* a, int a_mode, int64_t lda, int64_t Fa,
                    const float* b, int b_mode, int64_t ldb, int64_t Fb,
                    float* out, int64_t ldo, void* stream);
+/* ABI 13: the same op edge-parallel -- a wave takes 32 consecutive edges whatever their rows --
+ * for outputs of exactly 64, 128 or 256 columns (rows aligned to 4 / 8 / 16 B).  edge_rows =
+ * the destination row of each edge (int32 [nnz]; needed when an operand is GTA_IDX_DST),
+ * indices = the CSR source ids (needed for GTA_IDX_SRC).  Bitwise equal to gta_apply_edge;
+ * GTA_ERR_UNSUPPORTED for other widths. */
+int gta_apply_edge_flat(int bin, int sf, const int32_t* edge_rows, const int32_t* indices, int64_t nnz, const float* a,
+                        int a_mode, int64_t lda, int64_t Fa, const float* b, int b_mode, int64_t ldb, int64_t Fb,
+                        float* out, int64_t ldo, void* stream);
 
 /* ---- K5 APPLYNODE element-wise -----------------------------------------
  * out[i, c] = sf( a[i, c_a] (bin) b[i, c_b] ), same broadcast rules, ldb == 0

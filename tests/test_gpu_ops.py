@@ -587,14 +587,41 @@ def test_apply_edge_forms_agree(dev, Fa, Fb, modes):
     b = torch.from_numpy(rng.standard_normal((rows[modes[1]], Fb)).astype(np.float32)).to(dev)
     bmode = "edge" if modes[1] == "row" else modes[1]
     outs = []
-    for form in (0, 1):
+    for form, flat in ((0, False), (1, False), (1, True)):  # generic, row-sweep, edge-parallel (ABI 13)
         ops.set_debug("apply_edge_form", form)
+        ops.APPLY_EDGE_FLAT = flat
         try:
             outs.append(ops.apply_edge(g, "MUL", "LEAKY_RELU", a, modes[0], b, bmode,
                                        b_broadcast_row=modes[1] == "row"))
         finally:
             ops.set_debug("apply_edge_form", 1)
-    assert torch.equal(outs[0], outs[1])
+            ops.APPLY_EDGE_FLAT = True
+    assert torch.equal(outs[0], outs[1]) and torch.equal(outs[0], outs[2])
+
+
+@pytest.mark.parametrize("F", [64, 128, 256])
+@pytest.mark.parametrize("n,e", [(300, 6000), (2000, 2001), (7, 31), (100, 65)])
+@pytest.mark.parametrize("sf", ["NONE", "RELU", "EXP"])
+def test_apply_edge_flat_bitwise(dev, F, n, e, sf):
+    """gta_apply_edge_flat (32 edges per wave, whatever the rows) == the row-sweep form bitwise and the
+    fp64 oracle: every operand mode, a head-broadcast b, b absent, edge counts not a multiple of 32
+    or 8, empty rows."""
+    g, ip, ix = _graph(n, e, seed=F + n, empty_rows=min(3, n - 1), dev=dev)
+    rng = np.random.default_rng(F + e)
+    rows = {"src": g.n_rows, "dst": g.n_rows, "edge": g.nnz}
+    for am, bm, Fb in (("src", "dst", F), ("dst", "edge", F // 8), ("edge", "src", F), ("src", None, None)):
+        a = torch.from_numpy(rng.standard_normal((rows[am], F)).astype(np.float32)).to(dev)
+        b = None if bm is None else torch.from_numpy(rng.standard_normal((rows[bm], Fb)).astype(np.float32)).to(dev)
+        outs = []
+        for flat in (False, True):
+            ops.APPLY_EDGE_FLAT = flat
+            try:
+                outs.append(ops.apply_edge(g, "ADD", sf, a, am, b, bm or "edge"))
+            finally:
+                ops.APPLY_EDGE_FLAT = True
+        assert torch.equal(outs[0], outs[1]), (am, bm)
+        ref = isa_ref.apply_edge(ip, ix, "ADD", sf, a.cpu().numpy(), am, None if b is None else b.cpu().numpy(), bm)
+        assert np.allclose(outs[1].cpu().numpy(), ref, rtol=1e-5, atol=1e-5), (am, bm)
 
 
 @pytest.mark.parametrize("pf", [0, 2])
