@@ -10,12 +10,13 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libgta.so")
-ABI_VERSION = 13
+ABI_VERSION = 14
 
 # enum mirrors of include/gta.h
 GTA_F32, GTA_BF16, GTA_F32_BF16 = 0, 1, 2
 DIR_R, DIR_C = 0, 1
 IDX_EDGE, IDX_SRC, IDX_DST = 0, 1, 2
+OK, ERR_ARG, ERR_HIP, ERR_UNSUPPORTED = 0, -1, -2, -3
 BIN_NONE, BIN_ADD, BIN_MUL, BIN_DIV, BIN_SUB = 0, 1, 2, 3, 4
 SF = {"NONE": 0, "RELU": 1, "EXP_LEAKY_RELU": 2, "ELU": 3, "EXP": 4, "LEAKY_RELU": 5, "SIGMOID": 6,
       "TANH": 7, "RECIP": 8}
@@ -31,6 +32,8 @@ SIGNATURES = {
                              _i32, _vp, _i64, _vp, _vp]),
     "gta_aggregate_self": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _i32, _vp, _i64, _i64, _vp, _vp, _i64,
                                   _vp, _vp, _i64, _i32, _vp, _i64, _vp, _vp]),
+    "gta_aggregate_expr": (_i32, [_vp, _vp, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _i32, _i64, _vp, _i64, _vp,
+                                  _i64, _vp, _vp]),
     "gta_aggregate_plan_bytes": (_i64, [_i64, _i64, _i64]),
     "gta_aggregate_plan_build": (_i32, [_vp, _i64, _i64, _i64, _vp, _i64, _vp]),
     "gta_aggregate_workspace_bytes": (_i64, [_i64, _i64, _i64, _i64]),

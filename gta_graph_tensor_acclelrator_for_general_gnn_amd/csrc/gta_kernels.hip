@@ -248,7 +248,102 @@ __global__ void k_plan_fill(const int64_t* __restrict__ indptr, int64_t n_rows, 
 //   ds_bpermute.  Accumulation is fp32 in VGPRs, in a fixed order: results are
 //   bitwise reproducible run to run (no atomics).
 // ---------------------------------------------------------------------------
-enum { XM_IDX = 0, XM_EDGE = 1 };
+enum { XM_IDX = 0, XM_EDGE = 1, XM_EX1 = 2, XM_EX2 = 3, XM_EX3 = 4 };
+
+// XM_EX*: the gathered value of edge e is an expression of K3 apply_edge ops over up to four
+// operand rows (gta_aggregate_expr; DGN's op 2-7 tree, PNA's op 5-7), evaluated as the edge is
+// summed -- the [E, F] edge tensors the tree's ops would store are never written.  Per element,
+// with L0..L3 the operands' values:
+//   XM_EX1: t = sf0(L0 bin0 L1)             (bin0 NONE: sf0(L0))
+//   XM_EX2: u = sf0(L0 bin0 L1); t = sf1(swap ? L2 bin1 u : u bin1 L2)
+//   XM_EX3: u = sf0(L0 bin0 L1); v = sf1(L2 bin1 L3); t = sf2(u bin2 v)
+// each step sf_apply(bin_apply()) as k_apply_edge* computes it, each intermediate an fp32 value as
+// the stored edge tensor holds it (no contraction across steps), summed in k_aggregate's XM_EDGE
+// order: bitwise the unfused apply_edge ops + gather.  Operand modes: GTA_IDX_EDGE (row e; ld 0:
+// one row broadcast to every edge), GTA_IDX_SRC (row indices[e]), GTA_IDX_DST (the item's row).
+// Every operand is loaded per edge (row-constant ones hit L1).  Each step runs
+// over a whole unrolled step's values under ONE uniform switch on its op (per-element switches
+// made a 6.6 k-instruction kernel 7x slower than the unfused ops).  The op codes are packed in
+// `code` (kernel arguments in few SGPRs): mode l at bits 2l, bin i at 8 + 3i, sf i at 17 + 4i,
+// swap at 29.
+struct ExprArgs {
+  const float* p[4];
+  int ld[4];
+  int code;
+};
+
+__host__ __device__ constexpr int ex_mode(int code, int l) { return (code >> (2 * l)) & 3; }
+__host__ __device__ constexpr int ex_bin(int code, int i) { return (code >> (8 + 3 * i)) & 7; }
+__host__ __device__ constexpr int ex_sf(int code, int i) { return (code >> (17 + 4 * i)) & 15; }
+__host__ __device__ constexpr int ex_swap(int code) { return (code >> 29) & 1; }
+
+template <int XMODE>
+constexpr int expr_leaves() { return XMODE == XM_EX1 ? 2 : (XMODE == XM_EX2 ? 3 : (XMODE == XM_EX3 ? 4 : 0)); }
+
+// d[k] = a[k] bin b[k] over M values (bin NONE: d = a), bin_apply's arithmetic
+template <int M>
+__device__ __forceinline__ void bin_arr(int bin, float* d, const float* a, const float* b) {
+#pragma clang fp contract(off)
+  switch (bin) {
+    case GTA_BIN_ADD:
+#pragma unroll
+      for (int k = 0; k < M; ++k) d[k] = bin_apply(GTA_BIN_ADD, a[k], b[k]);
+      break;
+    case GTA_BIN_MUL:
+#pragma unroll
+      for (int k = 0; k < M; ++k) d[k] = bin_apply(GTA_BIN_MUL, a[k], b[k]);
+      break;
+    case GTA_BIN_DIV:
+#pragma unroll
+      for (int k = 0; k < M; ++k) d[k] = bin_apply(GTA_BIN_DIV, a[k], b[k]);
+      break;
+    case GTA_BIN_SUB:
+#pragma unroll
+      for (int k = 0; k < M; ++k) d[k] = bin_apply(GTA_BIN_SUB, a[k], b[k]);
+      break;
+    default:
+#pragma unroll
+      for (int k = 0; k < M; ++k) d[k] = a[k];
+  }
+}
+
+// d[k] = sf(d[k]) over M values, sf_apply's arithmetic
+template <int M>
+__device__ __forceinline__ void sf_arr(int sf, float* d) {
+#pragma clang fp contract(off)
+#define GTA_SF_CASE(K_)                                              \
+  case K_:                                                           \
+    _Pragma("unroll") for (int k = 0; k < M; ++k) d[k] = sf_apply(K_, d[k]); \
+    break;
+  switch (sf) {
+    GTA_SF_CASE(GTA_SF_RELU) GTA_SF_CASE(GTA_SF_EXP_LEAKY_RELU) GTA_SF_CASE(GTA_SF_ELU) GTA_SF_CASE(GTA_SF_EXP)
+    GTA_SF_CASE(GTA_SF_LEAKY_RELU) GTA_SF_CASE(GTA_SF_SIGMOID) GTA_SF_CASE(GTA_SF_TANH) GTA_SF_CASE(GTA_SF_RECIP)
+    default: break;  // GTA_SF_NONE
+  }
+#undef GTA_SF_CASE
+}
+
+// the expression over one unrolled step: L[l] = operand l's M values, t = the edge values
+template <int XMODE, int M>
+__device__ __forceinline__ void expr_eval(int code, float (&L)[4][M], float* t) {
+  float u[M];
+  bin_arr<M>(ex_bin(code, 0), u, L[0], L[1]);
+  sf_arr<M>(ex_sf(code, 0), u);
+  if constexpr (XMODE == XM_EX1) {
+#pragma unroll
+    for (int k = 0; k < M; ++k) t[k] = u[k];
+  } else if constexpr (XMODE == XM_EX2) {
+    if (ex_swap(code)) bin_arr<M>(ex_bin(code, 1), t, L[2], u);
+    else bin_arr<M>(ex_bin(code, 1), t, u, L[2]);
+    sf_arr<M>(ex_sf(code, 1), t);
+  } else {
+    float v[M];
+    bin_arr<M>(ex_bin(code, 1), v, L[2], L[3]);
+    sf_arr<M>(ex_sf(code, 1), v);
+    bin_arr<M>(ex_bin(code, 2), t, u, v);
+    sf_arr<M>(ex_sf(code, 2), t);
+  }
+}
 
 // WM_EDGE1: one weight per edge (H = 1: GCN's 1/sqrt(d_i d_j), GIN's edge operand) -- 64 weights
 // per coalesced load beside the 64 indices, broadcast to the edge's lanes like its index, instead of
@@ -265,15 +360,19 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
             const float* __restrict__ w, int64_t ldw, int gsz,
             const float* __restrict__ row_scale, float* __restrict__ y, int64_t ldy, int accumulate,
             float* __restrict__ partial, const TX* __restrict__ xs = nullptr, int64_t ldxs = 0,
-            const float* __restrict__ self_scale = nullptr, int y_bf16 = 0) {
+            const float* __restrict__ self_scale = nullptr, int y_bf16 = 0, const ExprArgs ex = ExprArgs{}) {
   // xs (gta_aggregate_self): y[row] = self_scale * xs[row] + row_scale[row] * sum, the self term
   // formed exactly as an applynode MUL by a broadcast scalar would (GIN op 3 + op 4).
   // y_bf16: y holds bf16 (RNE of the fp32 value; ldy in bf16 elements) -- for a consumer that rounds
   // its input to bf16 anyway (the fused GIN MLP), so the rounding happens once, here
+  // ex (XMODE XM_EX*): the edge value is an apply_edge expression of ex's operands (see ExprArgs)
   constexpr int EPI = kWave / LPE;                 // edges per wave instruction
-  // row loads in flight per lane: ~64 B of each lane's rows per unrolled step
+  constexpr int NL = expr_leaves<XMODE>();         // expression operands (0: a plain gather)
+  // row loads in flight per lane: ~64 B of each lane's rows per unrolled step (an expression
+  // gathers up to NL rows per edge: ~32 B of each)
   constexpr int XB = NV * VW * static_cast<int>(sizeof(TX));
-  constexpr int UR = URX ? URX : ((64 / XB) < 2 ? 2 : ((64 / XB) > 8 ? 8 : 64 / XB));
+  constexpr int RB = NL ? 32 : 64;
+  constexpr int UR = URX ? URX : ((RB / XB) < 2 ? 2 : ((RB / XB) > 8 ? 8 : RB / XB));
   constexpr int STEP = UR * EPI;                    // edges per unrolled step
   const int lane = threadIdx.x & (kWave - 1);
   const int64_t item = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
@@ -320,7 +419,7 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
 
     // source indices arrive 64 at a time; the next block's are prefetched while
     // this block's rows are in flight (clamped address: the load is unconditional)
-    const bool use_idx = (XMODE == XM_IDX) && !x_is_row;
+    const bool use_idx = ((XMODE == XM_IDX) && !x_is_row) || NL > 0;
     int idxv = 0;
     float wv = 0.f;
     if (use_idx && eb < ee) idxv = indices[min(eb + lane, ee - 1)];
@@ -335,12 +434,32 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
         Vec<VW> xv[UR][NV];
         float wh[UR][NV];
         Vec<VW> wf[(WMODE == WM_FULL) ? UR : 1][(WMODE == WM_FULL) ? NV : 1];
+        float lv[4][NL ? UR * NV * VW : 1];  // an expression's operand values per edge
         bool valid[UR];
 #pragma unroll
         for (int u = 0; u < UR; ++u) {
           const int j = s + u * EPI + sub;
           valid[u] = j < n;
           const int jj = j < n ? j : n - 1;
+          if constexpr (NL > 0) {
+            const int64_t sr = (LPE == kWave) ? __builtin_amdgcn_readlane(idxv, jj) : __shfl(idxv, jj);
+#pragma unroll
+            for (int l = 0; l < NL; ++l) {
+              // straight-line: every operand loaded per edge at a uniform address (a DST row or a
+              // broadcast row repeats within the item: L1 hits), no branch between the loads
+              const int md = ex_mode(ex.code, l);
+              const int64_t r = md == GTA_IDX_SRC ? sr : (md == GTA_IDX_DST ? row : e0 + jj);
+              const float* p = ex.p[l] + r * static_cast<int64_t>(ex.ld[l]);
+              Vec<VW> q[NV];
+#pragma unroll
+              for (int v = 0; v < NV; ++v) q[v].load(p + col[v]);
+#pragma unroll
+              for (int v = 0; v < NV; ++v)
+#pragma unroll
+                for (int k = 0; k < VW; ++k) lv[l][(u * NV + v) * VW + k] = q[v].v[k];
+            }
+            continue;
+          }
           int64_t xr;
           if (XMODE == XM_EDGE) {
             xr = e0 + jj;
@@ -369,6 +488,16 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
 #pragma unroll
             for (int v = 0; v < NV; ++v) wf[u][v].load(wp + col[v]);
           }
+        }
+        if constexpr (NL > 0) {
+          float t[UR * NV * VW];
+          expr_eval<XMODE, UR * NV * VW>(ex.code, lv, t);
+#pragma unroll
+          for (int u = 0; u < UR; ++u)
+#pragma unroll
+            for (int v = 0; v < NV; ++v)
+#pragma unroll
+              for (int k = 0; k < VW; ++k) xv[u][v].v[k] = t[(u * NV + v) * VW + k];
         }
 #pragma unroll
         for (int u = 0; u < UR; ++u) {
@@ -3695,6 +3824,7 @@ struct AggArgs {
   const float* row_scale; float* y; int64_t ldy; int accumulate; float* partial;
   const void* xs; int64_t ldxs; const float* self_scale;  // gta_aggregate_self's term (xs: x's dtype)
   int y_bf16;                                            // y stored as bf16 (gta_aggregate_self, y_dtype)
+  ExprArgs ex;                                           // gta_aggregate_expr's operands (XM_EX*)
 };
 
 template <int LPE, int VW, int NV, int XM, int WM, typename TX, int URX = 0>
@@ -3703,7 +3833,7 @@ void launch_agg(const AggArgs& a, int64_t n_items_bound, hipStream_t s) {
   k_aggregate<LPE, VW, NV, XM, WM, TX, URX><<<dim3(static_cast<unsigned>(blocks)), dim3(kBlock), 0, s>>>(
       a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, a.x_is_row, static_cast<const TX*>(a.x), a.ldx, a.F,
       a.w, a.ldw, a.gsz, a.row_scale, a.y, a.ldy, a.accumulate, a.partial, static_cast<const TX*>(a.xs), a.ldxs,
-      a.self_scale, a.y_bf16);
+      a.self_scale, a.y_bf16, a.ex);
 }
 
 // (non-temporal index/weight loads measured +3 %: plain loads throughout)
@@ -3727,8 +3857,23 @@ bool dispatch_w(int wm, bool bf, const AggArgs& a, int64_t nb, hipStream_t s) {
   return false;
 }
 
+// expressions (gta_aggregate_expr): fp32, unweighted; the 16-B form at every lane count, the 8-B
+// form (F in [128, 256) or F % 4 == 2) at 64 lanes per edge only
+template <int LPE, int VW, int NV>
+bool dispatch_expr(int xm, const AggArgs& a, int64_t nb, hipStream_t s) {
+  if constexpr (VW == 4 || (VW == 2 && LPE == kWave)) {
+    switch (xm) {
+      case XM_EX1: launch_agg<LPE, VW, NV, XM_EX1, WM_NONE, float>(a, nb, s); return true;
+      case XM_EX2: launch_agg<LPE, VW, NV, XM_EX2, WM_NONE, float>(a, nb, s); return true;
+      case XM_EX3: launch_agg<LPE, VW, NV, XM_EX3, WM_NONE, float>(a, nb, s); return true;
+    }
+  }
+  return false;
+}
+
 template <int LPE, int VW, int NV>
 bool dispatch_x(int xm, int wm, bool bf, const AggArgs& a, int64_t nb, hipStream_t s) {
+  if (xm >= XM_EX1) return !bf && wm == WM_NONE && dispatch_expr<LPE, VW, NV>(xm, a, nb, s);
   return xm == XM_EDGE ? dispatch_w<LPE, VW, NV, XM_EDGE>(wm, bf, a, nb, s)
                        : dispatch_w<LPE, VW, NV, XM_IDX>(wm, bf, a, nb, s);
 }
@@ -3963,9 +4108,21 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
                    const void* x, int64_t ldx, int64_t F, int x_dtype, const float* w, int64_t ldw, int64_t heads,
                    const float* row_scale, float* y, int64_t ldy, int accumulate, const void* plan,
                    int64_t plan_chunk, void* workspace, void* stream, const void* xs, int64_t ldxs,
-                   const float* self_scale, int y_bf16 = 0) {
+                   const float* self_scale, int y_bf16 = 0, const ExprArgs* ex = nullptr, int ex_mode = 0) {
   const CallTuning ct_(stream);  // knobs attached to this stream, if any (gta_tuning_attach)
   if (n_rows < 0 || nnz < 0 || F <= 0) return fail(GTA_ERR_ARG, "aggregate: bad sizes");
+  ExprArgs exa{};
+  if (ex) {  // gta_aggregate_expr: x_mode / x / w unused; every edge reads its source index
+    exa = *ex;
+    x_mode = GTA_IDX_EDGE;
+    x = exa.p[0];
+    w = nullptr;
+    if (nnz > 0 && !indices) return fail(GTA_ERR_ARG, "aggregate_expr: indices is NULL");
+    if (nnz == 0) {  // no edge is read; the per-item operand loads read y's first row instead
+      for (int l = 0; l < 4; ++l) { exa.p[l] = y; exa.ld[l] = 0; }
+      exa.code &= ~0xff;  // every mode GTA_IDX_EDGE
+    }
+  }
   if (y_bf16 && (accumulate || ldy < F)) return fail(GTA_ERR_ARG, "aggregate: a bf16 y takes no accumulate; ldy >= F");
   if (xs && (accumulate || ldxs < F)) return fail(GTA_ERR_ARG, "aggregate_self: no accumulate; ld_self >= F");
   if (x_mode != GTA_IDX_EDGE && x_mode != GTA_IDX_SRC && x_mode != GTA_IDX_DST)
@@ -3990,9 +4147,11 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
     wm = (heads == F) ? WM_FULL : ((heads == 1 && tuning().agg_w1) ? WM_EDGE1 : WM_HEAD);
     gsz = static_cast<int>(F / heads);
   }
-  const int xm = (x_mode == GTA_IDX_EDGE) ? XM_EDGE : XM_IDX;
-  // widest vector that keeps every access aligned
+  const int xm = ex ? ex_mode : ((x_mode == GTA_IDX_EDGE) ? XM_EDGE : XM_IDX);
+  // widest vector that keeps every access aligned (an expression: the width its unfused gather
+  // of a fresh [E, F] edge tensor takes -- its operands must allow it, checked below)
   auto ok_vw = [&](int vw) {
+    if (ex) return F % vw == 0 && ldy % vw == 0 && aligned(y, 4 * vw);
     if (F % vw || ldx % vw || ldy % vw || !aligned(x, xe * vw) || !aligned(y, (y_bf16 ? 2 : 4) * vw)) return false;
     if (xs && (ldxs % vw || !aligned(xs, xe * vw))) return false;
     if (wm == WM_HEAD && gsz % vw) return false;
@@ -4031,7 +4190,14 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
     while (lpe < ln) lpe <<= 1;
   }
 
+  if (ex) {
+    const int nl = ex_mode == XM_EX1 ? (ex_bin(exa.code, 0) == GTA_BIN_NONE ? 1 : 2) : (ex_mode == XM_EX2 ? 3 : 4);
+    for (int l = 0; l < nl; ++l)
+      if (exa.ld[l] % vw || !aligned(exa.p[l], 4 * vw))
+        return fail(GTA_ERR_UNSUPPORTED, "aggregate_expr: an operand's rows are not aligned to the gather's vector width");
+  }
   AggArgs a{};
+  a.ex = exa;
   a.indptr = indptr; a.indices = indices; a.n_rows = n_rows;
   a.use_plan = plan != nullptr; a.chunk = plan_chunk; a.x_is_row = (x_mode == GTA_IDX_DST);
   a.x = x; a.ldx = ldx; a.F = static_cast<int>(F); a.w = w; a.ldw = ldw; a.gsz = gsz;
@@ -4097,6 +4263,39 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
                   int64_t plan_chunk, void* workspace, void* stream) {
   return aggregate_impl(indptr, indices, n_rows, nnz, x_mode, x, ldx, F, x_dtype, w, ldw, heads, row_scale, y, ldy,
                         accumulate, plan, plan_chunk, workspace, stream, nullptr, 0, nullptr);
+}
+
+int gta_aggregate_expr(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int shape,
+                       const float* const* operands, const int* modes, const int64_t* lds, const int* bins,
+                       const int* sfs, int swap, int64_t F, float* y, int64_t ldy, const void* plan,
+                       int64_t plan_chunk, void* workspace, void* stream) {
+  if (shape < 1 || shape > 3) return fail(GTA_ERR_ARG, "aggregate_expr: shape must be 1, 2 or 3");
+  if (!operands || !modes || !lds || !bins || !sfs) return fail(GTA_ERR_ARG, "aggregate_expr: NULL operand arrays");
+  ExprArgs ex{};
+  int code = swap ? (1 << 29) : 0;
+  const int n_ops = shape;
+  for (int i = 0; i < n_ops; ++i) {
+    const bool none_ok = shape == 1 && i == 0;
+    if (bins[i] < (none_ok ? GTA_BIN_NONE : GTA_BIN_ADD) || bins[i] > GTA_BIN_SUB)
+      return fail(GTA_ERR_ARG, "aggregate_expr: bad bin");
+    if (sfs[i] < GTA_SF_NONE || sfs[i] > GTA_SF_RECIP) return fail(GTA_ERR_ARG, "aggregate_expr: bad sf");
+    code |= (bins[i] << (8 + 3 * i)) | (sfs[i] << (17 + 4 * i));
+  }
+  const int nl = shape == 1 ? (bins[0] == GTA_BIN_NONE ? 1 : 2) : shape + 1;
+  for (int l = 0; l < 4; ++l) {
+    const int k = l < nl ? l : 0;  // unused slots repeat operand 0
+    if (modes[k] != GTA_IDX_EDGE && modes[k] != GTA_IDX_SRC && modes[k] != GTA_IDX_DST)
+      return fail(GTA_ERR_ARG, "aggregate_expr: bad operand mode");
+    if ((lds[k] < F && !(modes[k] == GTA_IDX_EDGE && lds[k] == 0)) || (nnz > 0 && !operands[k]))
+      return fail(GTA_ERR_ARG, "aggregate_expr: operand rows need ld >= F (or ld 0: a broadcast row)");
+    if (lds[k] > INT32_MAX) return fail(GTA_ERR_UNSUPPORTED, "aggregate_expr: operand row stride >= 2^31");
+    ex.p[l] = operands[k];
+    ex.ld[l] = static_cast<int>(lds[k]);
+    code |= modes[k] << (2 * l);
+  }
+  ex.code = code;
+  return aggregate_impl(indptr, indices, n_rows, nnz, GTA_IDX_EDGE, ex.p[0], F, F, GTA_F32, nullptr, 0, 0, nullptr,
+                        y, ldy, 0, plan, plan_chunk, workspace, stream, nullptr, 0, nullptr, 0, &ex, XM_EX1 + shape - 1);
 }
 
 int gta_aggregate_self(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int x_mode,

@@ -138,6 +138,12 @@ class ExecResult:
                 f"{self.model_rw}))")
 
 
+def _forced(v):
+    return v.force() if isinstance(v, Lazy) else v
+
+
+EDGE_EXPR = True  # Executor.edge_expr's default (gta_aggregate_expr for applyedge trees); False: unfused (A/B)
+
 MAX_MATERIALIZE_BYTES = 96 << 30  # refuse to materialise a single edge tensor larger than this
 
 
@@ -154,6 +160,7 @@ class Executor:
         self.sem = semantics or Semantics()
         self.plan_chunk = plan_chunk
         self.values = {}
+        self._nmm = {}  # node GEMMs of _node_mm in this run: (op, x) -> x W
         self.alg_bytes = 0
         self.launches = 0
         # trace: per evaluated op, device time (HIP events), algorithmic bytes and launches, as
@@ -194,6 +201,9 @@ class Executor:
         #   to fp32 rounding, the gather's own value computed only if something asks for it
         self.mm_first = True
         self.reorder = self._match_mm_first()
+        #   and through two hops (SGC: gather -> scatter C -> MUL -> gather -> MM): A (A x) W == A (A (x W)),
+        #   both aggregates at the narrow width; the first gather's value computed only if asked for
+        self.two_hop = self._match_two_hop() if dist is None else {}
         #   node_mm: an applyedge MM of a scatter runs on the node tensor, (x W)[r(e)] == x[r(e)] W
         #   (bitwise: the same dot product per row), and stays a virtual scatter of x W
         #   mm_pushdown: MM(scatter a (+) scatter b) == (a W)[r(e)] (+) (b W)[r'(e)] (DGN op 2 -> 3),
@@ -211,6 +221,13 @@ class Executor:
         self.gather_acc = dist is None or dist.local_rows or dist.s.world == 1
         self.gacc = self._match_gather_acc()
         self.gacc_t = {T: A for A, (_, _, T) in self.gacc.items()}  # node op T -> its ADD consumer
+        #   edge_expr: a gather R whose edge value is a tree of applyedge ops (ADD / SUB / MUL / DIV,
+        #   SF post-ops, a pushed-down MM), each read only by the next, runs as one
+        #   gta_aggregate_expr: no [E, F] tensor for any op of the tree, bitwise the unfused ops and
+        #   gather (DGN ops 2-8, PNA ops 5-8).  The tree's ops stay available, computed unfused if read.
+        self.edge_expr = EDGE_EXPR
+        self.expr = self._match_edge_expr()
+        self.expr_nodes = {i for e in self.expr.values() for i in e["nodes"]}
 
     # ---------------------------------------------------------------- inputs
     def _ext(self, op, slot):
@@ -357,6 +374,39 @@ class Executor:
             found[G.idx] = M.idx
         return found
 
+    def _match_two_hop(self):
+        """{first gather G1: second gather G2} for G1 -> scatter C -> [MUL by an edge weight] -> G2 with
+        G2 in reorder (its narrowing MM), each intermediate read only by the next op, and G1 of the
+        form mm_first takes (a scatter C of a node tensor, directly or through a weight MUL)."""
+        ops_, ins, cons = self.g.ops, self.g.inputs, self.consumers
+        found = {}
+        for G2 in self.reorder:
+            P = ops_[ins[G2][0].op]
+            if P.type == "scatter":
+                S = P
+            else:
+                sc = [x.op for x in ins[P.idx] if x.kind == "op" and ops_[x.op].type == "scatter"]
+                if len(sc) != 1 or cons[sc[0]] != [P.idx]:
+                    continue
+                S = ops_[sc[0]]
+            if S.order != "C" or not ins[S.idx] or ins[S.idx][0].kind != "op":
+                continue
+            G1 = ops_[ins[S.idx][0].op]
+            if G1.type != "gather" or G1.order != "R" or G1.comp != "ADD" or cons[G1.idx] != [S.idx]:
+                continue
+            src = ins[G1.idx][0]
+            if src.kind != "op":
+                continue
+            P1 = ops_[src.op]
+            if P1.type == "applyedge" and P1.comp == "MUL":
+                sc1 = [x.op for x in ins[P1.idx] if x.kind == "op" and ops_[x.op].type == "scatter"]
+                if len(sc1) != 1 or ops_[sc1[0]].order != "C":
+                    continue
+            elif not (P1.type == "scatter" and P1.order == "C"):
+                continue
+            found[G1.idx] = G2
+        return found
+
     def _match_pushdown(self):
         """{applyedge ADD of two scatters: its only consumer, a single-input applyedge MM}."""
         found = {}
@@ -374,6 +424,126 @@ class Executor:
                     and self.sem.bin_of(op) == "ADD":
                 found[op.idx] = m.idx
         return found
+
+    def _match_edge_expr(self):
+        """{gather G: plan} for a gather R (ADD) of an applyedge tree that gta_aggregate_expr's shapes
+        cover.  plan: shape, swap, bins, sfs, leaves ((op, slot) of a computed operand, or ("pmm", MM
+        op, k): the k-th scatter of a pushed-down MM's sum, multiplied on its node rows) and nodes (the
+        tree's ops, deferred until G runs).  Trees the existing fusions take are left to them: a lone
+        MUL / MM (the weighted aggregate), the attention chains, the GIN self-term gathers."""
+        ops_, ins, cons = self.g.ops, self.g.inputs, self.consumers
+        att = set(self.attn)
+        for pat in self.softmax.values():
+            att.update(i for i in (pat["A"], pat["V"], pat["D"]) if i is not None)
+        acc_g = {g for g, _, _ in self.gacc.values()}
+
+        def node(i):  # -> ("bin", bin, sf, left, right, ops) | ("leaf", ref) | None (not coverable)
+            o = ops_[i]
+            if o.type != "applyedge" or i in att:
+                return None
+            if o.comp == "SF":
+                if len(ins[i]) != 1 or ins[i][0].kind != "op" or cons[ins[i][0].op] != [i]:
+                    return None
+                c = node(ins[i][0].op)
+                if c is None or c[0] != "bin" or c[2] is not None or c[1] == "PMM":
+                    return None  # an SF on a pushed-down MM acts on the sum: not this tree
+                return ("bin", c[1], self.sem.sf_of(o), c[3], c[4], c[5] + [i])
+            if o.comp == "MM":
+                src = ins[i][0] if len(ins[i]) == 1 else None
+                if src is None or src.kind != "op" or self.pushdown.get(src.op) != i:
+                    return None
+                return ("bin", "PMM", None, ("leaf", ("pmm", i, 0)), ("leaf", ("pmm", i, 1)), [i])
+            if o.comp not in ("ADD", "SUB", "MUL", "DIV") or len(ins[i]) != 2:
+                return None
+            b = self.sem.bin_of(o)
+            kids = []
+            for slot, x in enumerate(ins[i]):
+                sub = None
+                if x.kind == "op" and cons[x.op] == [i] and ops_[x.op].type == "applyedge":
+                    sub = node(x.op)
+                kids.append(sub if sub is not None else ("leaf", (i, slot)))
+            if b == "RDIV":
+                b, kids = "DIV", kids[::-1]
+            if b not in ("ADD", "SUB", "MUL", "DIV"):
+                return None
+            return ("bin", b, None, kids[0], kids[1], [i])
+
+        def leafy(t):
+            return t[0] == "bin" and t[3][0] == "leaf" and t[4][0] == "leaf"
+
+        def b_of(t):
+            return "ADD" if t[1] == "PMM" else t[1]
+
+        found = {}
+        for G in ops_:
+            if G.type != "gather" or G.order != "R" or G.comp != "ADD" or G.idx in acc_g:
+                continue
+            src = ins[G.idx][0] if len(ins[G.idx]) == 1 else None
+            if src is None or src.kind != "op" or cons[src.op] != [G.idx]:
+                continue
+            t = node(src.op)
+            if t is None:
+                continue
+            L, R = t[3], t[4]
+            if leafy(t):
+                if t[1] in ("MUL", "PMM") and t[2] is None:
+                    continue  # the weighted aggregate / the pushed-down MM's own path
+                e = dict(shape=1, swap=False, bins=[b_of(t)], sfs=[t[2]], leaves=[L[1], R[1]], nodes=t[5])
+            elif leafy(L) and R[0] == "leaf":
+                e = dict(shape=2, swap=False, bins=[b_of(L), t[1]], sfs=[L[2], t[2]], leaves=[L[3][1], L[4][1], R[1]],
+                         nodes=L[5] + t[5])
+            elif L[0] == "leaf" and leafy(R):
+                e = dict(shape=2, swap=True, bins=[b_of(R), t[1]], sfs=[R[2], t[2]], leaves=[R[3][1], R[4][1], L[1]],
+                         nodes=R[5] + t[5])
+            elif leafy(L) and leafy(R):
+                e = dict(shape=3, swap=False, bins=[b_of(L), b_of(R), t[1]], sfs=[L[2], R[2], t[2]],
+                         leaves=[L[3][1], L[4][1], R[3][1], R[4][1]], nodes=L[5] + R[5] + t[5])
+            else:
+                continue
+            found[G.idx] = e
+        return found
+
+    def _eval_edge_expr(self, G):
+        """G's value from one gta_aggregate_expr launch, or None (then the tree runs unfused)."""
+        e = self.expr[G.idx]
+        for i in e["nodes"]:
+            raw = self.values.get(i)
+            if not (isinstance(raw, Lazy) and raw.v is None):
+                return None
+        operands, gathered = [], 0
+        for ref in e["leaves"]:
+            if ref[0] == "pmm":
+                mm = self.g.ops[ref[1]]
+                v = self._source(self.g.ops[self.g.inputs[mm.idx][0].op], ref[2])
+                if not isinstance(v, Scat):
+                    return None
+                v = self._node_mm(mm, v)
+            else:
+                v = self._source(self.g.ops[ref[0]], ref[1])
+            if isinstance(v, Scat):
+                operands.append((v.t if v.t.dtype == torch.float32 else v.t.float(), v.mode))
+                gathered += v.mode == "src"
+            elif isinstance(v, EdgeT):
+                operands.append((v.t, "edge"))
+                gathered += 1
+            elif isinstance(v, tuple) and v[0] == "row":
+                operands.append((v[1], "row"))
+            else:
+                return None
+        F = operands[0][0].shape[1]
+        if any(t.shape[1] != F or t.dtype != torch.float32 for t, _ in operands):
+            return None
+        y = ops.aggregate_expr(self.graph, e["shape"], operands, e["bins"], e["sfs"], e["swap"], plan=self._plan())
+        if y is None:
+            return None
+        for mm in {ref[1] for ref in e["leaves"] if ref[0] == "pmm"}:
+            # a pushed-down MM read later is the pushed-down product, as the unfused run forms it,
+            # whether or not its sum's value has been asked for in between
+            mop, add = self.g.ops[mm], self.g.inputs[mm][0].op
+            self.values[mm] = Lazy(lambda mop=mop, add=add: self._pushdown_mm(mop, add))
+        n, E = self.graph.n_rows, self.graph.nnz
+        self._count(E * (4 + 4 * F * gathered) + n * (8 + 4 * F))
+        return NodeT(self.dist.reduce_rows(y) if self.dist is not None else y)
 
     def _match_gather_acc(self):
         """{applynode ADD A: (gather G, slot of T, node op T)} for A = ADD(G, T) where A is G's and T's
@@ -447,13 +617,18 @@ class Executor:
         return y
 
     def _node_mm(self, op, v, post_sf=None):
-        """applyedge MM of a virtual scatter: the GEMM runs over the node rows, the result stays virtual."""
+        """applyedge MM of a virtual scatter: the GEMM runs over the node rows, the result stays virtual.
+        The two scatters of one node table under one MM (DGN op 3's x[src] + x[dst]) share a GEMM."""
         W = self.tensors[f"w:{op.idx}"]
         x, W = self._mm_dtypes(v.local, W)
         if W.shape[0] != x.shape[1]:
             raise ValueError(f"op {op.idx}: weight rows {W.shape[0]} != feature width {x.shape[1]}")
-        xw = ops.update_mm(x, W, sf=post_sf)
-        self._count(x.shape[0] * (x.shape[1] * x.element_size() + W.shape[1] * 4) + W.numel() * W.element_size())
+        key = (op.idx, post_sf, x.data_ptr(), tuple(x.shape), tuple(x.stride()), x.dtype)
+        xw = self._nmm.get(key)
+        if xw is None:
+            xw = ops.update_mm(x, W, sf=post_sf)
+            self._count(x.shape[0] * (x.shape[1] * x.element_size() + W.shape[1] * 4) + W.numel() * W.element_size())
+            self._nmm[key] = xw
         return Scat(xw, v.mode, v.fill)
 
     def _pushdown_mm(self, op, add_idx, post_sf=None):
@@ -527,9 +702,8 @@ class Executor:
             return v
         return NodeT(self.dist.reduce_cols(v.t) if op.order == "C" else self.dist.reduce_rows(v.t))
 
-    def _eval_mm_first(self, G, M):
-        """Sets M's value to aggregate(x W) and returns G's value lazily; None if the operands
-        do not allow it (head-wise weights, edge-tensor features)."""
+    def _mm_first_operands(self, G):
+        """(x, w, fill) of a gather G = sum_e w_e x[src(e)] (w None: unweighted), or None."""
         v = self._source(G, 0)
         if isinstance(v, Deferred):
             p = self.g.ops[v.op]
@@ -554,6 +728,60 @@ class Executor:
             x, w, fill = v.local, None, v.fill
         else:
             return None
+        return x, w, fill
+
+    def _eval_two_hop(self, G2, M):
+        """M = A (A x) W as A (A (x W)): the first hop G1's value and its scatter stay unformed."""
+        G1 = next((g1 for g1, g2 in self.two_hop.items() if g2 == G2.idx), None)
+        raw = self.values.get(G1) if G1 is not None else None
+        if not (self.mm_first and isinstance(raw, Lazy) and raw.v is None):
+            return None
+        src = self.g.inputs[G2.idx][0]
+        P = self.g.ops[src.op]
+        w2 = None
+        if P.type != "scatter":  # the second hop's weight MUL: its operand that is not the scatter
+            pv = self.values.get(P.idx)
+            if not isinstance(pv, Deferred) or P.comp != "MUL" or self.sem.bin_of(P) != "MUL":
+                return None
+            slots = [k for k, x in enumerate(self.g.inputs[P.idx])
+                     if not (x.kind == "op" and self.g.ops[x.op].type == "scatter")]
+            others = [self._source(P, k) for k in slots]
+            if len(self.g.inputs[P.idx]) == 1:
+                extra = self._ext(P, 1)
+                others = [self._wrap_ext(extra)] if extra is not None else []
+            if len(others) > 1 or (others and isinstance(others[0], (tuple, Scat))):
+                return None
+            if others:
+                w2 = self._to_edge_tensor(others[0])
+                if w2.shape[1] != 1:
+                    return None
+        opnd = self._mm_first_operands(self.g.ops[G1])
+        if opnd is None:
+            return None
+        x, w1, fill = opnd
+        W = self.tensors[f"w:{M.idx}"]
+        if fill is not None or W.shape[0] != x.shape[1]:
+            return None
+        xw = self._node_gemm(x, M.idx, W).contiguous()
+        z = self._spmm(xw, "src", w1)
+        y = self._spmm(z, "src", w2)
+        n, E, F = self.graph.n_rows, self.graph.nnz, xw.shape[1]
+        for w in (w1, w2):
+            self._count(E * (4 + (4 if w is not None else 0) + 4 * F) + n * (8 + 4 * F))
+        self.values[M.idx] = NodeT(y)
+        return Lazy(lambda: self._gather_value(G2))
+
+    def _eval_mm_first(self, G, M):
+        """Sets M's value to aggregate(x W) and returns G's value lazily; None if the operands
+        do not allow it (head-wise weights, edge-tensor features)."""
+        if G.idx in self.two_hop.values():
+            v = self._eval_two_hop(G, M)
+            if v is not None:
+                return v
+        opnd = self._mm_first_operands(G)
+        if opnd is None:
+            return None
+        x, w, fill = opnd
         W = self.tensors[f"w:{M.idx}"]
         if W.shape[0] != x.shape[1]:
             return None
@@ -975,7 +1203,10 @@ class Executor:
             return v[1].expand(self.n_nodes, v[1].shape[1]).contiguous()
         raise TypeError(f"applynode operand is not a node tensor ({type(v).__name__})")
 
-    def _eval(self, op, block):
+    def _eval(self, op, block, expr=True):
+        if expr and self.edge_expr and op.idx in self.expr_nodes:
+            # a node of a fused expression tree: its gather runs it; computed unfused only if read
+            return Lazy(lambda: _forced(self._eval(op, block, expr=False)))
         fused_into = {p: c for p, c, _ in block.fused}
         if op.type == "scatter":
             src = self.g.inputs[op.idx][0]
@@ -1026,8 +1257,14 @@ class Executor:
         if op.type == "applyedge":
             return self._eval_applyedge(op)
         if op.type == "gather":
+            if self.edge_expr and op.idx in self.expr:
+                v = self._eval_edge_expr(op)
+                if v is not None:
+                    return v
             if self.gather_acc and any(g == op.idx for g, _, _ in self.gacc.values()):
                 return Lazy(lambda: self._gather_value(op))  # its ADD consumer accumulates it
+            if self.mm_first and op.idx in self.two_hop:
+                return Lazy(lambda: self._gather_value(op))  # the second hop's MM-first form runs it
             if self.mm_first and op.idx in self.reorder:
                 v = self._eval_mm_first(op, self.g.ops[self.reorder[op.idx]])
                 if v is not None:

@@ -6,11 +6,13 @@ One function per ISA op / fused pattern of the GTA stream:
   aggregate    fused applyedge MUL -> gather ADD (+ removed scatter FETCH)
                (hardware_info.yaml Inst_fused :35-38, code/interpreter.py:575-636, 764-802) -> gta_aggregate
   apply_edge   applyedge ADD/MUL/SF (genGraphOP.py:36, 55-60)              -> gta_apply_edge
+  aggregate_expr  a tree of applyedge ops -> gather ADD, fused (DGN, PNA)   -> gta_aggregate_expr
   apply_node   applynode ADD/MUL/SF (genGraphOP.py:62, 94-95, 103-108)     -> gta_apply_node
   update_mm    applynode/applyedge MM, `j,ij->i` (ISA_defination.yaml:1-31) -> gta_update_mm
   tile_nnz     calculate_sparsity (code/preprocessing.py:12-40)            -> gta_tile_nnz
 Shapes and strides are validated on the host before any launch.
 """
+import ctypes
 import math
 import threading
 import weakref
@@ -227,6 +229,67 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
     check(_L().gta_aggregate(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz, _MODES[x_mode],
                              _ptr(x), ldx, F, x_dt, _ptr(w), ldw, heads, _ptr(row_scale), _ptr(out), ldy,
                              int(bool(accumulate)), _ptr(pbuf), chunk, _ptr(ws), _stream(x.device)), "aggregate")
+    return out
+
+
+EXPR_SHAPES = {1: 2, 2: 3, 3: 4}  # gta_aggregate_expr shape -> operand count
+
+
+def aggregate_expr(graph, shape, operands, bins, sfs=None, swap=False, plan=None):
+    """y[i] = sum_{e in row i} t(e) with t an apply_edge expression (gta_aggregate_expr, ABI 14):
+      shape 1: t = sf0(L0 bin0 L1)   (bins[0] None: sf0(L0))
+      shape 2: u = sf0(L0 bin0 L1); t = sf1(L2 bin1 u if swap else u bin1 L2)
+      shape 3: u = sf0(L0 bin0 L1); v = sf1(L2 bin1 L3); t = sf2(u bin2 v)
+    operands: [(tensor, mode)] with mode "edge" / "src" / "dst", or "row" (a [1, F] row broadcast to
+    every edge); fp32, F columns each.  Bitwise equal to the apply_edge ops followed by
+    aggregate(..., "edge", plan=plan) of their output.  Returns None when an operand's alignment
+    does not admit that aggregate's vector width (GTA_ERR_UNSUPPORTED: run the ops unfused)."""
+    if shape not in EXPR_SHAPES:
+        raise ValueError(f"aggregate_expr: shape must be 1, 2 or 3 (got {shape})")
+    n_ops = shape
+    bins = list(bins) + [None] * (3 - len(bins))
+    sfs = list(sfs or []) + [None] * (3 - len(sfs or []))
+    n_l = 1 if (shape == 1 and bins[0] is None) else EXPR_SHAPES[shape]
+    if len(operands) != n_l:
+        raise ValueError(f"aggregate_expr: shape {shape} takes {n_l} operands (got {len(operands)})")
+    ts = [t for t, _ in operands]
+    _need_gpu(graph.indptr, *ts)
+    F = ts[0].shape[1]
+    ptrs, modes, lds = (ctypes.c_void_p * 4)(), (ctypes.c_int * 4)(), (ctypes.c_int64 * 4)()
+    for l, (t, m) in enumerate(operands):
+        if t.shape[1] != F:
+            raise ValueError("aggregate_expr: every operand has the same width")
+        ld = _rows(t, f"operand {l}")
+        if m == "row":
+            m, ld = "edge", 0
+            if t.shape[0] < 1:
+                raise ValueError("aggregate_expr: a broadcast row needs one row")
+        else:
+            need = {"edge": graph.nnz, "src": graph.n_cols, "dst": graph.n_rows}[m]
+            if t.shape[0] < need:
+                raise ValueError(f"aggregate_expr operand {l}: {m}-mode operand needs {need} rows")
+        ptrs[l], modes[l], lds[l] = t.data_ptr(), _MODES[m], ld
+    cb = (ctypes.c_int * 3)(*[_BINS[b] for b in bins])
+    cs = (ctypes.c_int * 3)(*[_sf(s) for s in sfs])
+    out = torch.empty(graph.n_rows, F, dtype=torch.float32, device=ts[0].device)
+    if graph.n_rows == 0:
+        return out
+    if isinstance(plan, int):
+        plan = graph.plan(plan)
+        if plan.splits == 0:  # as aggregate: no split row, the per-row form
+            plan = None
+    pbuf = ws = None
+    chunk = 0
+    if plan is not None:
+        if plan.graph is not graph:
+            raise ValueError("plan built for another graph")
+        pbuf, ws, chunk = plan.buf, plan.workspace(F), plan.chunk
+    rc = _L().gta_aggregate_expr(_ptr(graph.indptr), _ptr(graph.indices), graph.n_rows, graph.nnz, n_ops,
+                                 ptrs, modes, lds, cb, cs, int(bool(swap)), F, _ptr(out), F, _ptr(pbuf), chunk,
+                                 _ptr(ws), _stream(ts[0].device))
+    if rc == _lib.ERR_UNSUPPORTED:
+        return None
+    check(rc, "aggregate_expr")
     return out
 
 

@@ -37,7 +37,7 @@
 extern "C" {
 #endif
 
-#define GTA_ABI_VERSION 13 /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
+#define GTA_ABI_VERSION 14 /* 2: blocked plans of bounded items (nnz, item_edges); 3: per-thread tuning
                               hooks; 4: knob sets attached to streams (gta_tuning_*); 5: every UPDATE
                               on hand-written kernels (no vendor library), gta_update_mm_t_splits,
                               the blocked workspace is the slab rows alone and required, bf16
@@ -48,7 +48,8 @@ extern "C" {
                               gta_update_mlp (two chained node GEMMs in one pass); 10: bf16 y of
                               gta_aggregate_self, bf16 x of gta_update_mlp; 11: gta_gather_add takes the ISA
                               DIRECTION (dir R / C) and the CSC view of gta_csc_build; 12:
-                              gta_build_id, gta_synth_alpha and gta_row_ids (scan-free setup); 13: gta_apply_edge_flat */
+                              gta_build_id, gta_synth_alpha and gta_row_ids (scan-free setup); 13: gta_apply_edge_flat;
+                              14: gta_aggregate_expr */
 
 /* status codes */
 enum { GTA_OK = 0, GTA_ERR_ARG = -1, GTA_ERR_HIP = -2, GTA_ERR_UNSUPPORTED = -3 };
@@ -143,6 +144,26 @@ int gta_aggregate(const int64_t* indptr, const int32_t* indices, int64_t n_rows,
                   const float* w, int64_t ldw, int64_t heads,
                   const float* row_scale, float* y, int64_t ldy, int accumulate,
                   const void* plan, int64_t plan_chunk, void* workspace, void* stream);
+
+/* ABI 14: the aggregate of an apply_edge expression -- a gather R whose edge value is a tree of
+ * K3 ops over up to four operand rows, with no [E, F] edge tensor written for any of them:
+ *   shape 1: t = sf0(L0 bin0 L1)                 (bins[0] GTA_BIN_NONE: t = sf0(L0), one operand)
+ *   shape 2: u = sf0(L0 bin0 L1); t = sf1(swap ? L2 bin1 u : u bin1 L2)
+ *   shape 3: u = sf0(L0 bin0 L1); v = sf1(L2 bin1 L3); t = sf2(u bin2 v)
+ *   y[i, :] = sum_{e in row i} t(e, :)
+ * Operand l is operands[l] (fp32, F columns, row stride lds[l]) read per modes[l]: GTA_IDX_EDGE
+ * (row e; lds 0 = one row broadcast to every edge), GTA_IDX_SRC (row indices[e]), GTA_IDX_DST
+ * (row i).  Every step is the gta_apply_edge arithmetic with the intermediate rounded to fp32 as its
+ * stored output would be, and the sum runs in gta_aggregate(x_mode EDGE)'s order with the same
+ * plan: bitwise equal to the apply_edge ops followed by that aggregate of their [E, F] output.
+ * GTA_ERR_UNSUPPORTED when an operand's alignment or stride does not admit the vector width that
+ * aggregate would use for F (then run the ops unfused).  operands / modes / lds / bins / sfs are
+ * host arrays read during the call.  DGN ops 2-8 (the MM of op 3 pushed to the node rows) and PNA
+ * ops 5-8 of the genGraphOP op graphs (restated in frontend.py). */
+int gta_aggregate_expr(const int64_t* indptr, const int32_t* indices, int64_t n_rows, int64_t nnz, int shape,
+                       const float* const* operands, const int* modes, const int64_t* lds, const int* bins,
+                       const int* sfs, int swap, int64_t F, float* y, int64_t ldy, const void* plan,
+                       int64_t plan_chunk, void* workspace, void* stream);
 
 /* ABI 7: the aggregate with a self term, y[i, :] = self_scale[0] * x_self[i, :] + row_scale[i] *
  * sum_{e in row i} w(e) x[idx(e), :] (no accumulate).  x_self has x's dtype and F columns (ld_self

@@ -76,7 +76,9 @@ def main(names=None, reps=5, trace=False, graphed=False):
 if __name__ == "__main__":
     from gta_graph_tensor_acclelrator_for_general_gnn_amd import ops
     argv = [a for a in sys.argv[1:] if a not in ("--trace", "--hipgraph", "--no-mlp", "--graph-all", "--no-bf16-sum",
-                                                 "--no-edge-flat")]
+                                                 "--no-edge-flat", "--no-edge-expr")]
+    if "--no-edge-expr" in sys.argv[1:]:  # the applyedge trees of DGN / PNA unfused (A/B of gta_aggregate_expr, ABI 14)
+        executor.EDGE_EXPR = False
     if "--no-edge-flat" in sys.argv[1:]:  # apply_edge on the row-sweep forms (A/B of gta_apply_edge_flat, ABI 13)
         ops.APPLY_EDGE_FLAT = False
     if "--no-bf16-sum" in sys.argv[1:]:  # GIN's sum handed to the fused MLP in fp32 (A/B of ABI 10)

@@ -46,6 +46,32 @@ def aggregate(graph, x, x_mode="src", w=None, row_scale=None, out=None, accumula
     return _t(y)
 
 
+EXPR_CALLS = [0]  # fused expression gathers (the executor's DGN / PNA edge-expression fusion)
+
+
+def aggregate_expr(graph, shape, operands, bins, sfs=None, swap=False, plan=None):
+    """The oracle's apply_edge steps, then its gather (gta_aggregate_expr's definition)."""
+    EXPR_CALLS[0] += 1
+    ip, ix = graph.numpy()
+    sfs = list(sfs or []) + [None] * 3
+
+    def step(b, sf, x, y):
+        (xa, xm), (ya, ym) = x, (y if y is not None else (None, "edge"))
+        if xm == "row":
+            xa, xm = np.repeat(xa[:1], graph.nnz, axis=0), "edge"
+        return isa_ref.apply_edge(ip, ix, b, sf, xa, xm, ya, "edge" if ym == "row" else ym, ym == "row"), "edge"
+
+    L = [(_np(t), m) for t, m in operands]
+    u = step(bins[0], sfs[0], L[0], L[1] if len(L) > 1 else None)
+    if shape == 1:
+        t = u
+    elif shape == 2:
+        t = step(bins[1], sfs[1], L[2], u) if swap else step(bins[1], sfs[1], u, L[2])
+    else:
+        t = step(bins[2], sfs[2], u, step(bins[1], sfs[1], L[2], L[3]))
+    return _t(isa_ref.aggregate(ip, ix, t[0], "edge", None, None))
+
+
 def gather_add(graph, xe, out=None, accumulate=False, direction="R"):
     if direction == "C":
         ip, ix = graph.numpy()

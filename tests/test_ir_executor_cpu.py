@@ -255,6 +255,76 @@ def test_gather_acc_fusion_cpu(golden_dir, manifest, monkeypatch):
         assert nbytes[True] < nbytes[False]
 
 
+EXPR_SHAPES = {("DGN", False): (3, False, ["ADD", "ADD", "ADD"]), ("DGN", True): (3, False, ["ADD", "ADD", "ADD"]),
+               ("PNA", False): (2, True, ["ADD", "ADD"]), ("PNA", True): (2, True, ["ADD", "ADD"])}
+
+
+@pytest.mark.parametrize("network", ["DGN", "PNA"])
+def test_edge_expr_fusion_cpu(golden_dir, manifest, monkeypatch, network):
+    """DGN's op 2-7 tree (the MM of op 3 pushed to the node rows) and PNA's ops 5-7 run as one
+    expression gather (gta_aggregate_expr): matched with the expected shape, every op of every golden
+    stream (the tree's ops recomputed on demand) equal to the fp64 oracle, no [E, F] tensor of the
+    tree in the algorithmic bytes, and the GAT / GCN / GIN / SGC / GraphSAGE streams left alone."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    recs = [s for s in _streams(manifest) if s["network"] == network]
+    assert recs
+    gc, ip, ix = _cora_graph(golden_dir)
+    for rec in recs:
+        sem = Semantics.for_network(network, rec["reorder"])
+        og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+        st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+        tensors = workloads.make_tensors(og, gc, network, seed=6)
+        ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
+        nbytes = {}
+        for on in (True, False):
+            ex = executor.Executor(og, st, gc, tensors, sem)
+            ex.edge_expr = on
+            (e,) = ex.expr.values()
+            assert (e["shape"], e["swap"], e["bins"]) == EXPR_SHAPES[(network, rec["reorder"])], rec["file"]
+            calls = fake_ops.EXPR_CALLS[0]
+            ex.run()
+            assert fake_ops.EXPR_CALLS[0] == calls + (1 if on else 0), rec["file"]
+            nbytes[on] = ex.alg_bytes
+            compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
+        assert nbytes[True] < nbytes[False], rec["file"]
+    for s in _streams(manifest):
+        if s["network"] in ("DGN", "PNA"):
+            continue
+        sem = Semantics.for_network(s["network"], s["reorder"])
+        og = ir.OpGraph.load(os.path.join(golden_dir, "ops", s["op_yaml"]), sem.inputs)
+        st = ir.Stream.load(os.path.join(golden_dir, "streams", s["file"]))
+        tensors = workloads.make_tensors(og, gc, s["network"], seed=0)
+        assert not executor.Executor(og, st, gc, tensors, sem).expr, s["file"]
+
+
+def test_two_hop_mm_first_cpu(golden_dir, manifest, monkeypatch):
+    """SGC's gather -> scatter C -> MUL -> gather -> MM runs as A (A (x W)): where both weight MULs
+    are fused into their gathers, the first gather's [N, F_in] value is never formed (it stays unforced
+    through the run), the layer output and every op (recomputed on demand) match the fp64 oracle,
+    and fewer algorithmic bytes move than with mm_first off."""
+    monkeypatch.setattr(executor, "ops", fake_ops)
+    recs = [s for s in _streams(manifest) if s["network"] == "SGC"]
+    assert recs
+    gc, ip, ix = _cora_graph(golden_dir)
+    taken = 0
+    for rec in recs:
+        sem = Semantics.for_network("SGC", rec["reorder"])
+        og = ir.OpGraph.load(os.path.join(golden_dir, "ops", rec["op_yaml"]), sem.inputs)
+        st = ir.Stream.load(os.path.join(golden_dir, "streams", rec["file"]))
+        tensors = workloads.make_tensors(og, gc, "SGC", seed=7)
+        ref = execute_ref(og, sem, ip, ix, {k: v.double().numpy() for k, v in tensors.items()})
+        ex = executor.Executor(og, st, gc, tensors, sem)
+        assert ex.two_hop == {2: 5}, rec["file"]
+        ex.run()
+        fused = all(any(pair <= set(b.ops) for b in st.blocks) for pair in ({1, 2}, {4, 5}))  # both MULs deferred
+        first = ex.values[2]
+        if fused:
+            assert isinstance(first, executor.Lazy) and first.v is None, rec["file"]
+            taken += 1
+        compare({i: ex.tensor_of(i) for i in range(len(og))}, ref, range(len(og)))
+    assert taken >= len(recs) // 2
+
+
 def test_gin_bf16_model_input_cpu(golden_dir, manifest, monkeypatch):
     """The bf16 GIN configuration (x stored in bf16: BASELINE.md's 200-B rows, bf16 MLP weights):
     every op of the stream, the gather-accumulate fusion included, equals the fp64 oracle run on
