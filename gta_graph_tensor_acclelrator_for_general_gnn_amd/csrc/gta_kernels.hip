@@ -14,6 +14,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <utility>
 
 #include "../../include/gta.h"
 
@@ -711,6 +712,102 @@ k_agg_lean(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indic
     }
     o.store(yp);
   }
+}
+
+// gta_aggregate_expr for rows that exactly fill a wavefront (F = 128 at 8 B per lane, F = 256 at
+// 16 B: the shapes where k_aggregate's XM_EDGE form, the unfused gather, runs one edge per wave
+// instruction): U edges per step with every operand load of the step issued back to back at
+// addresses hoisted per item (a per-operand base and the index that scales its stride), one
+// expression pass over the step, then the same masked in-order sum as k_aggregate -- bitwise its
+// result.  The generic k_aggregate XM_EX* form spent ~20 scalar instructions selecting each load's
+// row and took 3 steps for a 10-edge row.
+// CM >= 0: the row-constant operands as a compile-time mask (bit l: operand l), so those operands
+// take no registers beside their one copy and no branch in the step; CM = -1: read from ex.
+template <int VW, int XMODE, int CM = -1>
+__global__ void __launch_bounds__(kBlock)
+k_agg_expr(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indices, int64_t n_rows, PlanView plan,
+           int use_plan, int64_t chunk, const ExprArgs ex, float* __restrict__ y, int64_t ldy,
+           float* __restrict__ partial, int F) {
+  constexpr int NL = expr_leaves<XMODE>();
+  // edges per step: the gathered operands' U * VW values each in registers
+  constexpr int NG = CM >= 0 ? NL - __builtin_popcount(CM & ((1 << NL) - 1)) : NL;
+  constexpr int U = VW == 4 ? 4 : (NG <= 1 ? 16 : 8);
+  const int lane = threadIdx.x & (kWave - 1);
+  const int64_t item = static_cast<int64_t>(blockIdx.x) * kWavesPerBlock + wave_id_uniform();
+  const int64_t n_items = use_plan ? plan.hdr[0] : n_rows;
+  if (item >= n_items) return;
+  int64_t row, eb, ee;
+  bool split = false;
+  if (use_plan) {
+    row = plan.item_row[item];
+    eb = plan.item_beg[item];
+    const int64_t rb = indptr[row], re = indptr[row + 1];
+    ee = min(eb + chunk, re);
+    split = (re - rb) > chunk;
+  } else {
+    row = item;
+    eb = indptr[row];
+    ee = indptr[row + 1];
+  }
+  const int col = lane * VW;
+  const float* base[NL];
+  int64_t ld[NL];
+  int kind[NL];  // 0: row indices[e], 1: row e, 2: the item's row (folded into base)
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    const int md = ex_mode(ex.code, l);
+    ld[l] = ex.ld[l];
+    kind[l] = md == GTA_IDX_SRC ? 0 : (md == GTA_IDX_DST ? 2 : 1);
+    base[l] = ex.p[l] + col + (md == GTA_IDX_DST ? row * ld[l] : 0);
+  }
+  float acc[VW];
+#pragma unroll
+  for (int k = 0; k < VW; ++k) acc[k] = 0.f;
+  // row-constant operands (the item's row, a broadcast row): loaded once, not per edge -- each
+  // 64-lane load is 4 line requests at the texture units, as many as a gathered row
+  Vec<VW> cst[NL];
+#pragma unroll
+  for (int l = 0; l < NL; ++l) {
+    if (CM >= 0 ? ((CM >> l) & 1) : (kind[l] == 2 || ld[l] == 0)) {
+      kind[l] = 2;
+      cst[l].load(base[l]);
+    }
+  }
+  int idxv = (eb < ee) ? indices[min(eb + lane, ee - 1)] : 0;
+  for (int64_t e0 = eb; e0 < ee; e0 += kWave) {
+    const int n = static_cast<int>(min<int64_t>(kWave, ee - e0));
+    const int idxn = indices[min(e0 + kWave + lane, ee - 1)];  // prefetch next block (clamped)
+    for (int s = 0; s < n; s += U) {
+      float L[4][U * VW];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int jj = s + u < n ? s + u : n - 1;
+        const int64_t sr = __builtin_amdgcn_readlane(idxv, jj);
+#pragma unroll
+        for (int l = 0; l < NL; ++l) {
+          Vec<VW> q;
+          if (CM >= 0 ? ((CM >> l) & 1) : kind[l] == 2) {
+            q = cst[l];
+          } else {
+            q.load(base[l] + (kind[l] == 0 ? sr : e0 + jj) * ld[l]);
+          }
+#pragma unroll
+          for (int k = 0; k < VW; ++k) L[l][u * VW + k] = q.v[k];
+        }
+      }
+      float t[U * VW];
+      expr_eval<XMODE, U * VW>(ex.code, L, t);
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int k = 0; k < VW; ++k) acc[k] += (s + u < n) ? t[u * VW + k] : 0.f;
+    }
+    idxv = idxn;
+  }
+  Vec<VW> o;
+#pragma unroll
+  for (int k = 0; k < VW; ++k) o.v[k] = acc[k];
+  o.store(split ? partial + item * static_cast<int64_t>(F) + col : y + row * ldy + col);
 }
 
 // Single-launch column-blocked form: one wave per plan item (a bounded part of one
@@ -3816,6 +3913,10 @@ k_row_ids(const int64_t* __restrict__ indptr, int64_t n_rows, int64_t* __restric
 // ---------------------------------------------------------------------------
 // host-side dispatch of the aggregate template family
 // ---------------------------------------------------------------------------
+struct AggArgs;
+template <int VW>
+void launch_expr_cm(int xm, int cm, dim3 grid, dim3 blk, hipStream_t s, const AggArgs& a);
+
 struct AggArgs {
   const int64_t* indptr; const int32_t* indices; int64_t n_rows;
   PlanView plan; int use_plan; int64_t chunk; int x_is_row;
@@ -3834,6 +3935,24 @@ void launch_agg(const AggArgs& a, int64_t n_items_bound, hipStream_t s) {
       a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, a.x_is_row, static_cast<const TX*>(a.x), a.ldx, a.F,
       a.w, a.ldw, a.gsz, a.row_scale, a.y, a.ldy, a.accumulate, a.partial, static_cast<const TX*>(a.xs), a.ldxs,
       a.self_scale, a.y_bf16, a.ex);
+}
+
+template <int VW, int XM, int CM>
+void launch_expr_one(dim3 grid, dim3 blk, hipStream_t s, const AggArgs& a) {
+  k_agg_expr<VW, XM, CM><<<grid, blk, 0, s>>>(a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, a.ex, a.y,
+                                              a.ldy, a.partial, a.F);
+}
+
+template <int VW, int XM, int... CMs>
+void launch_expr_masks(int cm, dim3 grid, dim3 blk, hipStream_t s, const AggArgs& a, std::integer_sequence<int, CMs...>) {
+  ((cm == CMs ? (launch_expr_one<VW, XM, CMs>(grid, blk, s, a), 0) : 0), ...);
+}
+
+template <int VW>
+void launch_expr_cm(int xm, int cm, dim3 grid, dim3 blk, hipStream_t s, const AggArgs& a) {
+  if (xm == XM_EX1) launch_expr_masks<VW, XM_EX1>(cm, grid, blk, s, a, std::make_integer_sequence<int, 4>{});
+  else if (xm == XM_EX2) launch_expr_masks<VW, XM_EX2>(cm, grid, blk, s, a, std::make_integer_sequence<int, 8>{});
+  else launch_expr_masks<VW, XM_EX3>(cm, grid, blk, s, a, std::make_integer_sequence<int, 16>{});
 }
 
 // (non-temporal index/weight loads measured +3 %: plain loads throughout)
@@ -3931,6 +4050,7 @@ struct Tuning {
   int agg_bf16_vw8 = 4;    // k_aggregate over bf16 rows in 16-B pieces (VW = 8) instead of 8-B pieces:
                            // 0 off, 4 / 8 = row loads in flight per lane and step (1 = 4)
   int agg_w1 = 1;          // k_aggregate with one weight per edge: 64 per load, broadcast (WM_EDGE1); 0 = WM_HEAD
+  int expr_lean = 1;       // k_agg_expr for gta_aggregate_expr at F = 128 / 256 (0: k_aggregate's XM_EX* form)
   int seg_phase = 0;       // blocked aggregate: 0 = items + reduce, 1 = items only, 2 = reduce only (bench timing)
   int att_lean = 1;        // k_att_h32 for the fused GAT aggregate at F = 128, 8 heads (0: the generic half-wave form)
   int att_direct = 1;      // k_att_h32: a row's only item writes y itself (1: at B <= 2, 2: always, 0: never)
@@ -3995,6 +4115,7 @@ const Knob* find_knob(const char* key) {
       {"seg_pf", &Tuning::seg_pf, nullptr},
       {"agg_bf16_vw8", &Tuning::agg_bf16_vw8, nullptr},
       {"agg_w1", &Tuning::agg_w1, nullptr},
+      {"expr_lean", &Tuning::expr_lean, nullptr},
       {"seg_phase", &Tuning::seg_phase, nullptr},
       {"att_lean", &Tuning::att_lean, nullptr},
       {"att_direct", &Tuning::att_direct, nullptr},
@@ -4232,6 +4353,26 @@ int aggregate_impl(const int64_t* indptr, const int32_t* indices, int64_t n_rows
       if (gl == 0) GTA_LEAN(1, 0); else if (gl == 4) GTA_LEAN(1, 4); else if (gl == 8) GTA_LEAN(1, 8); else GTA_LEAN(1, 16);
     }
 #undef GTA_LEAN
+    ok = true;
+  }
+  if (!ok && ex && tuning().expr_lean && lpe == kWave && nv == 1 && (vw == 2 || vw == 4)) {
+    const int64_t blocks = (bound + kWavesPerBlock - 1) / kWavesPerBlock;
+    const dim3 grid(static_cast<unsigned>(blocks)), blk(kBlock);
+#define GTA_EXPR(VW_, XM_)                                                                                   \
+  k_agg_expr<VW_, XM_><<<grid, blk, 0, s>>>(a.indptr, a.indices, a.n_rows, a.plan, a.use_plan, a.chunk, a.ex, a.y, \
+                                          a.ldy, a.partial, a.F)
+    if (vw == 2) {  // F = 128 (the genGraphOP layer-1 width): the row-constant operands as a template mask
+      int cm = 0;
+      const int nl = xm == XM_EX1 ? 2 : (xm == XM_EX2 ? 3 : 4);
+      for (int l = 0; l < nl; ++l) {
+        const int md = (a.ex.code >> (2 * l)) & 3;  // ex_mode() (a parameter here shadows its name)
+        if (md == GTA_IDX_DST || (md == GTA_IDX_EDGE && a.ex.ld[l] == 0)) cm |= 1 << l;
+      }
+      launch_expr_cm<2>(xm, cm, grid, blk, s, a);
+    } else {
+      if (xm == XM_EX1) GTA_EXPR(4, XM_EX1); else if (xm == XM_EX2) GTA_EXPR(4, XM_EX2); else GTA_EXPR(4, XM_EX3);
+    }
+#undef GTA_EXPR
     ok = true;
   }
   if (!ok && vw8) ok = dispatch_bf16_vw8(lpe, tuning().agg_bf16_vw8, wm, a, bound, s);

@@ -82,6 +82,16 @@ CASES = [  # (shape, modes, bins, sfs, swap)
 @pytest.mark.parametrize("case", range(len(CASES)))
 @pytest.mark.parametrize("plan", [None, 64])
 def test_aggregate_expr_bitwise_equals_unfused(dev, F, case, plan):
+    """Both forms (k_agg_expr at F = 128 / 256, k_aggregate's XM_EX* form) against the unfused ops."""
+    for lean in (1, 0):
+        ops.set_debug("expr_lean", lean)
+        try:
+            _expr_case(dev, F, case, plan)
+        finally:
+            ops.set_debug("expr_lean", 1)
+
+
+def _expr_case(dev, F, case, plan):
     shape, modes, bins, sfs, swap = CASES[case]
     g, ip, ix = _graph(300, 5000, seed=F + case, heavy_row=700, empty_rows=3, dev=dev)
     rng = np.random.default_rng(F * 7 + case)
