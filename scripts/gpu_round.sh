@@ -55,9 +55,9 @@ for s in $STEPS; do
     tile)
       timeout -k 10 ${T_TILE:-400} python -u scripts/tile_chunks.py ${TILE_ARGS} > gpurun_out/tile_chunks.log 2>&1
       rc=$?; echo "tile rc=$rc"; grep '^{' gpurun_out/tile_chunks.log; stop_if_fatal $rc tile ;;
-    xcd)
-      timeout -k 10 60 ./scripts/xcd_probe > gpurun_out/xcd_probe.log 2>&1
-      rc=$?; echo "xcd rc=$rc"; cat gpurun_out/xcd_probe.log; stop_if_fatal $rc xcd ;;
+    expr)
+      timeout -k 10 ${T_EXPR:-300} python -u scripts/expr_probe.py ${EXPR_ARGS:-128} > gpurun_out/expr_probe.log 2>&1
+      rc=$?; echo "expr rc=$rc"; grep '^{' gpurun_out/expr_probe.log; stop_if_fatal $rc expr ;;
     *) echo "unknown step $s";;
   esac
 done
