@@ -149,8 +149,10 @@ __device__ __forceinline__ int wave_id_uniform() {
 // ---------------------------------------------------------------------------
 // Aggregate plan (row chunks).  Layout inside the caller's plan buffer:
 //   int64 hdr[8]            : n_items, n_split, chunk, max_items, n_rows
-//   int32 item_row[max_items]
+//   int32 item_row[max_items]  : the item's row, bit 31 set when the row is split over several items
 //   int64 item_beg[max_items]
+//   int64 item_end[max_items]  : (begin, end) of the item's edges: an item's bounds in one level of
+//                                loads, no dependent indptr read (short rows: one fewer round trip)
 //   int32 split_row[n_rows], int32 split_first[n_rows], int32 split_cnt[n_rows]
 //   int64 offs[n_rows]      : exclusive scan of chunks per row (scratch)
 // ---------------------------------------------------------------------------
@@ -158,6 +160,7 @@ struct PlanView {
   int64_t* hdr;
   int32_t* item_row;
   int64_t* item_beg;
+  int64_t* item_end;
   int32_t* split_row;
   int32_t* split_first;
   int32_t* split_cnt;
@@ -175,6 +178,7 @@ PlanView plan_view(void* base, int64_t n_rows, int64_t max_items) {
   v.hdr = reinterpret_cast<int64_t*>(p); p += round16(8 * sizeof(int64_t));
   v.item_row = reinterpret_cast<int32_t*>(p); p += round16(max_items * 4);
   v.item_beg = reinterpret_cast<int64_t*>(p); p += round16(max_items * 8);
+  v.item_end = reinterpret_cast<int64_t*>(p); p += round16(max_items * 8);
   v.split_row = reinterpret_cast<int32_t*>(p); p += round16(n_rows * 4);
   v.split_first = reinterpret_cast<int32_t*>(p); p += round16(n_rows * 4);
   v.split_cnt = reinterpret_cast<int32_t*>(p); p += round16(n_rows * 4);
@@ -183,7 +187,7 @@ PlanView plan_view(void* base, int64_t n_rows, int64_t max_items) {
 }
 
 int64_t plan_bytes_for(int64_t n_rows, int64_t max_items) {
-  return round16(8 * 8) + round16(max_items * 4) + round16(max_items * 8) + 3 * round16(n_rows * 4) +
+  return round16(8 * 8) + round16(max_items * 4) + 2 * round16(max_items * 8) + 3 * round16(n_rows * 4) +
          round16((n_rows + 1) * 8);
 }
 
@@ -227,8 +231,9 @@ __global__ void k_plan_fill(const int64_t* __restrict__ indptr, int64_t n_rows, 
   const int64_t b = indptr[r], deg = indptr[r + 1] - b;
   const int64_t nc = chunks_of(deg, chunk), off = v.offs[r];
   for (int64_t j = 0; j < nc; ++j) {
-    v.item_row[off + j] = static_cast<int32_t>(r);
+    v.item_row[off + j] = static_cast<int32_t>(nc > 1 ? (static_cast<uint32_t>(r) | 0x80000000u) : r);
     v.item_beg[off + j] = b + j * chunk;
+    v.item_end[off + j] = min(b + (j + 1) * chunk, b + deg);
   }
   if (nc > 1) {  // compaction order is arbitrary; each split row's sum order is fixed
     unsigned long long s = atomicAdd(reinterpret_cast<unsigned long long*>(&v.hdr[1]), 1ull);
@@ -383,11 +388,11 @@ k_aggregate(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indi
   int64_t row, eb, ee;
   bool split = false;
   if (use_plan) {
-    row = plan.item_row[item];
+    const int32_t ir = plan.item_row[item];
+    row = ir & 0x7fffffff;
     eb = plan.item_beg[item];
-    const int64_t rb = indptr[row], re = indptr[row + 1];
-    ee = min(eb + chunk, re);
-    split = (re - rb) > chunk;
+    ee = plan.item_end[item];
+    split = ir < 0;
   } else {
     row = item;
     eb = indptr[row];
@@ -630,11 +635,11 @@ k_agg_lean(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indic
   int64_t row, eb, ee;
   bool split = false;
   if (use_plan) {
-    row = plan.item_row[item];
+    const int32_t ir = plan.item_row[item];
+    row = ir & 0x7fffffff;
     eb = plan.item_beg[item];
-    const int64_t rb = indptr[row], re = indptr[row + 1];
-    ee = min(eb + chunk, re);
-    split = (re - rb) > chunk;
+    ee = plan.item_end[item];
+    split = ir < 0;
   } else {
     row = item;
     eb = indptr[row];
@@ -739,11 +744,11 @@ k_agg_expr(const int64_t* __restrict__ indptr, const int32_t* __restrict__ indic
   int64_t row, eb, ee;
   bool split = false;
   if (use_plan) {
-    row = plan.item_row[item];
+    const int32_t ir = plan.item_row[item];
+    row = ir & 0x7fffffff;
     eb = plan.item_beg[item];
-    const int64_t rb = indptr[row], re = indptr[row + 1];
-    ee = min(eb + chunk, re);
-    split = (re - rb) > chunk;
+    ee = plan.item_end[item];
+    split = ir < 0;
   } else {
     row = item;
     eb = indptr[row];
